@@ -1,0 +1,43 @@
+# Build: HIP kernels (gfx950) + C ABI -> libfattn.so, the kernel_test harness,
+# and the test-only CPU oracle (oracle/Makefile).  No cmake/ninja needed.
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+PKG     := ggml-cuda-experiments_amd
+LIBDIR  := $(PKG)/lib
+BINDIR  := $(PKG)/bin
+LIB     := $(LIBDIR)/libfattn.so
+HARNESS := $(BINDIR)/kernel_test
+
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
+            -munsafe-fp-atomics -Iinclude
+CSRC := $(wildcard $(PKG)/csrc/*.hip)
+CHDR := $(wildcard $(PKG)/csrc/*.h) include/fattn.h
+
+.PHONY: all lib harness oracle clean asm
+
+all: lib harness oracle
+
+lib: $(LIB)
+
+$(LIB): $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared $(CSRC) -o $@
+
+harness: $(HARNESS)
+
+$(HARNESS): $(PKG)/host/kernel_test.cpp $(LIB) include/fattn.h
+	@mkdir -p $(BINDIR)
+	$(HIPCC) -O2 -std=c++17 -Iinclude $(PKG)/host/kernel_test.cpp -L$(LIBDIR) -lfattn \
+	    -Wl,-rpath,'$$ORIGIN/../lib' -o $@
+
+oracle:
+	$(MAKE) -C oracle
+
+# ISA dump for inspection (not part of the build)
+asm:
+	@mkdir -p build/asm
+	cd build/asm && $(HIPCC) $(HIPFLAGS) -c ../../$(PKG)/csrc/fattn_api.hip -save-temps -o fattn_api.o
+
+clean:
+	rm -rf $(LIBDIR) $(BINDIR) build
+	$(MAKE) -C oracle clean

@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark the hot path: Q8_0-KV flash-decoding attention on MI355X.
+
+Workload (BASELINE.json metric "attn TFLOPS & HBM GB/s per GPU; head_dim=128
+seq=4096 Q8_0 KV", configs[2]): 32 heads, head_dim 128, KV length 4096, one
+query row, Q8_0 K and V in ggml block layout (per-head contiguous), f16 mask
+row, f32 Q / O.  One step = one FLASH_ATTN_EXT call (split-KV kernel + combine)
+over one sequence.  Each step reads a different one of R independent KV caches
+(R * 35.7 MB > the 256 MiB Infinity Cache), so the number is HBM, not cache.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): heads x batch
+shard embarrassingly; every rank decodes its own sequence (weak scaling), the
+data path has no collective, and after the K timed steps the ranks' outputs are
+collected with ONE RCCL all_gather over xGMI (inside the timed region).
+
+Prints ONE JSON line (rank 0).  `value` = whole-job algorithmic bytes / time
+(GB/s); `roofline` prices the dominant kernel (fattn_split_kernel) from HIP
+events around that kernel alone; `cpu_baseline` times the reference's own CPU
+oracle (src/utils.h compiled from /root/reference into oracle/_ref) on a bounded
+sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ggml-cuda-experiments_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_F16_PEAK_TFLOPS = 2500.0
+
+
+def hip_events(n):
+    """Raw hipEvent_t handles (torch's Event exposes no handle; the main kernel's
+    events are recorded by libfattn on the launch stream)."""
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
+    hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+    hip.hipEventSynchronize.argtypes = [C.c_void_p]
+    hip.hipEventDestroy.argtypes = [C.c_void_p]
+    evs = []
+    for _ in range(n):
+        e = C.c_void_p()
+        assert hip.hipEventCreate(C.byref(e)) == 0
+        evs.append(e.value)
+    return hip, evs
+
+
+def cpu_baseline(seconds: float, threads: int):
+    """The reference's CPU oracle (kernel_test.h:50-62 calling src/utils.h, built
+    from /root/reference into oracle/_ref) on the config-3 shape with the Q8_0
+    K/V dequantised to f32 beforehand (dequant not timed).  Repeats the whole
+    32-head problem until `seconds` elapse (at least once)."""
+    import numpy as np
+    from oracle import oracle as orc
+    D, H, Hkv, N = 128, 32, 32, 4096
+    kind = "reference" if orc.ref_available() else "port"
+    orc.srand(1)
+    q, k, v, m = (orc.random(n) for n in (D * H, D * N * Hkv, D * N * Hkv, N))
+    kq = orc.dequantize(orc.quantize(k.reshape(-1, D), orc.TYPE_Q8_0), orc.TYPE_Q8_0, D).reshape(-1)
+    vq = orc.dequantize(orc.quantize(v.reshape(-1, D), orc.TYPE_Q8_0), orc.TYPE_Q8_0, D).reshape(-1)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        orc.kernel_test_cpu(q, kq, vq, m, N, D, H, Hkv, impl="ref" if kind == "reference" else "oracle",
+                            n_threads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    bytes_per = (D * H * 4) * 2 + 2 * Hkv * N * (D // 32 * 34) + N * 2
+    return {"value": round(bytes_per * reps / el / 1e9, 4), "unit": "GB/s", "cores": threads if kind == "reference" else 1,
+            "kind": kind,
+            "sample": f"{reps} x full config-3 problem (32 heads x 4096 x 128, Q8_0 K/V dequantised untimed), "
+                      f"{el:.1f} s, heads split over {threads} threads, reference src/utils.h loops",
+            "ms_per_problem": round(el / reps * 1e3, 2), "host_cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--rotate", type=int, default=16, help="independent KV caches cycled through")
+    ap.add_argument("--kv-type", default="q8_0", choices=["q8_0", "q4_0", "f16"])
+    ap.add_argument("--heads", type=int, default=32)
+    ap.add_argument("--kv-heads", type=int, default=0)
+    ap.add_argument("--kv-len", type=int, default=4096)
+    ap.add_argument("--n-q", type=int, default=1)
+    ap.add_argument("--head-dim", type=int, default=128)
+    ap.add_argument("--layout", default="head", choices=["head", "pos"])
+    ap.add_argument("--kv-chunk", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import fattn
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    D, H, N, NQ = args.head_dim, args.heads, args.kv_len, args.n_q
+    Hkv = args.kv_heads or H
+    typ = fattn.TYPE_NAMES[args.kv_type]
+    rb = fattn.row_size(typ, D)
+    R = args.rotate
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+
+    # --- synthetic inputs, resident in HBM before timing
+    kv_sets = []
+    for r in range(R):
+        pair = []
+        for _ in range(2):
+            x = torch.rand((Hkv * N, D), generator=g, device=dev, dtype=torch.float32) * 2 - 1
+            if typ == fattn.TYPE_F16:
+                pair.append(x.to(torch.float16).view(torch.uint8).reshape(-1))
+            else:
+                pair.append(fattn.quantize(x, typ).reshape(-1))
+            del x
+        kv_sets.append(pair)
+    q = torch.rand((1, NQ, H, D), generator=g, device=dev) * 2 - 1
+    npad = (N + 63) // 64 * 64
+    mask = (torch.rand((NQ, npad), generator=g, device=dev) * 2 - 1).to(torch.float16)
+    steps_out = torch.empty((args.steps, 1, NQ, H, D), dtype=torch.float32, device=dev)
+    warm_out = torch.empty((1, NQ, H, D), dtype=torch.float32, device=dev)
+
+    att = fattn.Attention(fattn.q_view(q), fattn.kv_view(kv_sets[0][0], typ, D, N, Hkv, layout=args.layout),
+                          fattn.kv_view(kv_sets[0][1], typ, D, N, Hkv, layout=args.layout),
+                          fattn.mask_view(mask), warm_out, 1.0 / D ** 0.5, kv_chunk=args.kv_chunk)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    hip, evs = hip_events(2 * args.steps)
+
+    def step(i, out, ev=None):
+        kvs = kv_sets[i % R]
+        att.retarget(k=kvs[0].data_ptr(), v=kvs[1].data_ptr(), dst=out.data_ptr())
+        if ev is None:
+            att(stream)
+        else:
+            att(stream, evs[2 * ev], evs[2 * ev + 1])
+
+    for i in range(args.warmup):
+        step(i, warm_out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    gathered = torch.empty((world,) + tuple(steps_out.shape), dtype=torch.float32, device=dev) if world > 1 else None
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, steps_out[i], ev=i)
+    if world > 1:
+        dist.all_gather_into_tensor(gathered, steps_out)   # the single RCCL gather over xGMI
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    # dominant-kernel duration from the HIP events around each main-kernel launch
+    f = C.c_float()
+    kms = []
+    for i in range(args.steps):
+        hip.hipEventElapsedTime(C.byref(f), evs[2 * i], evs[2 * i + 1])
+        kms.append(f.value)
+    kms.sort()
+    kern_ms_avg = sum(kms) / len(kms)
+
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms_avg], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_avg = float(t[0]), float(t[1])
+
+    bytes_step = (NQ * H * D * 4) * 2 + 2 * Hkv * N * rb + NQ * N * 2
+    flops_step = 4 * NQ * N * D * H
+    total_bytes = bytes_step * args.steps * world
+    value = total_bytes / elapsed / 1e9
+    achieved = bytes_step / (kern_ms_avg * 1e-3) / 1e9
+
+    if rank == 0:
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic_r01.json")
+        if os.path.exists(tf):
+            try:
+                tj = json.load(open(tf))
+                if tj.get("workload") == f"decode_{args.kv_type}_h{H}_hkv{Hkv}_d{D}_n{N}_q{NQ}":
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        res = {
+            "metric": "attn TFLOPS & HBM GB/s per GPU; head_dim=128 seq=4096 Q8_0 KV",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f16",
+            "data": "synthetic (uniform [-1,1) Q/K/V, K/V quantised on device to ggml blocks; random f16 mask)",
+            "config": {"workload": f"decode_{args.kv_type}_h{H}_hkv{Hkv}_d{D}_n{N}_q{NQ}", "heads": H,
+                       "kv_heads": Hkv, "head_dim": D, "kv_len": N, "n_q": NQ, "kv_type": args.kv_type,
+                       "kv_layout": args.layout, "kv_rotation": R, "parallelism": f"heads_x_batch_shard{world}",
+                       "bytes_per_step": bytes_step, "flops_per_step": flops_step},
+            "tflops": round(flops_step * args.steps * world / elapsed / 1e12, 4),
+            "kernel_ms_avg": round(kern_ms_avg, 5),
+            "kernel_ms_median": round(kms[len(kms) // 2], 5),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "fattn_split_kernel<Q8_0,Q8_0,128,16,mask>"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, min(args.cpu_threads, os.cpu_count() or 1))
+        print(json.dumps(res), flush=True)
+    for e in evs:
+        hip.hipEventDestroy(e)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

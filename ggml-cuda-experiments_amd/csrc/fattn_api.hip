@@ -1,0 +1,337 @@
+// fattn_api.hip -- C-ABI entry points (include/fattn.h) and host-side dispatch.
+//
+// The reference launches its kernels inline from host code with hard-coded
+// template parameters (src/kernel_test.h:157-199, src/flash-matrix.cu:179-255).
+// Here the host side validates the ggml views, picks the instantiation
+// (head dim x K type x V type x addressing granule), sizes the split-KV grid
+// for 256 CUs, and launches on the caller's stream.  Nothing allocates;
+// nothing synchronises (graph-capturable).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "fattn_quant.h"
+#include "fattn_split.h"
+
+using namespace fattn;
+
+namespace {
+
+constexpr int kCUs = 256;
+
+inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
+inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
+
+struct Plan {
+    SplitArgs a;
+    int kt, vt;  // vt may be VT_F16T
+    int D;
+    int gran;
+    dim3 grid;
+    size_t ws_bytes;
+};
+
+// Validate and build the launch plan.  Returns FATTN_OK or an error.
+int make_plan(const fattn_params* p, Plan& pl) {
+    if (!p || !p->q.data || !p->k.data || !p->v.data || !p->dst) return FATTN_ERR_INVALID_ARG;
+    const fattn_tensor &q = p->q, &k = p->k, &v = p->v, &mk = p->mask;
+    if (q.type != FATTN_TYPE_F32 || q.nb[0] != 4) return FATTN_ERR_UNSUPPORTED_TYPE;
+    const int64_t D = q.ne[0];
+    if (D != 64 && D != 128) return FATTN_ERR_UNSUPPORTED_HEAD_DIM;
+    if (k.ne[0] != D || v.ne[0] != D) return FATTN_ERR_INVALID_ARG;
+    const int64_t NQ = q.ne[1], H = q.ne[2], S = q.ne[3];
+    const int64_t N = k.ne[1], Hkv = k.ne[2], Skv = k.ne[3];
+    if (NQ <= 0 || H <= 0 || S <= 0 || N <= 0 || Hkv <= 0 || Skv <= 0) return FATTN_ERR_INVALID_ARG;
+    if (v.ne[1] != N || v.ne[2] != Hkv || v.ne[3] != Skv) return FATTN_ERR_INVALID_ARG;
+    if (H % Hkv || S % Skv) return FATTN_ERR_INVALID_ARG;
+    if (N > (int64_t)1 << 30 || NQ * H * S > (int64_t)1 << 31) return FATTN_ERR_INVALID_ARG;
+    if (k.type != FATTN_TYPE_F16 && !is_quant(k.type)) return FATTN_ERR_UNSUPPORTED_TYPE;
+    if (v.type != FATTN_TYPE_F16 && !is_quant(v.type)) return FATTN_ERR_UNSUPPORTED_TYPE;
+    if (k.type != v.type) return FATTN_ERR_UNSUPPORTED_TYPE;  // mixed K/V types: not instantiated
+    if ((uintptr_t)q.data % 16 || q.nb[1] % 16 || q.nb[2] % 16 || q.nb[3] % 16) return FATTN_ERR_ALIGNMENT;
+
+    const size_t rowK = fattn_row_size(k.type, D), rowV = fattn_row_size(v.type, D);
+    // K rows must be contiguous (nb[0] = element size / block granular)
+    if (k.type == FATTN_TYPE_F16 && k.nb[0] != 2) return FATTN_ERR_BAD_STRIDE;
+    if (is_quant(k.type) && k.nb[0] != (int64_t)fattn_row_size(k.type, 32)) return FATTN_ERR_BAD_STRIDE;
+    bool v_trans = false;
+    if (v.type == FATTN_TYPE_F16 && v.nb[0] != 2) {
+        if (v.nb[1] != 2) return FATTN_ERR_BAD_STRIDE;
+        v_trans = true;
+        if (N % kStep || v.nb[0] % 16 || (uintptr_t)v.data % 16) return FATTN_ERR_BAD_STRIDE;
+    }
+    if (is_quant(v.type) && v.nb[0] != (int64_t)fattn_row_size(v.type, 32)) return FATTN_ERR_BAD_STRIDE;
+    if (k.nb[1] % 4 || k.nb[2] % 4 || k.nb[3] % 4 || (uintptr_t)k.data % 4) return FATTN_ERR_ALIGNMENT;
+    if (v.nb[1] % 2 || v.nb[2] % 4 || v.nb[3] % 4 || (uintptr_t)v.data % 4) return FATTN_ERR_ALIGNMENT;
+    if (!v_trans && v.nb[1] % 4) return FATTN_ERR_ALIGNMENT;
+
+    const bool has_mask = mk.data != nullptr;
+    if (has_mask) {
+        if (mk.type != FATTN_TYPE_F16 || mk.ne[0] < N || mk.ne[1] < NQ) return FATTN_ERR_INVALID_ARG;
+        if ((uintptr_t)mk.data % 2 || mk.nb[1] % 2) return FATTN_ERR_ALIGNMENT;
+    }
+
+    // fast path: 16-B pieces
+    bool g16 = true;
+    if (is_quant(k.type)) {
+        g16 = g16 && k.nb[1] == (int64_t)rowK && N % kStep == 0 && (uintptr_t)k.data % 16 == 0 && k.nb[2] % 16 == 0 &&
+              k.nb[3] % 16 == 0;
+        g16 = g16 && v.nb[1] == (int64_t)rowV && (uintptr_t)v.data % 16 == 0 && v.nb[2] % 16 == 0 && v.nb[3] % 16 == 0;
+    } else {
+        g16 = g16 && (uintptr_t)k.data % 16 == 0 && k.nb[1] % 16 == 0 && k.nb[2] % 16 == 0 && k.nb[3] % 16 == 0;
+        if (!v_trans)
+            g16 = g16 && (uintptr_t)v.data % 16 == 0 && v.nb[1] % 16 == 0 && v.nb[2] % 16 == 0 && v.nb[3] % 16 == 0;
+        else
+            g16 = g16 && v.nb[2] % 16 == 0 && v.nb[3] % 16 == 0;
+    }
+    if (has_mask) g16 = g16 && (uintptr_t)mk.data % 16 == 0 && mk.nb[1] % 16 == 0 && N % kStep == 0;
+    if (!g16 && v_trans) return FATTN_ERR_BAD_STRIDE;
+
+    SplitArgs& a = pl.a;
+    std::memset(&a, 0, sizeof(a));
+    a.q = (const uint8_t*)q.data;
+    a.k = (const uint8_t*)k.data;
+    a.v = (const uint8_t*)v.data;
+    a.mask = (const uint8_t*)mk.data;
+    a.dst = p->dst;
+    a.q_nb1 = q.nb[1]; a.q_nb2 = q.nb[2]; a.q_nb3 = q.nb[3];
+    a.k_nb1 = k.nb[1]; a.k_nb2 = k.nb[2]; a.k_nb3 = k.nb[3];
+    a.v_nb0 = v.nb[0]; a.v_nb1 = v.nb[1]; a.v_nb2 = v.nb[2]; a.v_nb3 = v.nb[3];
+    a.m_nb1 = has_mask ? mk.nb[1] : 0;
+    a.NQ = (int)NQ; a.H = (int)H; a.S = (int)S; a.N = (int)N;
+    a.rk2 = (int)(H / Hkv);
+    a.rk3 = (int)(S / Skv);
+    a.R = std::min(a.rk2, kRows);
+    a.QPT = kRows / a.R;
+    a.n_hsub = (a.rk2 + a.R - 1) / a.R;
+    a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
+    a.has_mask = has_mask ? 1 : 0;
+    a.scale_log2 = p->scale * 1.4426950408889634f;
+
+    const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
+    if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
+    // split-KV sizing: ~2 workgroups per CU; chunk a multiple of 4 waves x 32
+    const int quantum = kStep * kSplitWaves;
+    int chunk_len;
+    if (p->kv_chunk > 0) {
+        chunk_len = (p->kv_chunk + quantum - 1) / quantum * quantum;
+    } else {
+        const int64_t target = 2 * kCUs;
+        int64_t nch = std::max<int64_t>(1, (target + Y * S - 1) / (Y * S));
+        chunk_len = (int)((N + nch - 1) / nch);
+        chunk_len = (chunk_len + quantum - 1) / quantum * quantum;
+    }
+    a.chunk_len = chunk_len;
+    a.n_chunks = (int)((N + chunk_len - 1) / chunk_len);
+    pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
+    pl.ws_bytes = a.n_chunks > 1 ? (size_t)S * Y * a.n_chunks * kRows * (D + 2) * sizeof(float) : 0;
+    pl.kt = k.type;
+    pl.vt = v_trans ? VT_F16T : v.type;
+    pl.D = (int)D;
+    pl.gran = g16 ? 16 : 4;
+    return FATTN_OK;
+}
+
+struct Events {
+    hipEvent_t begin = nullptr, end = nullptr;
+};
+
+template <int KT, int VT, int D, int GRAN, bool HM>
+int launch_split_hm(const Plan& pl, hipStream_t st, const Events& ev) {
+    using C = SplitCfg<KT, VT, D>;
+    auto kern = fattn_split_kernel<KT, VT, D, GRAN, HM>;
+    static bool attr_set = false;  // idempotent; benign race
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::ldsBytes);
+        attr_set = true;
+    }
+    if (ev.begin) (void)hipEventRecord(ev.begin, st);
+    hipLaunchKernelGGL(kern, pl.grid, dim3(kSplitWaves * kWave), C::ldsBytes, st, pl.a);
+    if (hipGetLastError() != hipSuccess) return FATTN_ERR_LAUNCH;
+    if (ev.end) (void)hipEventRecord(ev.end, st);
+    if (pl.a.n_chunks > 1) {
+        hipLaunchKernelGGL(fattn_combine_kernel<D>, dim3(pl.grid.y, pl.grid.z), dim3(256), 0, st, pl.a);
+        if (hipGetLastError() != hipSuccess) return FATTN_ERR_LAUNCH;
+    }
+    return FATTN_OK;
+}
+
+template <int KT, int VT, int D, int GRAN>
+int launch_split(const Plan& pl, hipStream_t st, const Events& ev) {
+    return pl.a.has_mask ? launch_split_hm<KT, VT, D, GRAN, true>(pl, st, ev)
+                         : launch_split_hm<KT, VT, D, GRAN, false>(pl, st, ev);
+}
+
+template <int KT, int VT, int D>
+int launch_gran(const Plan& pl, hipStream_t st, const Events& ev) {
+    if constexpr (VT == VT_F16T) {
+        return launch_split<KT, VT, D, 16>(pl, st, ev);
+    } else {
+        return pl.gran == 16 ? launch_split<KT, VT, D, 16>(pl, st, ev) : launch_split<KT, VT, D, 4>(pl, st, ev);
+    }
+}
+
+template <int D>
+int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
+    if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_gran<FATTN_TYPE_Q8_0, FATTN_TYPE_Q8_0, D>(pl, st, ev);
+    if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_gran<FATTN_TYPE_Q4_0, FATTN_TYPE_Q4_0, D>(pl, st, ev);
+    if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_gran<FATTN_TYPE_F16, FATTN_TYPE_F16, D>(pl, st, ev);
+    if (pl.kt == FATTN_TYPE_F16 && pl.vt == VT_F16T) return launch_gran<FATTN_TYPE_F16, VT_F16T, D>(pl, st, ev);
+    return FATTN_ERR_UNSUPPORTED_TYPE;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fattn_version(void) { return "fattn-gfx950 0.1"; }
+
+const char* fattn_strerror(int s) {
+    switch (s) {
+        case FATTN_OK: return "ok";
+        case FATTN_ERR_INVALID_ARG: return "invalid argument";
+        case FATTN_ERR_UNSUPPORTED_TYPE: return "unsupported tensor type";
+        case FATTN_ERR_UNSUPPORTED_HEAD_DIM: return "unsupported head dim (64, 128)";
+        case FATTN_ERR_BAD_STRIDE: return "unsupported strides / layout";
+        case FATTN_ERR_WORKSPACE: return "workspace too small";
+        case FATTN_ERR_LAUNCH: return "HIP launch failed";
+        case FATTN_ERR_ALIGNMENT: return "misaligned pointer or stride";
+        default: return "unknown error";
+    }
+}
+
+size_t fattn_row_size(int type, int64_t k) {
+    switch (type) {
+        case FATTN_TYPE_F32: return (size_t)k * 4;
+        case FATTN_TYPE_F16: return (size_t)k * 2;
+        case FATTN_TYPE_Q8_0: return k % QK ? 0 : (size_t)(k / QK) * kQ8Bytes;
+        case FATTN_TYPE_Q4_0: return k % QK ? 0 : (size_t)(k / QK) * kQ4Bytes;
+        default: return 0;
+    }
+}
+
+size_t fattn_workspace_size(const fattn_params* p) {
+    Plan pl;
+    if (make_plan(p, pl) != FATTN_OK) return 0;
+    return pl.ws_bytes;
+}
+
+int fattn_ext(const fattn_params* p, void* stream) { return fattn_ext_events(p, stream, nullptr, nullptr); }
+
+int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* ev_end) {
+    Plan pl;
+    const int rc = make_plan(p, pl);
+    if (rc != FATTN_OK) return rc;
+    if (pl.ws_bytes) {
+        if (!p->workspace || p->workspace_bytes < pl.ws_bytes || (uintptr_t)p->workspace % 16) return FATTN_ERR_WORKSPACE;
+        pl.a.ws_o = (float*)p->workspace;
+        pl.a.ws_ml = (float*)((uint8_t*)p->workspace + (size_t)pl.grid.z * pl.grid.y * pl.a.n_chunks * kRows * pl.D * 4);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    Events ev;
+    ev.begin = (hipEvent_t)ev_begin;
+    ev.end = (hipEvent_t)ev_end;
+    return pl.D == 128 ? launch_types<128>(pl, st, ev) : launch_types<64>(pl, st, ev);
+}
+
+int fattn_ext_f16_launch(const void* q, const void* k, const void* v, const void* mask, float* dst, float scale,
+                         int ne00, int ne01, int ne02, int ne03, int ne10, int ne11, int ne12, int ne13, int ne31,
+                         int nb31, int nb01, int nb02, int nb03, int nb11, int nb12, int nb13, int ne0, int ne1,
+                         int ne2, int ne3, int k_type, int v_type, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+    // flash-llama.h:120-125: V shares K's shape and strides.
+    (void)ne0; (void)ne1; (void)ne2; (void)ne3;
+    fattn_params p;
+    std::memset(&p, 0, sizeof(p));
+    p.q = {q, FATTN_TYPE_F32, 0, {ne00, ne01, ne02, ne03}, {4, nb01, nb02, nb03}};
+    const int64_t kb0 = k_type == FATTN_TYPE_F16 ? 2 : (int64_t)fattn_row_size(k_type, 32);
+    const int64_t vb0 = v_type == FATTN_TYPE_F16 ? 2 : (int64_t)fattn_row_size(v_type, 32);
+    p.k = {k, k_type, 0, {ne10, ne11, ne12, ne13}, {kb0, nb11, nb12, nb13}};
+    p.v = {v, v_type, 0, {ne10, ne11, ne12, ne13}, {vb0, nb11, nb12, nb13}};
+    if (mask) p.mask = {mask, FATTN_TYPE_F16, 0, {ne11, ne31, 1, 1}, {2, nb31, (int64_t)nb31 * ne31, (int64_t)nb31 * ne31}};
+    p.dst = dst;
+    p.scale = scale;
+    p.workspace = workspace;
+    p.workspace_bytes = workspace_bytes;
+    return fattn_ext(&p, stream);
+}
+
+static void fill_row_params(fattn_params& p, const float* query, const void* key, const void* value, const void* mask,
+                            float* qkv, int head_dim, int kv_size, int num_heads, float scale, int head_stride,
+                            int r_kv_heads) {
+    std::memset(&p, 0, sizeof(p));
+    const int64_t D = head_dim, N = kv_size, H = num_heads, Hkv = num_heads / r_kv_heads;
+    p.q = {query, FATTN_TYPE_F32, 0, {D, 1, H, 1}, {4, D * H * 4, D * 4, D * H * 4}};
+    // key [Hkv][N][D] f16 (flash_row_float.h:19,58): kv head offset head_stride elements
+    p.k = {key, FATTN_TYPE_F16, 0, {D, N, Hkv, 1}, {2, D * 2, (int64_t)head_stride * 2, (int64_t)head_stride * 2 * Hkv}};
+    // value f16 transposed [Hkv][D][N] (flash_row_float.h:177)
+    p.v = {value, FATTN_TYPE_F16, 0, {D, N, Hkv, 1}, {N * 2, 2, (int64_t)head_stride * 2, (int64_t)head_stride * 2 * Hkv}};
+    if (mask) p.mask = {mask, FATTN_TYPE_F16, 0, {N, 1, 1, 1}, {2, N * 2, N * 2, N * 2}};
+    p.dst = qkv;  // [1][H][D] == qkv[h*D + d] (flash_row_float.h:469)
+    p.scale = scale;
+}
+
+size_t fattn_row_workspace_size(int head_dim, int kv_size, int num_heads) {
+    fattn_params p;
+    static const float dummy_f[4] = {0, 0, 0, 0};
+    fill_row_params(p, dummy_f, dummy_f, dummy_f, nullptr, (float*)dummy_f, head_dim, kv_size, num_heads,
+                    1.0f, head_dim * kv_size, 1);
+    Plan pl;
+    p.q.data = (const void*)(uintptr_t)16;  // alignment-only placeholders
+    p.k.data = p.v.data = (const void*)(uintptr_t)16;
+    if (make_plan(&p, pl) != FATTN_OK) return 0;
+    return pl.ws_bytes;
+}
+
+int fattn_row(const float* query, const void* key, const void* value, const void* mask, void* tmp, size_t tmp_bytes,
+              float* qkv, int head_dim, int kv_size, int num_heads, float scale, int head_stride, int r_kv_heads,
+              void* stream) {
+    if (r_kv_heads <= 0 || num_heads % r_kv_heads) return FATTN_ERR_INVALID_ARG;
+    fattn_params p;
+    fill_row_params(p, query, key, value, mask, qkv, head_dim, kv_size, num_heads, scale, head_stride, r_kv_heads);
+    p.workspace = tmp;
+    p.workspace_bytes = tmp_bytes;
+    return fattn_ext(&p, stream);
+}
+
+int fattn_dequantize(int type, const void* src, float* dst, int64_t k, int64_t n_rows, void* stream) {
+    if (!src || !dst || k <= 0 || n_rows <= 0) return FATTN_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t n = k * n_rows;
+    if (type == FATTN_TYPE_F16) {
+        hipLaunchKernelGGL(dequant_f16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           (const uint16_t*)src, dst, n);
+    } else if (type == FATTN_TYPE_Q8_0 || type == FATTN_TYPE_Q4_0) {
+        if (k % QK) return FATTN_ERR_INVALID_ARG;
+        const int64_t nb = n / QK;
+        if (type == FATTN_TYPE_Q8_0)
+            hipLaunchKernelGGL(dequant_q8_0_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st,
+                               (const uint8_t*)src, dst, nb);
+        else
+            hipLaunchKernelGGL(dequant_q4_0_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st,
+                               (const uint8_t*)src, dst, nb);
+    } else {
+        return FATTN_ERR_UNSUPPORTED_TYPE;
+    }
+    return hipGetLastError() == hipSuccess ? FATTN_OK : FATTN_ERR_LAUNCH;
+}
+
+int fattn_quantize(int type, const float* src, void* dst, int64_t k, int64_t n_rows, void* stream) {
+    if (!src || !dst || k <= 0 || n_rows <= 0) return FATTN_ERR_INVALID_ARG;
+    if (k % QK) return FATTN_ERR_INVALID_ARG;
+    if ((uintptr_t)src % 16) return FATTN_ERR_ALIGNMENT;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t nb = k * n_rows / QK;
+    if (type == FATTN_TYPE_Q8_0)
+        hipLaunchKernelGGL(quant_q8_0_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, src,
+                           (uint8_t*)dst, nb);
+    else if (type == FATTN_TYPE_Q4_0)
+        hipLaunchKernelGGL(quant_q4_0_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, src,
+                           (uint8_t*)dst, nb);
+    else
+        return FATTN_ERR_UNSUPPORTED_TYPE;
+    return hipGetLastError() == hipSuccess ? FATTN_OK : FATTN_ERR_LAUNCH;
+}
+
+}  // extern "C"

@@ -1,0 +1,150 @@
+// fattn_common.h -- shared device helpers for the gfx950 attention kernels.
+//
+// Replaces src/tensor-mma.h (WMMA 16x16x16 fragments, WARP_SIZE 32) and the
+// warp_reduce_* butterflies of src/cuda_info.h:46-85 with CDNA4 primitives:
+// wave64 shuffles and __builtin_amdgcn_mfma_f32_16x16x32_f16.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fattn.h"
+
+namespace fattn {
+
+constexpr int kWave = 64;
+
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+// ggml block geometry
+constexpr int QK = 32;
+constexpr int kQ8Bytes = 34;  // {f16 d; int8 qs[32]}
+constexpr int kQ4Bytes = 18;  // {f16 d; uint8 qs[16]}
+
+template <int T>
+struct TypeInfo;
+template <>
+struct TypeInfo<FATTN_TYPE_F16> {
+    static constexpr int block_elems = 1;
+    static constexpr int block_bytes = 2;
+};
+template <>
+struct TypeInfo<FATTN_TYPE_Q8_0> {
+    static constexpr int block_elems = QK;
+    static constexpr int block_bytes = kQ8Bytes;
+};
+template <>
+struct TypeInfo<FATTN_TYPE_Q4_0> {
+    static constexpr int block_elems = QK;
+    static constexpr int block_bytes = kQ4Bytes;
+};
+
+template <int T, int D>
+constexpr int row_bytes() {
+    return D / TypeInfo<T>::block_elems * TypeInfo<T>::block_bytes;
+}
+
+// ---------------------------------------------------------------- bit helpers
+
+__device__ __forceinline__ uint32_t perm_b32(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t shift) {
+    return __builtin_amdgcn_alignbyte(hi, lo, shift);
+}
+__device__ __forceinline__ f16x2 as_h2(uint32_t x) { return __builtin_bit_cast(f16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(f16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// f16 pair with both halves = the f16 whose bits are the low 16 bits of x
+__device__ __forceinline__ f16x2 bcast_h(uint32_t bits16) {
+    const uint32_t b = bits16 & 0xffffu;
+    return as_h2(b | (b << 16));
+}
+
+// Four int8 (two's complement, packed in a dword) -> two f16 pairs holding the
+// exact integer values.  Magic-number trick: f16 bits 0x64uu = 1024 + uu, so
+// with uu = q ^ 0x80 = q + 128 the value is 1152 + q; subtracting 1152 is exact.
+__device__ __forceinline__ void i8x4_to_h2x2(uint32_t w, f16x2& lo, f16x2& hi) {
+    const uint32_t t = w ^ 0x80808080u;
+    const uint32_t p0 = perm_b32(0x64646464u, t, 0x04010400u);  // bytes: t0,0x64,t1,0x64
+    const uint32_t p1 = perm_b32(0x64646464u, t, 0x04030402u);  // bytes: t2,0x64,t3,0x64
+    const f16x2 off = {(f16)-1152.0f, (f16)-1152.0f};
+    lo = as_h2(p0) + off;
+    hi = as_h2(p1) + off;
+}
+
+// Four nibbles already isolated in the low 4 bits of each byte of w ->
+// two f16 pairs holding (nib - 8) exactly (Q4_0 offset).
+__device__ __forceinline__ void u4x4_to_h2x2(uint32_t w, f16x2& lo, f16x2& hi) {
+    const uint32_t p0 = perm_b32(0x64646464u, w, 0x04010400u);
+    const uint32_t p1 = perm_b32(0x64646464u, w, 0x04030402u);
+    const f16x2 off = {(f16)-1032.0f, (f16)-1032.0f};
+    lo = as_h2(p0) + off;
+    hi = as_h2(p1) + off;
+}
+
+// ---------------------------------------------------------------- LDS reads
+// The ggml block rows sit in LDS exactly as in HBM, so a block's qs bytes are
+// only 2-byte aligned.  read8_at<MOD8>() returns the 8 bytes at `off` where
+// off % 8 == MOD8 is known at compile time.
+
+template <int MOD8>
+__device__ __forceinline__ u32x2 read8_at(const uint8_t* smem, uint32_t off) {
+    u32x2 r;
+    if constexpr (MOD8 == 0) {
+        r = *(const u32x2*)(smem + off);
+    } else if constexpr (MOD8 == 4) {
+        r.x = *(const uint32_t*)(smem + off);
+        r.y = *(const uint32_t*)(smem + off + 4);
+    } else if constexpr (MOD8 == 2) {
+        const u32x2 w01 = *(const u32x2*)(smem + off - 2);
+        const uint32_t w2 = *(const uint32_t*)(smem + off + 6);
+        r.x = alignbyte(w01.y, w01.x, 2);
+        r.y = alignbyte(w2, w01.y, 2);
+    } else {  // 6
+        const uint32_t w0 = *(const uint32_t*)(smem + off - 2);
+        const u32x2 w12 = *(const u32x2*)(smem + off + 2);
+        r.x = alignbyte(w12.x, w0, 2);
+        r.y = alignbyte(w12.y, w12.x, 2);
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------- wave reductions
+// wave64 replacements for warp_reduce_max / warp_reduce_sum (cuda_info.h:46-85).
+// Attention only needs the 4 lanes {l, l^16, l^32, l^48} that share one MFMA
+// column, so these reduce over that group.
+__device__ __forceinline__ float grp4_max(float x) {
+    x = fmaxf(x, __shfl_xor(x, 16, kWave));
+    x = fmaxf(x, __shfl_xor(x, 32, kWave));
+    return x;
+}
+__device__ __forceinline__ float grp4_sum(float x) {
+    x += __shfl_xor(x, 16, kWave);
+    x += __shfl_xor(x, 32, kWave);
+    return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) x = fmaxf(x, __shfl_xor(x, m, kWave));
+    return x;
+}
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) x += __shfl_xor(x, m, kWave);
+    return x;
+}
+
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+}  // namespace fattn

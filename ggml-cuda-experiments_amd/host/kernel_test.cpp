@@ -1,0 +1,316 @@
+// kernel_test.cpp -- MI355X counterpart of the reference's launch/verify harness
+// (src/kernel_test.h:1-249, entered from main() in src/flash-matrix.cu:341-346).
+//
+// Same flags and the same flow: synthetic inputs from rand() in the order
+// Q, K, V, mask (kernel_test.h:45-48; srand never called -> glibc seed 1),
+// a CPU reference with the reference's arithmetic (kernel_test.h:50-62: operands
+// rounded through fp16, fp32 accumulation, single-pass online softmax), the GPU
+// path through the C ABI (include/fattn.h), a timed launch and the max-diff
+// report (kernel_test.h:201-234).  Differences from the reference harness, all
+// additive: a pass/fail threshold and exit code (the reference prints a diff
+// with no threshold), warmup + repeated timing (median), and K/V types.
+//
+//   --no-kv-parallel     one KV chunk per head (the flash_attn_ext path, kernel_test.h:180-199)
+//   --n-warps N          accepted for compatibility (kernel_test.h:9-13); the gfx950
+//                        kernel always runs 4 wave64s per workgroup
+//   --kv-size N          KV length, min 256 (kernel_test.h:14-18)
+//   --kv-type T          f16 (default, as the reference) | q8_0 | q4_0
+//   --head-dim D --heads H --kv-heads Hkv --iters I --tol T
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fattn.h"
+
+#define HIP_CHECK(x)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) {                                                                   \
+            fprintf(stderr, "HIP error %s at %s:%d (%s)\n", hipGetErrorString(e_), __FILE__, __LINE__, #x); \
+            exit(2);                                                                              \
+        }                                                                                         \
+    } while (0)
+
+namespace {
+
+// ---- host fp16 (round to nearest even), the conversions utils.h relies on
+uint16_t f2h(float f) {
+    uint32_t x;
+    std::memcpy(&x, &f, 4);
+    const uint32_t sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return (uint16_t)(sign | (ax > 0x7f800000u ? 0x7e00u : 0x7c00u));
+    if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);
+    if (ax < 0x38800000u) {
+        if (ax <= 0x33000000u) return (uint16_t)sign;
+        const uint32_t e = ax >> 23, m = (ax & 0x7fffffu) | 0x800000u, sh = 126u - e;
+        uint32_t q = m >> sh;
+        const uint32_t rem = m & ((1u << sh) - 1u), half = 1u << (sh - 1u);
+        if (rem > half || (rem == half && (q & 1u))) q++;
+        return (uint16_t)(sign | q);
+    }
+    uint32_t h = ((((ax >> 23) - 112u) << 10) | ((ax & 0x7fffffu) >> 13));
+    const uint32_t rem = ax & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+    return (uint16_t)(sign | h);
+}
+float h2f(uint16_t h) {
+    const uint32_t sign = ((uint32_t)h & 0x8000u) << 16, e = (h >> 10) & 0x1fu;
+    uint32_t m = h & 0x3ffu, x;
+    if (e == 0) {
+        if (m == 0) {
+            x = sign;
+        } else {
+            int ee = -1;
+            do {
+                ee++;
+                m <<= 1;
+            } while (!(m & 0x400u));
+            x = sign | ((uint32_t)(112 - ee) << 23) | ((m & 0x3ffu) << 13);
+        }
+    } else if (e == 31) {
+        x = sign | 0x7f800000u | (m << 13);
+    } else {
+        x = sign | ((e + 112u) << 23) | (m << 13);
+    }
+    float f;
+    std::memcpy(&f, &x, 4);
+    return f;
+}
+float rh(float x) { return h2f(f2h(x)); }
+
+// kernel_test.h:45-48 / utils.h:57-61
+void random_fill(std::vector<float>& a) {
+    for (auto& x : a) x = 1.0f - ((float)rand() * 1.0f / (float)RAND_MAX) * 2.0f;
+}
+
+// kernel_test.h:50-62 with utils.h:5-49 arithmetic
+void cpu_reference(const std::vector<float>& q, const std::vector<float>& k, const std::vector<float>& v,
+                   const std::vector<float>& mask, std::vector<float>& out, int N, int D, int H, int Hkv, float scale) {
+    const int r = H / Hkv;
+    std::vector<float> s(N);
+    for (int h = 0; h < H; h++) {
+        const float* kh = k.data() + (size_t)(h / r) * D * N;
+        const float* vh = v.data() + (size_t)(h / r) * D * N;
+        for (int c = 0; c < N; c++) {
+            float acc = 0.0f;
+            for (int i = 0; i < D; i++) {
+                const float p = rh(q[(size_t)h * D + i]) * rh(kh[(size_t)c * D + i]);
+                acc = acc + p;
+            }
+            s[c] = acc * scale + mask[c];
+        }
+        float M = -INFINITY, S = 0.0f;
+        for (int i = 0; i < N; i++) {
+            if (s[i] > M) {
+                S = 1.0f + S * expf(M - s[i]);
+                M = s[i];
+            } else {
+                S += expf(s[i] - M);
+            }
+        }
+        for (int i = 0; i < N; i++) s[i] = expf(s[i] - M) / S;
+        for (int c = 0; c < D; c++) {
+            float acc = 0.0f;
+            for (int i = 0; i < N; i++) {
+                const float p = rh(s[i]) * rh(vh[(size_t)i * D + c]);
+                acc = acc + p;
+            }
+            out[(size_t)h * D + c] = acc;
+        }
+    }
+}
+
+void print_array(const char* name, const float* a, int count) {  // utils.h:63-71
+    printf("---------------- %s ------------------\n", name);
+    for (int i = 0; i < count; i++) printf("%0.4ff, ", a[i]);
+    printf("\n");
+}
+
+int parse_type(const std::string& s) {
+    if (s == "f16") return FATTN_TYPE_F16;
+    if (s == "q8_0") return FATTN_TYPE_Q8_0;
+    if (s == "q4_0") return FATTN_TYPE_Q4_0;
+    fprintf(stderr, "unknown --kv-type %s\n", s.c_str());
+    exit(2);
+}
+
+}  // namespace
+
+int main(int argc, const char* argv[]) {
+    int kv_size = 512, num_warps = 8, head_dim = 128, num_heads = 32, num_kv_heads = 8, iters = 20;
+    int kv_type = FATTN_TYPE_F16;
+    bool parallel_kv = true;
+    float tol = 1e-3f;
+    for (int i = 1; i < argc; i++) {
+        const std::string a = argv[i];
+        auto next = [&]() -> const char* {
+            if (++i >= argc) {
+                fprintf(stderr, "missing value for %s\n", a.c_str());
+                exit(2);
+            }
+            return argv[i];
+        };
+        if (a == "--no-kv-parallel") parallel_kv = false;
+        else if (a == "--n-warps") num_warps = atoi(next());
+        else if (a == "--kv-size") kv_size = std::max(256, atoi(next()));
+        else if (a == "--kv-type") kv_type = parse_type(next());
+        else if (a == "--head-dim") head_dim = atoi(next());
+        else if (a == "--heads") num_heads = atoi(next());
+        else if (a == "--kv-heads") num_kv_heads = atoi(next());
+        else if (a == "--iters") iters = std::max(1, atoi(next()));
+        else if (a == "--tol") tol = (float)atof(next());
+        else {
+            fprintf(stderr, "unknown flag %s\n", a.c_str());
+            return 2;
+        }
+    }
+    if (num_warps != 8 && num_warps != 4 && num_warps != 2 && num_warps != 1)
+        printf("invalid num_warps, should be 2, 4, 8\n");  // kernel_test.h:176-178 (informational)
+
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, 0));
+    printf("GPU: %s (%s), CUs: %d, LDS/block max: %zu KB, HBM: %zu MB\n", prop.name, prop.gcnArchName,
+           prop.multiProcessorCount, prop.sharedMemPerBlock / 1024, prop.totalGlobalMem >> 20);
+
+    const int D = head_dim, H = num_heads, Hkv = num_kv_heads, N = kv_size;
+    const float scale = 1.0f / sqrtf((float)D);
+    if (H % Hkv) {
+        fprintf(stderr, "heads must be a multiple of kv-heads\n");
+        return 2;
+    }
+    std::vector<float> query((size_t)D * H), key((size_t)D * N * Hkv), value((size_t)D * N * Hkv), mask(N);
+    random_fill(query);
+    random_fill(key);
+    random_fill(value);
+    random_fill(mask);
+
+    hipStream_t stream;
+    HIP_CHECK(hipStreamCreate(&stream));
+    float *d_q, *d_out, *d_kf, *d_vf;
+    void *d_k, *d_v, *d_mask, *d_ws;
+    const size_t rb = fattn_row_size(kv_type, D);
+    HIP_CHECK(hipMalloc(&d_q, sizeof(float) * D * H));
+    HIP_CHECK(hipMalloc(&d_out, sizeof(float) * D * H));
+    HIP_CHECK(hipMalloc(&d_k, rb * N * Hkv));
+    HIP_CHECK(hipMalloc(&d_v, rb * N * Hkv));
+    HIP_CHECK(hipMalloc(&d_mask, 2 * (size_t)N));
+    HIP_CHECK(hipMemcpyAsync(d_q, query.data(), sizeof(float) * D * H, hipMemcpyHostToDevice, stream));
+    std::vector<uint16_t> mask16(N);
+    for (int i = 0; i < N; i++) mask16[i] = f2h(mask[i]);
+    HIP_CHECK(hipMemcpyAsync(d_mask, mask16.data(), 2 * (size_t)N, hipMemcpyHostToDevice, stream));
+
+    // K/V storage.  f16: K [Hkv][N][D]; V transposed [Hkv][D][N] on the parallel
+    // path (-DFA_KV_BLOCK_256, kernel_test.h:96-105), row-major otherwise.
+    // q8_0/q4_0: quantised on the GPU (fattn_quantize) from the f32 values; the
+    // CPU reference then uses the dequantised values (fattn_dequantize).
+    std::vector<float> kref = key, vref = value;
+    const bool vtrans = parallel_kv && kv_type == FATTN_TYPE_F16;
+    if (kv_type == FATTN_TYPE_F16) {
+        std::vector<uint16_t> k16(key.size()), v16(value.size());
+        for (size_t i = 0; i < key.size(); i++) k16[i] = f2h(key[i]);
+        for (int h = 0; h < Hkv; h++)
+            for (int n = 0; n < N; n++)
+                for (int d = 0; d < D; d++) {
+                    const size_t src = ((size_t)h * N + n) * D + d;
+                    const size_t dst = vtrans ? ((size_t)h * D + d) * N + n : src;
+                    v16[dst] = f2h(value[src]);
+                }
+        HIP_CHECK(hipMemcpyAsync(d_k, k16.data(), 2 * k16.size(), hipMemcpyHostToDevice, stream));
+        HIP_CHECK(hipMemcpyAsync(d_v, v16.data(), 2 * v16.size(), hipMemcpyHostToDevice, stream));
+    } else {
+        HIP_CHECK(hipMalloc(&d_kf, sizeof(float) * key.size()));
+        HIP_CHECK(hipMalloc(&d_vf, sizeof(float) * value.size()));
+        HIP_CHECK(hipMemcpyAsync(d_kf, key.data(), 4 * key.size(), hipMemcpyHostToDevice, stream));
+        HIP_CHECK(hipMemcpyAsync(d_vf, value.data(), 4 * value.size(), hipMemcpyHostToDevice, stream));
+        int rc = fattn_quantize(kv_type, d_kf, d_k, D, (int64_t)N * Hkv, stream);
+        rc = rc ? rc : fattn_quantize(kv_type, d_vf, d_v, D, (int64_t)N * Hkv, stream);
+        rc = rc ? rc : fattn_dequantize(kv_type, d_k, d_kf, D, (int64_t)N * Hkv, stream);
+        rc = rc ? rc : fattn_dequantize(kv_type, d_v, d_vf, D, (int64_t)N * Hkv, stream);
+        if (rc) {
+            fprintf(stderr, "quantize failed: %s\n", fattn_strerror(rc));
+            return 2;
+        }
+        HIP_CHECK(hipMemcpyAsync(kref.data(), d_kf, 4 * key.size(), hipMemcpyDeviceToHost, stream));
+        HIP_CHECK(hipMemcpyAsync(vref.data(), d_vf, 4 * value.size(), hipMemcpyDeviceToHost, stream));
+    }
+    HIP_CHECK(hipStreamSynchronize(stream));
+
+    // CPU reference (kernel_test.h:50-66)
+    std::vector<float> qkv((size_t)D * H), qkv_gpu((size_t)D * H);
+    cpu_reference(query, kref, vref, mask, qkv, N, D, H, Hkv, scale);
+    print_array("Reference", qkv.data(), 16);
+
+    // GPU launch description
+    fattn_params p;
+    std::memset(&p, 0, sizeof(p));
+    p.q = {d_q, FATTN_TYPE_F32, 0, {D, 1, H, 1}, {4, (int64_t)D * H * 4, (int64_t)D * 4, (int64_t)D * H * 4}};
+    const int64_t eb = kv_type == FATTN_TYPE_F16 ? 2 : (int64_t)fattn_row_size(kv_type, 32);
+    p.k = {d_k, kv_type, 0, {D, N, Hkv, 1}, {eb, (int64_t)rb, (int64_t)rb * N, (int64_t)rb * N * Hkv}};
+    if (vtrans)
+        p.v = {d_v, kv_type, 0, {D, N, Hkv, 1}, {(int64_t)N * 2, 2, (int64_t)rb * N, (int64_t)rb * N * Hkv}};
+    else
+        p.v = {d_v, kv_type, 0, {D, N, Hkv, 1}, {eb, (int64_t)rb, (int64_t)rb * N, (int64_t)rb * N * Hkv}};
+    p.mask = {d_mask, FATTN_TYPE_F16, 0, {N, 1, 1, 1}, {2, (int64_t)N * 2, (int64_t)N * 2, (int64_t)N * 2}};
+    p.dst = d_out;
+    p.scale = scale;
+    p.kv_chunk = parallel_kv ? 0 : N;  // --no-kv-parallel: whole KV per workgroup
+    const size_t ws = fattn_workspace_size(&p);
+    HIP_CHECK(hipMalloc(&d_ws, std::max<size_t>(ws, 16)));
+    p.workspace = d_ws;
+    p.workspace_bytes = std::max<size_t>(ws, 16);
+
+    int rc = fattn_ext(&p, stream);
+    if (rc) {
+        fprintf(stderr, "fattn_ext failed: %s\n", fattn_strerror(rc));
+        return 2;
+    }
+    HIP_CHECK(hipStreamSynchronize(stream));
+    // timing: warmup done above; median of `iters` event-timed launches
+    hipEvent_t start, stop;
+    HIP_CHECK(hipEventCreate(&start));
+    HIP_CHECK(hipEventCreate(&stop));
+    std::vector<float> times;
+    for (int it = 0; it < iters; it++) {
+        HIP_CHECK(hipEventRecord(start, stream));
+        rc = fattn_ext(&p, stream);
+        HIP_CHECK(hipEventRecord(stop, stream));
+        HIP_CHECK(hipEventSynchronize(stop));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, start, stop));
+        times.push_back(ms);
+    }
+    std::sort(times.begin(), times.end());
+    const float millis = times[times.size() / 2];
+    HIP_CHECK(hipMemcpyAsync(qkv_gpu.data(), d_out, 4 * qkv_gpu.size(), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    print_array(parallel_kv ? "Parallel KV HIP" : "No paralell KV HIP", qkv_gpu.data(), 16);
+
+    // kernel_test.h:215-234 (+ a normwise relative error and a threshold)
+    float max_diff = 0.0f, max_ref = 0.0f;
+    int head_idx = 0, dim_idx = 0;
+    for (int h = 0; h < H; h++)
+        for (int i = 0; i < D; i++) {
+            const float d = fabsf(qkv[(size_t)h * D + i] - qkv_gpu[(size_t)h * D + i]);
+            max_ref = std::max(max_ref, fabsf(qkv[(size_t)h * D + i]));
+            if (d > max_diff || std::isnan(d)) {
+                max_diff = std::isnan(d) ? INFINITY : d;
+                head_idx = h;
+                dim_idx = i;
+            }
+        }
+    const double bytes = (double)D * H * 4 * 2 + 2.0 * rb * N * Hkv + 2.0 * N;
+    const double flops = 4.0 * N * D * H;
+    printf("\ncuda time: %.4f ms  (%.1f GB/s, %.3f TFLOP/s; median of %d)\n", millis, bytes / millis / 1e6,
+           flops / millis / 1e9, iters);
+    printf("R (%.4f) CUDA(%.4f) diff: %.4f - head = %d, dim = %d\n", qkv[(size_t)head_idx * D + dim_idx],
+           qkv_gpu[(size_t)head_idx * D + dim_idx], max_diff, head_idx, dim_idx);
+    const float rel = max_diff / std::max(max_ref, 1e-30f);
+    printf("normwise rel err %.3g (tol %.1g): %s\n", rel, tol, rel <= tol ? "PASS" : "FAIL");
+    return rel <= tol ? 0 : 1;
+}

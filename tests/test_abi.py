@@ -1,0 +1,102 @@
+"""CPU: the C-ABI library loads, exports every symbol include/fattn.h declares,
+and validates arguments without touching a GPU (no compute calls here)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import fattn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "fattn.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(fattn_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_symbols_parsed():
+    syms = header_symbols()
+    assert "fattn_ext" in syms and "fattn_quantize" in syms and len(syms) == len(fattn.EXPORTS)
+    assert set(syms) == set(fattn.EXPORTS)
+
+
+def test_library_exports_every_header_symbol():
+    L = fattn.lib()
+    for s in header_symbols():
+        assert hasattr(L, s), s
+
+
+def test_nm_exports():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", fattn.LIB_PATH], capture_output=True, text=True).stdout
+    for s in header_symbols():
+        assert re.search(rf"\bT {s}$", out, flags=re.M), s
+
+
+def test_strerror_and_sizes():
+    assert fattn.strerror(0) == "ok"
+    assert "stride" in fattn.strerror(-4)
+    assert fattn.row_size(fattn.TYPE_Q8_0, 128) == 136
+    assert fattn.row_size(fattn.TYPE_Q4_0, 128) == 72
+    assert fattn.row_size(fattn.TYPE_F16, 128) == 256
+    assert fattn.row_size(fattn.TYPE_Q8_0, 100) == 0
+    assert fattn.lib().fattn_version().startswith(b"fattn-gfx950")
+
+
+def _params(D=128, NQ=1, H=32, Hkv=32, N=4096, kt=fattn.TYPE_Q8_0, kv_chunk=0, ptr=1 << 20, mask=True):
+    rb = fattn.row_size(kt, D)
+    eb = 2 if kt == fattn.TYPE_F16 else fattn.BLOCK_BYTES.get(kt, 4)
+    q = fattn.View(ptr, fattn.TYPE_F32, (D, NQ, H, 1), (4, H * D * 4, D * 4, NQ * H * D * 4))
+    k = fattn.View(ptr, kt, (D, N, Hkv, 1), (eb, rb, rb * N, rb * N * Hkv))
+    m = fattn.View(ptr, fattn.TYPE_F16, (N, NQ, 1, 1), (2, N * 2, N * 2 * NQ, N * 2 * NQ)) if mask else None
+    return fattn.ext_params(q, k, k, m, ptr, 0.088, kv_chunk=kv_chunk)
+
+
+def test_workspace_size_config3():
+    p = _params()
+    ws = fattn.workspace_size(p)
+    # 32 heads x n_chunks partial slots of 16 rows x (D + 2) floats
+    assert ws > 0 and ws % (16 * 130 * 4) == 0
+
+
+def test_single_chunk_needs_no_workspace():
+    assert fattn.workspace_size(_params(N=128)) == 0
+
+
+@pytest.mark.parametrize("bad", [
+    dict(D=96), dict(D=256), dict(H=30, Hkv=8), dict(N=0), dict(kt=fattn.TYPE_F32), dict(kt=5),
+])
+def test_rejects_invalid(bad):
+    p = _params(**bad)
+    assert fattn.workspace_size(p) == 0
+    with pytest.raises(fattn.FattnError):
+        fattn.flash_attn_ext(p, stream=0)
+
+
+def test_rejects_missing_workspace():
+    p = _params()
+    with pytest.raises(fattn.FattnError) as e:
+        fattn.flash_attn_ext(p, stream=0)
+    assert e.value.code == -5
+
+
+def test_rejects_misaligned_q():
+    p = _params()
+    p.q.data = (1 << 20) + 4
+    assert fattn.lib().fattn_ext(C.byref(p), None) == -7
+
+
+def test_rejects_null():
+    p = _params()
+    p.q.data = None
+    assert fattn.lib().fattn_ext(C.byref(p), None) == -1
+    assert fattn.lib().fattn_quantize(fattn.TYPE_Q8_0, None, None, 32, 1, None) == -1
+    assert fattn.lib().fattn_dequantize(fattn.TYPE_Q8_0, None, None, 32, 1, None) == -1
+
+
+def test_row_workspace_size():
+    assert fattn.lib().fattn_row_workspace_size(128, 4096, 32) > 0
+    assert fattn.lib().fattn_row_workspace_size(96, 4096, 32) == 0

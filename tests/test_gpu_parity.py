@@ -1,0 +1,206 @@
+"""GPU parity: the HIP path (C ABI -> libfattn.so) against the CPU oracle.
+
+Bar (BASELINE.json north_star): dequant / quantize bit-exact; attention within
+1e-3 normwise relative error per output row (problems.attn_rel_err), NaN rows
+(fully masked) identical.  BASELINE configs 2-5 run at their full sizes.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+import fattn
+from gpu_util import run_gpu, upload, views
+from oracle import oracle as orc
+from problems import attn_rel_err, make_problem
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-3
+
+
+# ------------------------------------------------------------------ unit: dequant / quantize
+
+@pytest.mark.parametrize("typ", [fattn.TYPE_Q8_0, fattn.TYPE_Q4_0])
+def test_dequantize_bitexact(dev, typ):
+    import torch
+    rng = np.random.default_rng(1)
+    nblk = 4096
+    bb = orc.BLOCK_BYTES[typ]
+    blocks = rng.integers(0, 256, size=(nblk, bb), dtype=np.uint8)
+    # finite scales spanning normals and subnormals, both signs
+    d = orc.f32_to_f16_bits(rng.choice([1, -1], nblk).astype(np.float32) *
+                            np.exp2(rng.uniform(-24, 8, nblk)).astype(np.float32))
+    blocks[:, 0:2] = d.view(np.uint8).reshape(nblk, 2)
+    ref = orc.dequantize(blocks.reshape(-1), typ, nblk * 32).reshape(-1)
+    got = fattn.dequantize(torch.from_numpy(blocks.reshape(-1)).to(dev), typ, 128).cpu().numpy().reshape(-1)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_dequantize_f16_exhaustive(dev):
+    import torch
+    bits = np.arange(65536, dtype=np.uint16)
+    bits = bits[(bits & 0x7c00) != 0x7c00]  # finite only
+    ref = orc.f16_bits_to_f32(bits)
+    n = bits.size // 64 * 64
+    got = fattn.dequantize(torch.from_numpy(bits[:n].view(np.int16)).to(dev), fattn.TYPE_F16, 64).cpu().numpy()
+    assert np.array_equal(got.reshape(-1).view(np.uint32), ref[:n].view(np.uint32))
+
+
+@pytest.mark.parametrize("typ", [fattn.TYPE_Q8_0, fattn.TYPE_Q4_0])
+def test_quantize_bitexact(dev, typ):
+    import torch
+    rng = np.random.default_rng(2)
+    x = (rng.standard_normal((512, 128)) * np.exp2(rng.uniform(-10, 10, (512, 1)))).astype(np.float32)
+    x[3] = 0.0  # all-zero block -> d = 0, id = 0
+    x[7, :32] = 1.0
+    ref = orc.quantize(x, typ)
+    got = fattn.quantize(torch.from_numpy(x).to(dev), typ).cpu().numpy()
+    assert np.array_equal(got, ref.reshape(got.shape))
+
+
+# ------------------------------------------------------------------ BASELINE configs (full size)
+
+@pytest.mark.parametrize("layout", ["head", "pos"])
+def test_config2_f16_decode(dev, layout):
+    p = make_problem(D=128, NQ=1, H=32, N=2048, kv_type="f16", layout=layout, seed=20)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+def test_config2_f16_vtrans(dev):
+    """flash_row_float layout: V stored transposed [Hkv][D][N]."""
+    p = make_problem(D=128, NQ=1, H=32, N=2048, kv_type="f16", v_trans=True, seed=21)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("layout", ["head", "pos"])
+def test_config3_q8_0(dev, layout):
+    p = make_problem(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", layout=layout, seed=30)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+def test_config4_q4_0_gqa(dev):
+    p = make_problem(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0", seed=40)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+def test_config5_batch64_shard(dev):
+    """Config 5's per-GPU shard: 64 query rows, 4 of the 32 heads, N=4096, Q8_0."""
+    p = make_problem(D=128, NQ=64, H=4, N=4096, kv_type="q8_0", seed=50)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+# ------------------------------------------------------------------ sweep
+
+CASES = []
+for D in (64, 128):
+    for kt in ("f16", "q8_0", "q4_0"):
+        for layout in ("head", "pos", "padded"):
+            CASES.append(dict(D=D, kv_type=kt, layout=layout, NQ=1, H=4, Hkv=4, N=256, mask="random"))
+        CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=3, H=8, Hkv=2, N=100, mask="causal"))
+        CASES.append(dict(D=D, kv_type=kt, layout="pos", NQ=17, H=4, Hkv=4, N=200, mask="random"))
+        CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=2, H=6, Hkv=2, N=96, mask="none"))
+        CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=5, H=32, Hkv=1, N=64, mask="neginf_blocks"))
+        CASES.append(dict(D=D, kv_type=kt, layout="pos", NQ=1, H=2, Hkv=2, N=1, mask="random"))
+        CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=4, H=2, Hkv=2, N=33, mask="random", S=3))
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_sweep(dev, case):
+    p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+
+
+@pytest.mark.parametrize("chunk", [128, 256, 1024, 100000])
+def test_chunking_invariance(dev, chunk):
+    """Forced split-KV chunk sizes (many partials / single chunk) agree with the oracle."""
+    p = make_problem(D=128, NQ=2, H=8, Hkv=4, N=1500, kv_type="q8_0", layout="pos", seed=7)
+    assert attn_rel_err(run_gpu(p, kv_chunk=chunk), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("kt", ["f16", "q8_0", "q4_0"])
+def test_extreme_rescale(dev, kt):
+    """Large scores force the online-softmax rescale branch (guide rule 26)."""
+    p = make_problem(D=128, NQ=4, H=4, N=1024, kv_type=kt, seed=8, extreme=True)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+def test_fully_masked_rows_are_nan(dev):
+    p = make_problem(D=64, NQ=3, H=2, N=128, kv_type="q8_0", mask="zero", seed=9)
+    m = orc.f16_bits_to_f32(p.mask_bits)
+    m[1, :] = -np.inf   # row 1 sees nothing -> NaN (src/utils.h:30-49 semantics)
+    p.mask_bits = orc.f32_to_f16_bits(m)
+    got, ref = run_gpu(p), p.oracle()
+    assert np.isnan(ref[:, 1]).all() and np.isnan(got[:, 1]).all()
+    assert attn_rel_err(got, ref) <= RTOL
+
+
+def test_deterministic(dev):
+    p = make_problem(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", seed=11)
+    a, b = run_gpu(p), run_gpu(p)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+# ------------------------------------------------------------------ reference entry points
+
+def test_kernel_test_flow(dev):
+    """src/kernel_test.h as the reference runs it: srand(1) (glibc default seed),
+    random() fill order Q, K, V, mask; GQA 32/8, D=128, kv_size=512; CPU
+    reference = kernel_test.h:50-62; GPU = fattn_row with V transposed
+    (-DFA_KV_BLOCK_256 layout, kernel_test.h:96-105) and f16 mask."""
+    import torch
+    D, H, Hkv, N = 128, 32, 8, 512
+    orc.srand(1)
+    query = orc.random(D * H)
+    key = orc.random(D * N * Hkv)
+    value = orc.random(D * N * Hkv)
+    mask = orc.random(N)
+    ref = orc.kernel_test_cpu(query, key, value, mask, N, D, H, Hkv)
+    kf16 = orc.f32_to_f16_bits(key)
+    vt = orc.f32_to_f16_bits(value.reshape(Hkv, N, D).transpose(0, 2, 1).copy())
+    mf16 = orc.f32_to_f16_bits(mask)
+    d = lambda a: torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a).to(dev)
+    qkv = torch.empty(H * D, dtype=torch.float32, device=dev)
+    fattn.row(d(query), d(kf16), d(vt), d(mf16), qkv, D, N, H, 1.0 / np.sqrt(np.float32(D)), D * N, H // Hkv)
+    torch.cuda.synchronize()
+    got = qkv.cpu().numpy()
+    # the reference's CPU side adds the f32 mask, the GPU the f16 one (as the reference does)
+    assert attn_rel_err(got.reshape(H, D), ref.reshape(H, D)) <= RTOL
+
+
+def test_ext_f16_launch_positional(dev):
+    """flash-llama.h:7-32 argument list, as kernel_test.h:191-198 passes it."""
+    import torch
+    p = make_problem(D=128, NQ=1, H=32, Hkv=8, N=512, kv_type="f16", mask="random", seed=12, mask_pad=512)
+    t = upload(p, dev)
+    L = fattn.lib()
+    ws = torch.empty(1 << 22, dtype=torch.uint8, device=dev)
+    D, N = 128, 512
+    mrows = p.mask_bits.shape[0]
+    rc = L.fattn_ext_f16_launch(
+        t["q"].data_ptr(), t["k"].data_ptr(), t["v"].data_ptr(), t["mask"].data_ptr(), t["dst"].data_ptr(),
+        p.scale, D, 1, 32, 1, D, N, 8, 1, mrows, N * 2, D * 4 * 32, D * 4, D * 32 * 4,
+        D * 2, D * N * 2, D * N * 8 * 2, D, 32, 1, 1, fattn.TYPE_F16, fattn.TYPE_F16, ws.data_ptr(), ws.numel(),
+        torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, fattn.strerror(rc)
+    torch.cuda.synchronize()
+    assert attn_rel_err(t["dst"].cpu().numpy(), p.oracle()) <= RTOL
+
+
+def test_graph_capture(dev):
+    """The launch path allocates nothing and does not sync: capturable into a HIP graph."""
+    import torch
+    p = make_problem(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", seed=13)
+    t = upload(p, dev)
+    att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        att(s.cuda_stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        att(s.cuda_stream)
+    t["dst"].fill_(float("nan"))
+    g.replay()
+    torch.cuda.synchronize()
+    assert attn_rel_err(t["dst"].cpu().numpy(), p.oracle()) <= RTOL
