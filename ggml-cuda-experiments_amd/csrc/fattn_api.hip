@@ -68,8 +68,9 @@ int make_plan(const fattn_params* p, Plan& pl) {
 
     const bool has_mask = mk.data != nullptr;
     if (has_mask) {
-        if (mk.type != FATTN_TYPE_F16 || mk.ne[0] < N || mk.ne[1] < NQ) return FATTN_ERR_INVALID_ARG;
-        if ((uintptr_t)mk.data % 2 || mk.nb[1] % 2) return FATTN_ERR_ALIGNMENT;
+        // rows padded to an even length (ggml pads to GGML_KQ_MASK_PAD), dword aligned
+        if (mk.type != FATTN_TYPE_F16 || mk.ne[0] < N + (N & 1) || mk.ne[1] < NQ) return FATTN_ERR_INVALID_ARG;
+        if ((uintptr_t)mk.data % 4 || mk.nb[1] % 4) return FATTN_ERR_ALIGNMENT;
     }
 
     // fast path: 16-B pieces

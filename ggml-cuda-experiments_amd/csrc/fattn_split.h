@@ -112,7 +112,9 @@ struct StepPlan {
     static constexpr int PK = C::kBytes / GRAN;
     static constexpr int PV = C::vBytes / GRAN;
     static constexpr int NIKV = (PK + PV + kWave - 1) / kWave;
-    static constexpr int MG = GRAN == 16 ? 16 : 2;       // mask granule
+    // mask granule: LDS-DMA writes lane*4 bytes for sub-dword sizes, so the
+    // generic path moves dwords (2 positions) and needs even-padded mask rows
+    static constexpr int MG = GRAN == 16 ? 16 : 4;
     static constexpr int MPR = kStep * 2 / MG;           // mask pieces per row
     // all 16 mask rows are always copied (rows past the tile clamp to a valid
     // query row) so every step issues the same, compile-time instruction count
@@ -183,12 +185,13 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const uint8_t* kb
             const int mr = q / P::MPR;
             const int off = (q % P::MPR) * P::MG;
             const int qrow = min(mrow0 + mr, a.NQ - 1);
-            const int pos = min(n0 + off / 2, a.N - 1);
+            int pos = n0 + off / 2;
+            if constexpr (P::MG == 4) pos = min(pos, (a.N - 1) & ~1);  // rows padded to even length
             const uint8_t* src = a.mask + (int64_t)qrow * a.m_nb1 + (int64_t)pos * 2;
             if constexpr (P::MG == 16) {
                 __builtin_amdgcn_global_load_lds((const void*)src, (void*)(mbuf + i * kWave * 16), 16, 0, 0);
             } else {
-                __builtin_amdgcn_global_load_lds((const void*)src, (void*)(mbuf + i * kWave * 2), 2, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)src, (void*)(mbuf + i * kWave * 4), 4, 0, 0);
             }
         }
     }

@@ -72,8 +72,8 @@ def lib() -> C.CDLL:
         L.fattn_ext_events.restype = C.c_int
         L.fattn_ext_events.argtypes = [C.POINTER(FattnParams), vp, vp, vp]
         L.fattn_ext_f16_launch.restype = C.c_int
-        L.fattn_ext_f16_launch.argtypes = [vp, vp, vp, vp, vp, C.c_float] + [C.c_int] * 22 + [C.c_int, C.c_int, vp,
-                                                                                             sz, vp]
+        L.fattn_ext_f16_launch.argtypes = ([vp, vp, vp, vp, vp, C.c_float] + [C.c_int] * 20 +
+                                           [C.c_int, C.c_int, vp, sz, vp])
         L.fattn_row_workspace_size.restype = sz
         L.fattn_row_workspace_size.argtypes = [C.c_int, C.c_int, C.c_int]
         L.fattn_row.restype = C.c_int

@@ -80,8 +80,9 @@ typedef struct fattn_tensor {
  *   k    F16/Q8_0/Q4_0  ne = [D, N, Hkv, Skv]  rows contiguous (nb[0] = type size)
  *   v    same type family as k, ne = [D, N, Hkv, Skv]; rows contiguous, or for
  *        F16 only transposed (nb[1] == 2, nb[0] == N*2 style strides)
- *   mask F16 ne = [N, rows >= n_q] (row = query index, broadcast over heads and
- *        sequences), or data == NULL for no mask
+ *   mask F16 ne = [N', rows >= n_q] with N' >= N rounded up to even (ggml pads
+ *        mask rows to GGML_KQ_MASK_PAD), 4-byte aligned rows; row = query
+ *        index, broadcast over heads and sequences; or data == NULL for no mask
  *   dst  f32 contiguous [S][n_q][H][D]
  *   H % Hkv == 0 (GQA broadcast), S % Skv == 0.
  *   softmax(scale * q.k^T + mask) . v per (seq, head, query row).  A row whose
