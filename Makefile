@@ -13,15 +13,26 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-functi
 CSRC := $(wildcard $(PKG)/csrc/*.hip)
 CHDR := $(wildcard $(PKG)/csrc/*.h) include/fattn.h
 
-.PHONY: all lib harness oracle clean asm
+.PHONY: all lib harness oracle clean asm stamps tests-hip
 
-all: lib harness oracle
+all: lib harness oracle tests-hip
 
 lib: $(LIB)
 
 $(LIB): $(CSRC) $(CHDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared $(CSRC) -o $@
+
+# diagnostic library with per-wave phase stamps (tools/stamps.py); never loaded by the product path
+stamps: $(LIBDIR)/libfattn_stamps.so $(LIBDIR)/libfattn_nocompute.so
+
+$(LIBDIR)/libfattn_nocompute.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_STAMPS -DFATTN_DIAG_NOCOMPUTE -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_stamps.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_STAMPS -shared $(CSRC) -o $@
 
 harness: $(HARNESS)
 
@@ -41,3 +52,10 @@ asm:
 clean:
 	rm -rf $(LIBDIR) $(BINDIR) build
 	$(MAKE) -C oracle clean
+
+# test-only HIP probes (tests/hip) -> tests/_build/libprims.so
+tests-hip: tests/_build/libprims.so
+
+tests/_build/libprims.so: tests/hip/prims.hip $(CHDR)
+	@mkdir -p tests/_build
+	$(HIPCC) $(HIPFLAGS) -shared tests/hip/prims.hip -o $@

@@ -145,50 +145,67 @@ def main():
     q = torch.rand((1, NQ, H, D), generator=g, device=dev) * 2 - 1
     npad = (N + 63) // 64 * 64
     mask = (torch.rand((NQ, npad), generator=g, device=dev) * 2 - 1).to(torch.float16)
-    steps_out = torch.empty((args.steps, 1, NQ, H, D), dtype=torch.float32, device=dev)
-    warm_out = torch.empty((1, NQ, H, D), dtype=torch.float32, device=dev)
+    outs = torch.empty((R, 1, NQ, H, D), dtype=torch.float32, device=dev)
 
     att = fattn.Attention(fattn.q_view(q), fattn.kv_view(kv_sets[0][0], typ, D, N, Hkv, layout=args.layout),
                           fattn.kv_view(kv_sets[0][1], typ, D, N, Hkv, layout=args.layout),
-                          fattn.mask_view(mask), warm_out, 1.0 / D ** 0.5, kv_chunk=args.kv_chunk)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    hip, evs = hip_events(2 * args.steps)
+                          fattn.mask_view(mask), outs[0], 1.0 / D ** 0.5, kv_chunk=args.kv_chunk)
 
-    def step(i, out, ev=None):
+    def step(i, stream=None, ev=None):
         kvs = kv_sets[i % R]
-        att.retarget(k=kvs[0].data_ptr(), v=kvs[1].data_ptr(), dst=out.data_ptr())
+        att.retarget(k=kvs[0].data_ptr(), v=kvs[1].data_ptr(), dst=outs[i % R].data_ptr())
         if ev is None:
             att(stream)
         else:
-            att(stream, evs[2 * ev], evs[2 * ev + 1])
+            att(stream, ev[0], ev[1])
 
+    # 1) dominant-kernel duration: eager launches with HIP events recorded by
+    #    libfattn around the main kernel only (not part of the timed region)
+    n_ev = min(args.steps, 200)
+    hip, evs = hip_events(2 * n_ev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
     for i in range(args.warmup):
-        step(i, warm_out)
+        step(i, stream)
+    for i in range(n_ev):
+        step(i, stream, (evs[2 * i], evs[2 * i + 1]))
+    torch.cuda.synchronize()
+    f = C.c_float()
+    kms = []
+    for i in range(n_ev):
+        hip.hipEventElapsedTime(C.byref(f), evs[2 * i], evs[2 * i + 1])
+        kms.append(f.value)
+    kms.sort()
+    kern_ms_avg = sum(kms) / len(kms)
+
+    # 2) the timed job: the K steps (step i reads KV cache i % R) captured
+    #    back-to-back into one HIP graph -- the launch-bound inner loop lives on
+    #    the device, not in Python -- and replayed once inside the timed region
+    K = args.steps
+    gs = torch.cuda.Stream(dev)
+    gs.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(gs):
+        for i in range(min(K, R)):
+            step(i)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=gs):
+        for i in range(K):
+            step(i)
+    graph.replay()   # untimed warm replay
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-
-    gathered = torch.empty((world,) + tuple(steps_out.shape), dtype=torch.float32, device=dev) if world > 1 else None
+    gathered = torch.empty((world,) + tuple(outs.shape), dtype=torch.float32, device=dev) if world > 1 else None
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, steps_out[i], ev=i)
+    graph.replay()
     if world > 1:
-        dist.all_gather_into_tensor(gathered, steps_out)   # the single RCCL gather over xGMI
+        dist.all_gather_into_tensor(gathered, outs)   # the single RCCL gather over xGMI
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-
-    # dominant-kernel duration from the HIP events around each main-kernel launch
-    f = C.c_float()
-    kms = []
-    for i in range(args.steps):
-        hip.hipEventElapsedTime(C.byref(f), evs[2 * i], evs[2 * i + 1])
-        kms.append(f.value)
-    kms.sort()
-    kern_ms_avg = sum(kms) / len(kms)
 
     if world > 1:
         t = torch.tensor([elapsed, kern_ms_avg], dtype=torch.float64, device=dev)
@@ -233,7 +250,7 @@ def main():
             "kernel_ms_median": round(kms[len(kms) // 2], 5),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "fattn_split_kernel<Q8_0,Q8_0,128,16,mask>"},
+                         "kernel": f"fattn_split_kernel<{args.kv_type},{args.kv_type},D{D}>"},
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, min(args.cpu_threads, os.cpu_count() or 1))

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 #include "fattn_quant.h"
 #include "fattn_split.h"
@@ -29,8 +30,98 @@ struct Plan {
     int D;
     int gran;
     dim3 grid;
-    size_t ws_bytes;
+    int lds;
+    size_t ws_bytes, ml_bytes;
 };
+
+// LDS geometry of one instantiation (type-erased for the planner)
+struct Geom {
+    int step_bytes, vsc_bytes, merge_bytes;
+    int wave_bytes(int nbuf) const {
+        const int w = (nbuf * step_bytes + vsc_bytes + 15) / 16 * 16;
+        return w > merge_bytes ? w : merge_bytes;
+    }
+    int lds_bytes(int nbuf) const { return kSplitWaves * wave_bytes(nbuf); }
+};
+
+template <int KT, int VT, int D>
+Geom geom_of() {
+    using C = SplitCfg<KT, VT, D>;
+    return Geom{C::stepBytes, C::vscBytes, C::mergeBytes};
+}
+
+Geom geom(int kt, int vt, int D) {
+    auto pick = [&](auto d) -> Geom {
+        constexpr int DD = decltype(d)::value;
+        if (kt == FATTN_TYPE_Q8_0) return geom_of<FATTN_TYPE_Q8_0, FATTN_TYPE_Q8_0, DD>();
+        if (kt == FATTN_TYPE_Q4_0) return geom_of<FATTN_TYPE_Q4_0, FATTN_TYPE_Q4_0, DD>();
+        if (vt == VT_F16T) return geom_of<FATTN_TYPE_F16, VT_F16T, DD>();
+        return geom_of<FATTN_TYPE_F16, FATTN_TYPE_F16, DD>();
+    };
+    return D == 128 ? pick(std::integral_constant<int, 128>()) : pick(std::integral_constant<int, 64>());
+}
+
+constexpr int kLdsPerCU = 163840;
+
+// fattn_combine_kernel limits: one (chunk, row) pair per thread for the (m, l)
+// loads and at most MAXC chunks folded per thread
+bool combine_ok(int64_t nch, int rv, int D) {
+    const int ept = D / 16, maxc = 64 / ept * 2;
+    const int G = std::max(1, kRows / std::max(rv, 1));
+    int ncp = 1;
+    while (ncp < nch) ncp <<= 1;
+    return nch <= 64 && ncp * rv <= 256 && (nch + G - 1) / G <= maxc;
+}
+
+// Split-KV sizing for 256 CUs.  Every wave streams `spw` steps of 32 positions;
+// the grid is sized so that all (Y x S x chunks) workgroups are co-resident
+// (one wave per step when the problem is small: maximum memory-level
+// parallelism, no tail), limited by LDS (steps in flight) and registers.
+int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t NQ) {
+    SplitArgs& a = pl.a;
+    const Geom G = geom(pl.kt, pl.vt, pl.D);
+    const int quantum = kStep * kSplitWaves;
+    const int64_t steps = (N + kStep - 1) / kStep;
+    const int vgpr_wgs = (pl.kt == FATTN_TYPE_F16 || pl.gran == 4) ? 2 : 4;  // __launch_bounds__ waves/SIMD
+    const int rv_max = std::min<int64_t>(kRows, (int64_t)a.R * std::min<int64_t>(a.QPT, NQ));
+    int spw = 1, nbuf = 1;
+    if (kv_chunk > 0) {
+        spw = (int)((kv_chunk + quantum - 1) / quantum);
+        for (;;) {  // a forced chunk is a lower bound: grow it until the combine fits
+            const int64_t nch = (N + (int64_t)spw * quantum - 1) / ((int64_t)spw * quantum);
+            if (nch == 1 || combine_ok(nch, rv_max, pl.D)) break;
+            spw++;
+        }
+    } else {
+        for (;;) {
+            nbuf = (spw == 1 || pl.kt == FATTN_TYPE_F16) ? 1 : 2;
+            const int wgs_cu = std::max(1, std::min(vgpr_wgs, kLdsPerCU / G.lds_bytes(nbuf)));
+            const int64_t slots = (int64_t)kCUs * wgs_cu * kSplitWaves;
+            const int64_t need = (int64_t)((steps + spw - 1) / spw) * Y * S;  // waves at this spw
+            const int64_t nch = (N + (int64_t)spw * quantum - 1) / ((int64_t)spw * quantum);
+            const bool reducer_ok = nch == 1 || combine_ok(nch, rv_max, pl.D);
+            if ((need <= slots && reducer_ok) || nch == 1) break;
+            spw++;
+        }
+    }
+    nbuf = std::min(spw, (pl.kt == FATTN_TYPE_F16) ? 1 : 2);
+    a.nbuf = nbuf;
+    a.wave_bytes = G.wave_bytes(nbuf);
+    a.chunk_len = spw * quantum;
+    a.n_chunks = (int)((N + a.chunk_len - 1) / a.chunk_len);
+    a.ncp = 1;
+    while (a.ncp < a.n_chunks) a.ncp <<= 1;
+    if (a.n_chunks > 1 && !combine_ok(a.n_chunks, rv_max, pl.D)) return FATTN_ERR_INVALID_ARG;
+    pl.lds = G.lds_bytes(nbuf);
+    pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
+    if (a.n_chunks > 1) {
+        pl.ml_bytes = ((size_t)S * Y * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
+        pl.ws_bytes = pl.ml_bytes + (size_t)S * Y * a.n_chunks * kRows * pl.D * sizeof(float);
+    } else {
+        pl.ml_bytes = pl.ws_bytes = 0;
+    }
+    return FATTN_OK;
+}
 
 // Validate and build the launch plan.  Returns FATTN_OK or an error.
 int make_plan(const fattn_params* p, Plan& pl) {
@@ -105,6 +196,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     a.rk3 = (int)(S / Skv);
     a.R = std::min(a.rk2, kRows);
     a.QPT = kRows / a.R;
+    a.R_inv = 1.0f / (float)a.R;
     a.n_hsub = (a.rk2 + a.R - 1) / a.R;
     a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
     a.has_mask = has_mask ? 1 : 0;
@@ -112,25 +204,12 @@ int make_plan(const fattn_params* p, Plan& pl) {
 
     const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
     if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
-    // split-KV sizing: ~2 workgroups per CU; chunk a multiple of 4 waves x 32
-    const int quantum = kStep * kSplitWaves;
-    int chunk_len;
-    if (p->kv_chunk > 0) {
-        chunk_len = (p->kv_chunk + quantum - 1) / quantum * quantum;
-    } else {
-        const int64_t target = 2 * kCUs;
-        int64_t nch = std::max<int64_t>(1, (target + Y * S - 1) / (Y * S));
-        chunk_len = (int)((N + nch - 1) / nch);
-        chunk_len = (chunk_len + quantum - 1) / quantum * quantum;
-    }
-    a.chunk_len = chunk_len;
-    a.n_chunks = (int)((N + chunk_len - 1) / chunk_len);
-    pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
-    pl.ws_bytes = a.n_chunks > 1 ? (size_t)S * Y * a.n_chunks * kRows * (D + 2) * sizeof(float) : 0;
     pl.kt = k.type;
     pl.vt = v_trans ? VT_F16T : v.type;
     pl.D = (int)D;
     pl.gran = g16 ? 16 : 4;
+    const int rc = size_split(pl, p->kv_chunk, Y, S, N, NQ);
+    if (rc != FATTN_OK) return rc;
     return FATTN_OK;
 }
 
@@ -140,15 +219,14 @@ struct Events {
 
 template <int KT, int VT, int D, int GRAN, bool HM>
 int launch_split_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    using C = SplitCfg<KT, VT, D>;
     auto kern = fattn_split_kernel<KT, VT, D, GRAN, HM>;
     static bool attr_set = false;  // idempotent; benign race
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::ldsBytes);
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsPerCU);
         attr_set = true;
     }
     if (ev.begin) (void)hipEventRecord(ev.begin, st);
-    hipLaunchKernelGGL(kern, pl.grid, dim3(kSplitWaves * kWave), C::ldsBytes, st, pl.a);
+    hipLaunchKernelGGL(kern, pl.grid, dim3(kSplitWaves * kWave), pl.lds, st, pl.a);
     if (hipGetLastError() != hipSuccess) return FATTN_ERR_LAUNCH;
     if (ev.end) (void)hipEventRecord(ev.end, st);
     if (pl.a.n_chunks > 1) {
@@ -185,6 +263,13 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
 }  // namespace
 
 extern "C" {
+
+#ifdef FATTN_STAMPS
+// diagnostic build only: where the split kernel writes its phase stamps
+int fattn_debug_set_stamps(void* dev_ptr) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(void*)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 const char* fattn_version(void) { return "fattn-gfx950 0.1"; }
 
@@ -226,8 +311,8 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
     if (rc != FATTN_OK) return rc;
     if (pl.ws_bytes) {
         if (!p->workspace || p->workspace_bytes < pl.ws_bytes || (uintptr_t)p->workspace % 16) return FATTN_ERR_WORKSPACE;
-        pl.a.ws_o = (float*)p->workspace;
-        pl.a.ws_ml = (float*)((uint8_t*)p->workspace + (size_t)pl.grid.z * pl.grid.y * pl.a.n_chunks * kRows * pl.D * 4);
+        pl.a.ws_ml = (float*)p->workspace;
+        pl.a.ws_o = (float*)((uint8_t*)p->workspace + pl.ml_bytes);
     }
     hipStream_t st = (hipStream_t)stream;
     Events ev;

@@ -121,17 +121,28 @@ __device__ __forceinline__ u32x2 read8_at(const uint8_t* smem, uint32_t off) {
 // ---------------------------------------------------------------- wave reductions
 // wave64 replacements for warp_reduce_max / warp_reduce_sum (cuda_info.h:46-85).
 // Attention only needs the 4 lanes {l, l^16, l^32, l^48} that share one MFMA
-// column, so these reduce over that group.
-__device__ __forceinline__ float grp4_max(float x) {
-    x = fmaxf(x, __shfl_xor(x, 16, kWave));
-    x = fmaxf(x, __shfl_xor(x, 32, kWave));
-    return x;
+// column.  gfx950's v_permlane16_swap / v_permlane32_swap exchange rows of 16 /
+// halves of 32 lanes on the VALU (no LDS round trip like ds_bpermute):
+// swap(a=x, b=x) leaves a = x with odd rows <- even rows and b = x with even
+// rows <- odd rows, so op(a, b) is the xor-16 (resp. xor-32) reduction in every
+// lane.  Written as inline asm with both registers in/out: through the
+// __builtin_amdgcn_permlane*_swap intrinsics hipcc (ROCm 7.2) stores the first
+// result for both when the operands are copies of one value (caught by
+// tests/test_gpu_prims.py).  The s_nop covers the VALU-write -> permlane hazard,
+// which the compiler does not see inside the asm.
+__device__ __forceinline__ float xor16_pair(float x, bool is_max) {
+    float a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return is_max ? fmaxf(a, b) : a + b;
 }
-__device__ __forceinline__ float grp4_sum(float x) {
-    x += __shfl_xor(x, 16, kWave);
-    x += __shfl_xor(x, 32, kWave);
-    return x;
+__device__ __forceinline__ float xor32_pair(float x, bool is_max) {
+    float a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return is_max ? fmaxf(a, b) : a + b;
 }
+__device__ __forceinline__ float grp4_max(float x) { return xor32_pair(xor16_pair(x, true), true); }
+__device__ __forceinline__ float grp4_sum(float x) { return xor32_pair(xor16_pair(x, false), false); }
+
 __device__ __forceinline__ float wave_max(float x) {
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) x = fmaxf(x, __shfl_xor(x, m, kWave));

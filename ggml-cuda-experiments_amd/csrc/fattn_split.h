@@ -57,10 +57,14 @@ struct SplitArgs {
     int R;              // q-heads packed per tile
     int QPT;            // query rows per tile
     int n_hsub, n_qt;   // head subgroups, query-row tiles
+    float R_inv;        // 1/R: m / R == int((m + 0.5) * R_inv) exactly for m, R <= 16
     int chunk_len;      // positions per workgroup (multiple of kStep*kSplitWaves)
     int n_chunks;
+    int ncp;            // next power of two >= n_chunks (combine kernel)
     float scale_log2;   // scale * log2(e)
     int has_mask;
+    int nbuf;           // steps in flight per wave (1..4); LDS per wave = wave_bytes
+    int wave_bytes;
 };
 
 template <int KT, int VT, int D>
@@ -73,13 +77,15 @@ struct SplitCfg {
     static constexpr int vBytes = kStep * rowV;
     static constexpr int mBytes = kRows * kStep * 2;  // up to 16 distinct mask rows
     static constexpr int stepBytes = (kBytes + vBytes + mBytes + 15) / 16 * 16;
-    static constexpr int nbufRaw = 20480 / stepBytes;
-    static constexpr int NBUF = nbufRaw < 2 ? 2 : (nbufRaw > 4 ? 4 : nbufRaw);
-    static constexpr int vscBytes = (VTT == FATTN_TYPE_F16) ? 0 : kStep * (D / QK) * 2;
-    static constexpr int waveBytes = (NBUF * stepBytes + vscBytes + 15) / 16 * 16;
-    static constexpr int mergeBytes = kRows * (D + 2) * 4;
-    static_assert(waveBytes >= mergeBytes, "merge scratch must fit in a wave's buffers");
-    static constexpr int ldsBytes = kSplitWaves * waveBytes;
+    static constexpr int vscBytes = 0;
+    static constexpr int kMergeStride = D + 4;  // floats; +16 B per row spreads rows over banks
+    static constexpr int mergeBytes = kRows * kMergeStride * 4 + kRows * 2 * 4;
+    // bytes of LDS one wave needs with nbuf steps in flight
+    static constexpr int wave_bytes(int nbuf) {
+        const int w = (nbuf * stepBytes + vscBytes + 15) / 16 * 16;
+        return w > mergeBytes ? w : mergeBytes;
+    }
+    static constexpr int lds_bytes(int nbuf) { return kSplitWaves * wave_bytes(nbuf); }
 };
 
 template <int N>
@@ -90,13 +96,13 @@ __device__ __forceinline__ void wait_vmcnt_c() {
 }
 
 // wait until at most `outstanding` whole steps (NI instructions each) remain
-template <int NI, int NBUF>
+template <int NI>
 __device__ __forceinline__ void wait_steps(int outstanding) {
     switch (__builtin_amdgcn_readfirstlane(outstanding)) {
         case 0: wait_vmcnt_c<0>(); break;
         case 1: wait_vmcnt_c<NI>(); break;
-        case 2: if constexpr (NBUF > 2) wait_vmcnt_c<2 * NI>(); break;
-        default: if constexpr (NBUF > 3) wait_vmcnt_c<3 * NI>(); break;
+        case 2: wait_vmcnt_c<2 * NI>(); break;
+        default: wait_vmcnt_c<3 * NI>(); break;
     }
 }
 
@@ -197,11 +203,40 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const uint8_t* kb
     }
 }
 
+// ---------------------------------------------------------------- block scales
+// The f16 scale of block b of a raw ggml row sits at byte BB*b.  row_scales()
+// fetches the dwords holding all of a row's scales (2 x ds_read2_b32 for 4
+// blocks); scale_bits() extracts block b's 16 bits.
+template <int T, int D>
+struct RowScales {
+    uint32_t w[D / QK];
+};
+template <int T, int D>
+__device__ __forceinline__ RowScales<T, D> row_scales(const uint8_t* row) {
+    constexpr int BB = TypeInfo<T>::block_bytes;
+    RowScales<T, D> s;
+#pragma unroll
+    for (int b = 0; b < D / QK; b++) s.w[b] = *(const uint32_t*)(row + ((BB * b) & ~3));
+    return s;
+}
+template <int T, int D>
+__device__ __forceinline__ uint32_t scale_bits(const RowScales<T, D>& s, int b) {
+    constexpr int BB = TypeInfo<T>::block_bytes;
+    return ((BB * b) & 2) ? (s.w[b] >> 16) : (s.w[b] & 0xffffu);
+}
+// f16 pair {scale of row r0, scale of row r1} for block b
+template <int T, int D>
+__device__ __forceinline__ f16x2 scale_pair(const RowScales<T, D>& s0, const RowScales<T, D>& s1, int b) {
+    constexpr int BB = TypeInfo<T>::block_bytes;
+    // v_perm: low half from s0.w[b], high half from s1.w[b]
+    return as_h2(((BB * b) & 2) ? perm_b32(s1.w[b], s0.w[b], 0x07060302u) : perm_b32(s1.w[b], s0.w[b], 0x05040100u));
+}
+
 // ---------------------------------------------------------------- operands
 // K operand (A of S^T = K.Q^T) for tile t (16 rows), block/k-step b:
 // lane l -> row 16t + (l&15), elements d = 32b + 8(l>>4) + j.
 template <int KT, int D>
-__device__ __forceinline__ f16x8 k_operand(const uint8_t* kb, int row, int g, int b) {
+__device__ __forceinline__ f16x8 k_operand(const uint8_t* kb, int row, int g, int b, uint32_t dbits) {
     if constexpr (KT == FATTN_TYPE_F16) {
         constexpr int CPR = D * 2 / 16;
         const int chunk = (4 * b + g) ^ (row & (CPR - 1));
@@ -216,7 +251,7 @@ __device__ __forceinline__ f16x8 k_operand(const uint8_t* kb, int row, int g, in
             case 4: raw = read8_at<4>(kb, base + 2 + 8 * g); break;
             default: raw = read8_at<6>(kb, base + 2 + 8 * g); break;
         }
-        const f16x2 d = bcast_h(*(const uint16_t*)(kb + base));
+        const f16x2 d = bcast_h(dbits);
         f16x2 h0, h1, h2, h3;
         i8x4_to_h2x2(raw.x, h0, h1);
         i8x4_to_h2x2(raw.y, h2, h3);
@@ -235,7 +270,7 @@ __device__ __forceinline__ f16x8 k_operand(const uint8_t* kb, int row, int g, in
             default: raw = read8_at<6>(kb, base + 2 + 8 * (g & 1)); break;
         }
         const uint32_t sh = (g >> 1) * 4;
-        const f16x2 d = bcast_h(*(const uint16_t*)(kb + base));
+        const f16x2 d = bcast_h(dbits);
         f16x2 h0, h1, h2, h3;
         u4x4_to_h2x2((raw.x >> sh) & 0x0F0F0F0Fu, h0, h1);
         u4x4_to_h2x2((raw.y >> sh) & 0x0F0F0F0Fu, h2, h3);
@@ -279,40 +314,94 @@ __device__ __forceinline__ f16x8 v_operand_f16(const uint8_t* vb, int c, int g, 
     }
 }
 
+// ---------------------------------------------------------------- tile geometry
+// A tile packs rows m = (query row m / R, head m % R).  No runtime integer
+// division (hipcc expands those into long scalar loops).
+__device__ __forceinline__ int div_R(const SplitArgs& a, int m) { return (int)(((float)m + 0.5f) * a.R_inv); }
+
+// number of valid rows of tile (qt, hs); they form a prefix [0, rv)
+__device__ __forceinline__ int tile_rows(const SplitArgs& a, int qt, int hs) {
+    const int rows_q = min(a.QPT, a.NQ - qt * a.QPT);
+    const int heads = min(a.R, a.rk2 - hs * a.R);
+    return rows_q * heads;  // heads < R only when R == 16 (then QPT == 1)
+}
+
+// ---------------------------------------------------------------- diagnostics
+// Diagnostic build only (-DFATTN_STAMPS, libfattn_stamps.so): lane 0 of every
+// wave records s_memrealtime (100 MHz) at phase boundaries into g_stamps
+// [block][wave][8].  No stamp executes in the product library.
+#ifdef FATTN_STAMPS
+__device__ unsigned long long* g_stamps;
+#define FATTN_STAMP(k)                                                                          \
+    do {                                                                                        \
+        if (lane == 0 && g_stamps) {                                                            \
+            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                     \
+            const int64_t blk_ = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
+            g_stamps[(blk_ * kSplitWaves + wave) * 8 + (k)] = t_;                                \
+        }                                                                                       \
+    } while (0)
+#else
+#define FATTN_STAMP(k) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------- kernel
 
 template <int KT, int VT, int D, int GRAN, bool HM>
-__global__ __launch_bounds__(kSplitWaves * kWave, 2) void fattn_split_kernel(const SplitArgs a) {
+__global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4) ? 2 : 4) void fattn_split_kernel(
+    const SplitArgs a) {
     using C = SplitCfg<KT, VT, D>;
     using P = StepPlan<KT, VT, D, GRAN>;
     constexpr int NI = P::NIKV + (HM ? P::NIM : 0);  // VMEM instructions per step
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NB = D / QK;   // 32-wide k-steps of QK^T (= ggml blocks per row)
-    constexpr int NC = D / 16;   // 16-wide output column groups
+    constexpr int NC = D / 16;   // 16-wide output column groups (MFMA tiles of O^T)
     constexpr float kNegInf = -__builtin_inff();
+    constexpr bool kVQ8 = C::VTT == FATTN_TYPE_Q8_0;
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int g = lane >> 4;
     const int i16 = lane & 15;
+    FATTN_STAMP(0);
 
     // ---- tile decode: y -> (kv head, head subgroup, query-row tile)
     const int chunk = blockIdx.x;
     const int y = blockIdx.y;
     const int iq3 = blockIdx.z;
-    const int qt = y % a.n_qt;
-    const int hs = (y / a.n_qt) % a.n_hsub;
-    const int ik2 = y / (a.n_qt * a.n_hsub);
-    const int ik3 = iq3 / a.rk3;
+    int qt = 0, hs = 0, ik2 = y, ik3 = iq3;  // common case without runtime division
+    if (a.n_qt != 1 || a.n_hsub != 1) {
+        qt = y % a.n_qt;
+        hs = (y / a.n_qt) % a.n_hsub;
+        ik2 = y / (a.n_qt * a.n_hsub);
+    }
+    if (a.rk3 != 1) ik3 = iq3 / a.rk3;
 
     // this lane's MFMA column m = i16 -> (query row, q head)
     const int m = i16;
-    const int mq = m / a.R;
-    const int mh = hs * a.R + (m % a.R);
+    const int mq = div_R(a, m);
+    const int mh = hs * a.R + (m - mq * a.R);
     const int iq1 = qt * a.QPT + mq;
     const int iq2 = ik2 * a.rk2 + mh;
     const bool row_ok = (m < a.QPT * a.R) && (iq1 < a.NQ) && (mh < a.rk2);
 
+    // ---- this wave's KV slice
+    const int wl = a.chunk_len / kSplitWaves;
+    const int c_hi = min(a.N, (chunk + 1) * a.chunk_len);
+    const int w_lo = chunk * a.chunk_len + wave * wl;
+    const int w_hi = min(c_hi, w_lo + wl);
+    const int nsteps = w_hi > w_lo ? (w_hi - w_lo + kStep - 1) / kStep : 0;
+    const int nbuf = a.nbuf;
+
+    const uint8_t* kbase = a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3;
+    const uint8_t* vbase = a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3;
+    uint8_t* wbuf = smem + wave * a.wave_bytes;
+    const int mrow0 = qt * a.QPT;
+
+    for (int s = 0; s < nbuf && s < nsteps; s++) {
+        issue_step<KT, VT, D, GRAN, HM>(a, kbase, vbase, w_lo + s * kStep, mrow0, wbuf + s * C::stepBytes, lane);
+    }
+
+    FATTN_STAMP(1);
     // ---- Q^T operand (B of S^T = K.Q^T), rounded to f16 like src/utils.h:10
     f16x8 qop[NB];
     {
@@ -329,25 +418,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave, 2) void fattn_split_kernel(con
             qop[b] = row_ok ? h : z;
         }
     }
-    // all ordinary global loads retire before the first LDS-DMA is issued
+    // Q is loaded after the first steps' LDS-DMA is in flight, so the HBM stream
+    // starts at once; waiting for Q (the youngest loads) retires those steps too
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-    // ---- this wave's KV slice
-    const int wl = a.chunk_len / kSplitWaves;
-    const int c_hi = min(a.N, (chunk + 1) * a.chunk_len);
-    const int w_lo = chunk * a.chunk_len + wave * wl;
-    const int w_hi = min(c_hi, w_lo + wl);
-    const int nsteps = w_hi > w_lo ? (w_hi - w_lo + kStep - 1) / kStep : 0;
-
-    const uint8_t* kbase = a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3;
-    const uint8_t* vbase = a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3;
-    uint8_t* wbuf = smem + wave * C::waveBytes;
-    uint8_t* vsc = wbuf + C::NBUF * C::stepBytes;
-    const int mrow0 = qt * a.QPT;
-
-    for (int s = 0; s < C::NBUF && s < nsteps; s++) {
-        issue_step<KT, VT, D, GRAN, HM>(a, kbase, vbase, w_lo + s * kStep, mrow0, wbuf + s * C::stepBytes, lane);
-    }
 
     float m_run = kNegInf;  // running max (log2 domain) of column m
     float l_run = 0.0f;     // this lane's partial row sum
@@ -356,39 +429,43 @@ __global__ __launch_bounds__(kSplitWaves * kWave, 2) void fattn_split_kernel(con
     for (int c = 0; c < NC; c++) o[c] = f32x4{0, 0, 0, 0};
 
     const float log2e = 1.4426950408889634f;
+    int cur = 0;  // buffer of step s
     for (int s = 0; s < nsteps; s++) {
-        wait_steps<NI, C::NBUF>(min(C::NBUF - 1, nsteps - 1 - s));
-        const uint8_t* buf = wbuf + (s % C::NBUF) * C::stepBytes;
+        wait_steps<NI>(min(nbuf - 1, nsteps - 1 - s));
+        if (s == 0) FATTN_STAMP(2);
+#ifdef FATTN_DIAG_NOCOMPUTE
+        // diagnostic build only: memory-side ceiling of this access pattern
+        if (s + nbuf < nsteps) {
+            issue_step<KT, VT, D, GRAN, HM>(a, kbase, vbase, w_lo + (s + nbuf) * kStep, mrow0,
+                                            wbuf + cur * C::stepBytes, lane);
+        }
+        cur = (cur + 1 == nbuf) ? 0 : cur + 1;
+        continue;
+#endif
+        const uint8_t* buf = wbuf + cur * C::stepBytes;
         const uint8_t* kb = buf;
         const uint8_t* vb = buf + C::kBytes;
         const uint8_t* mb = buf + C::kBytes + C::vBytes;
         const int n0 = w_lo + s * kStep;
         const int nvalid = min(kStep, w_hi - n0);
 
-        // -- V scales -> compact [b][row] f16 array (quantised V only)
-        if constexpr (C::vscBytes > 0) {
-            constexpr int E = kStep * NB;
-#pragma unroll
-            for (int e0 = 0; e0 < E; e0 += kWave) {
-                const int e = e0 + lane;
-                if (e < E) {
-                    const int row = e % kStep, b = e / kStep;
-                    const uint16_t sc = *(const uint16_t*)(vb + row * C::rowV + b * TypeInfo<C::VTT>::block_bytes);
-                    *(uint16_t*)(vsc + (b * kStep + row) * 2) = sc;
-                }
-            }
-        }
-
         // -- S^T = K.Q^T for the two 16-row tiles
         f32x4 st[2];
 #pragma unroll
         for (int t = 0; t < 2; t++) {
             st[t] = f32x4{0, 0, 0, 0};
+            if constexpr (KT == FATTN_TYPE_F16) {
 #pragma unroll
-            for (int b = 0; b < NB; b++) st[t] = mfma16(k_operand<KT, D>(kb, 16 * t + i16, g, b), qop[b], st[t]);
+                for (int b = 0; b < NB; b++) st[t] = mfma16(k_operand<KT, D>(kb, 16 * t + i16, g, b, 0), qop[b], st[t]);
+            } else {
+                const RowScales<KT, D> ks = row_scales<KT, D>(kb + (16 * t + i16) * C::rowK);
+#pragma unroll
+                for (int b = 0; b < NB; b++)
+                    st[t] = mfma16(k_operand<KT, D>(kb, 16 * t + i16, g, b, scale_bits(ks, b)), qop[b], st[t]);
+            }
         }
 
-        // -- scale + mask (log2 domain), tail positions -> -inf
+        // -- scale + mask (log2 domain); positions past this wave's slice -> -inf
         float sv[8];
 #pragma unroll
         for (int t = 0; t < 2; t++) {
@@ -401,31 +478,28 @@ __global__ __launch_bounds__(kSplitWaves * kWave, 2) void fattn_split_kernel(con
             }
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int pos = 16 * t + 4 * g + r;
                 const float x = st[t][r] * a.scale_log2 + mk[r] * log2e;
-                sv[4 * t + r] = pos < nvalid ? x : kNegInf;
+                sv[4 * t + r] = (16 * t + 4 * g + r) < nvalid ? x : kNegInf;
             }
         }
 
-        // -- online softmax for column m (4 lanes share it)
-        float tmax = sv[0];
-#pragma unroll
-        for (int j = 1; j < 8; j++) tmax = fmaxf(tmax, sv[j]);
+        // -- online softmax for column m (the 4 lanes l, l^16, l^32, l^48 share it)
+        float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
+                           fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
         tmax = grp4_max(tmax);
         const float m_new = fmaxf(m_run, tmax);
         const float m_use = (m_new == kNegInf) ? 0.0f : m_new;
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+        if (__builtin_amdgcn_ballot_w64(m_new != m_run)) {  // rescale only when a max moved
+            const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+            l_run *= alpha;
+#pragma unroll
+            for (int c = 0; c < NC; c++) o[c] *= alpha;
+        }
         m_run = m_new;
-        float psum = 0.0f;
         float pv[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            pv[j] = __builtin_amdgcn_exp2f(sv[j] - m_use);
-            psum += pv[j];
-        }
-        l_run = l_run * alpha + psum;
-#pragma unroll
-        for (int c = 0; c < NC; c++) o[c] *= alpha;
+        for (int j = 0; j < 8; j++) pv[j] = __builtin_amdgcn_exp2f(sv[j] - m_use);
+        l_run += ((pv[0] + pv[1]) + (pv[2] + pv[3])) + ((pv[4] + pv[5]) + (pv[6] + pv[7]));
 
         f16x8 pb;
         pb.s0 = (f16)pv[0]; pb.s1 = (f16)pv[1]; pb.s2 = (f16)pv[2]; pb.s3 = (f16)pv[3];
@@ -436,98 +510,111 @@ __global__ __launch_bounds__(kSplitWaves * kWave, 2) void fattn_split_kernel(con
 #pragma unroll
             for (int c = 0; c < NC; c++) o[c] = mfma16(v_operand_f16<VT, D>(vb, c, g, i16), pb, o[c]);
         } else {
-            const bool tail = nvalid < kStep;
+            const int rA = 4 * g, rB = 16 + 4 * g;
+            // scales of this lane's 8 rows (4g..4g+3, 16+4g..16+4g+3), all blocks
+            RowScales<C::VTT, D> vs[8];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                vs[r] = row_scales<C::VTT, D>(vb + (rA + r) * C::rowV);
+                vs[4 + r] = row_scales<C::VTT, D>(vb + (rB + r) * C::rowV);
+            }
 #pragma unroll
             for (int b = 0; b < NB; b++) {
-                // scales of rows 4g..4g+3 and 16+4g..16+4g+3 for block b
-                const u32x2 s0 = *(const u32x2*)(vsc + (b * kStep + 4 * g) * 2);
-                const u32x2 s1 = *(const u32x2*)(vsc + (b * kStep + 16 + 4 * g) * 2);
-                const f16x2 d01 = as_h2(s0.x), d23 = as_h2(s0.y), d45 = as_h2(s1.x), d67 = as_h2(s1.y);
+                const f16x2 d01 = scale_pair(vs[0], vs[1], b), d23 = scale_pair(vs[2], vs[3], b);
+                const f16x2 d45 = scale_pair(vs[4], vs[5], b), d67 = scale_pair(vs[6], vs[7], b);
                 constexpr int BB = TypeInfo<C::VTT>::block_bytes;
-                const uint8_t* col = vb + b * BB + 2;
-                const int rA = 4 * g, rB = 16 + 4 * g;
-                if constexpr (C::VTT == FATTN_TYPE_Q8_0) {
+                if constexpr (kVQ8) {
+                    // one u16 per row carries columns 2i (-> tile E_b) and 2i+1 (-> tile O_b)
+                    const uint8_t* cp = vb + b * BB + 2 + 2 * i16;
+                    uint32_t w[8];
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const uint8_t* cp = col + 16 * h + i16;
-                        uint32_t x0 = lds_u8_pair(cp + (rA + 0) * C::rowV, cp + (rA + 1) * C::rowV);
-                        uint32_t x1 = lds_u8_pair(cp + (rA + 2) * C::rowV, cp + (rA + 3) * C::rowV);
-                        uint32_t x2 = lds_u8_pair(cp + (rB + 0) * C::rowV, cp + (rB + 1) * C::rowV);
-                        uint32_t x3 = lds_u8_pair(cp + (rB + 2) * C::rowV, cp + (rB + 3) * C::rowV);
-                        const f16x2 off = {(f16)-1152.0f, (f16)-1152.0f};
-                        f16x2 v0 = (as_h2(x0 ^ 0x64806480u) + off) * d01;
-                        f16x2 v1 = (as_h2(x1 ^ 0x64806480u) + off) * d23;
-                        f16x2 v2 = (as_h2(x2 ^ 0x64806480u) + off) * d45;
-                        f16x2 v3 = (as_h2(x3 ^ 0x64806480u) + off) * d67;
-                        if (tail) {
-                            const f16x2 z = {0, 0};
-                            v0 = (rA + 1 < nvalid) ? v0 : ((rA < nvalid) ? f16x2{v0.x, 0} : z);
-                            v1 = (rA + 3 < nvalid) ? v1 : ((rA + 2 < nvalid) ? f16x2{v1.x, 0} : z);
-                            v2 = (rB + 1 < nvalid) ? v2 : ((rB < nvalid) ? f16x2{v2.x, 0} : z);
-                            v3 = (rB + 3 < nvalid) ? v3 : ((rB + 2 < nvalid) ? f16x2{v3.x, 0} : z);
-                        }
-                        f16x8 av;
-                        av.s01 = v0; av.s23 = v1; av.s45 = v2; av.s67 = v3;
-                        o[2 * b + h] = mfma16(av, pb, o[2 * b + h]);
+                    for (int r = 0; r < 4; r++) {
+                        w[r] = *(const uint16_t*)(cp + (rA + r) * C::rowV);
+                        w[4 + r] = *(const uint16_t*)(cp + (rB + r) * C::rowV);
                     }
-                } else {  // Q4_0: both nibbles of one byte feed column groups 2b and 2b+1
-                    const uint8_t* cp = col + i16;
-                    const uint32_t x0 = lds_u8_pair(cp + (rA + 0) * C::rowV, cp + (rA + 1) * C::rowV);
-                    const uint32_t x1 = lds_u8_pair(cp + (rA + 2) * C::rowV, cp + (rA + 3) * C::rowV);
-                    const uint32_t x2 = lds_u8_pair(cp + (rB + 0) * C::rowV, cp + (rB + 1) * C::rowV);
-                    const uint32_t x3 = lds_u8_pair(cp + (rB + 2) * C::rowV, cp + (rB + 3) * C::rowV);
+                    f16x8 ae, ao;
+                    const f16x2 off = {(f16)-1152.0f, (f16)-1152.0f};
+                    const f16x2 dd[4] = {d01, d23, d45, d67};
+#pragma unroll
+                    for (int pr = 0; pr < 4; pr++) {
+                        // bytes [e_r, o_r, e_r+1, o_r+1] -> xor 0x80 -> f16 magic 0x64xx
+                        const uint32_t t2 = (w[2 * pr] | (w[2 * pr + 1] << 16)) ^ 0x80808080u;
+                        const f16x2 ve = (as_h2(perm_b32(0x64646464u, t2, 0x04020400u)) + off) * dd[pr];
+                        const f16x2 vo = (as_h2(perm_b32(0x64646464u, t2, 0x04030401u)) + off) * dd[pr];
+                        ae[2 * pr] = ve.x; ae[2 * pr + 1] = ve.y;
+                        ao[2 * pr] = vo.x; ao[2 * pr + 1] = vo.y;
+                    }
+                    o[2 * b] = mfma16(ae, pb, o[2 * b]);
+                    o[2 * b + 1] = mfma16(ao, pb, o[2 * b + 1]);
+                } else {  // Q4_0: byte i carries column i (low nibble) and 16+i (high nibble)
+                    const uint8_t* cp = vb + b * BB + 2 + i16;
+                    uint32_t w[8];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        w[r] = cp[(rA + r) * C::rowV];
+                        w[4 + r] = cp[(rB + r) * C::rowV];
+                    }
+                    f16x8 al, ah;
                     const f16x2 off = {(f16)-1032.0f, (f16)-1032.0f};
+                    const f16x2 dd[4] = {d01, d23, d45, d67};
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const int sh = 4 * h;
-                        f16x2 v0 = (as_h2(((x0 >> sh) & 0x000F000Fu) | 0x64006400u) + off) * d01;
-                        f16x2 v1 = (as_h2(((x1 >> sh) & 0x000F000Fu) | 0x64006400u) + off) * d23;
-                        f16x2 v2 = (as_h2(((x2 >> sh) & 0x000F000Fu) | 0x64006400u) + off) * d45;
-                        f16x2 v3 = (as_h2(((x3 >> sh) & 0x000F000Fu) | 0x64006400u) + off) * d67;
-                        if (tail) {
-                            const f16x2 z = {0, 0};
-                            v0 = (rA + 1 < nvalid) ? v0 : ((rA < nvalid) ? f16x2{v0.x, 0} : z);
-                            v1 = (rA + 3 < nvalid) ? v1 : ((rA + 2 < nvalid) ? f16x2{v1.x, 0} : z);
-                            v2 = (rB + 1 < nvalid) ? v2 : ((rB < nvalid) ? f16x2{v2.x, 0} : z);
-                            v3 = (rB + 3 < nvalid) ? v3 : ((rB + 2 < nvalid) ? f16x2{v3.x, 0} : z);
-                        }
-                        f16x8 av;
-                        av.s01 = v0; av.s23 = v1; av.s45 = v2; av.s67 = v3;
-                        o[2 * b + h] = mfma16(av, pb, o[2 * b + h]);
+                    for (int pr = 0; pr < 4; pr++) {
+                        const uint32_t x = w[2 * pr] | (w[2 * pr + 1] << 16);
+                        const f16x2 vl = (as_h2((x & 0x000F000Fu) | 0x64006400u) + off) * dd[pr];
+                        const f16x2 vh = (as_h2(((x >> 4) & 0x000F000Fu) | 0x64006400u) + off) * dd[pr];
+                        al[2 * pr] = vl.x; al[2 * pr + 1] = vl.y;
+                        ah[2 * pr] = vh.x; ah[2 * pr + 1] = vh.y;
                     }
+                    o[2 * b] = mfma16(al, pb, o[2 * b]);
+                    o[2 * b + 1] = mfma16(ah, pb, o[2 * b + 1]);
                 }
             }
         }
 
-        // -- refill this buffer with step s + NBUF
-        if (s + C::NBUF < nsteps) {
+        // -- refill this buffer with step s + nbuf
+        if (s + nbuf < nsteps) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            issue_step<KT, VT, D, GRAN, HM>(a, kbase, vbase, w_lo + (s + C::NBUF) * kStep, mrow0,
-                                        wbuf + (s % C::NBUF) * C::stepBytes, lane);
+            issue_step<KT, VT, D, GRAN, HM>(a, kbase, vbase, w_lo + (s + nbuf) * kStep, mrow0,
+                                            wbuf + cur * C::stepBytes, lane);
         }
+        cur = (cur + 1 == nbuf) ? 0 : cur + 1;
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    FATTN_STAMP(3);
 
-    // ---- per-wave state -> LDS (this wave's own buffers), then merge 4 waves
+    // ---- per-wave state -> LDS (this wave's own region), then merge the 4 waves
     const float l_tot = grp4_sum(l_run);
-    float* mo = (float*)wbuf;                 // [16][D]
-    float* mml = (float*)(wbuf + kRows * D * 4);  // [16][2]
+    constexpr int MS = C::kMergeStride;
+    float* mo = (float*)wbuf;                      // [16][MS]
+    float* mml = (float*)(wbuf + kRows * MS * 4);  // [16][2]
+    if constexpr (kVQ8) {
+        // tile E_b holds columns 32b + 2(4g+reg), O_b the odd neighbours
 #pragma unroll
-    for (int c = 0; c < NC; c++) *(f32x4*)(mo + m * D + 16 * c + 4 * g) = o[c];
+        for (int b = 0; b < NB; b++) {
+            const f32x4 e = o[2 * b], od = o[2 * b + 1];
+            *(f32x4*)(mo + m * MS + 32 * b + 8 * g) = f32x4{e.x, od.x, e.y, od.y};
+            *(f32x4*)(mo + m * MS + 32 * b + 8 * g + 4) = f32x4{e.z, od.z, e.w, od.w};
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < NC; c++) *(f32x4*)(mo + m * MS + 16 * c + 4 * g) = o[c];
+    }
     if (g == 0) {
         mml[2 * m] = m_run;
         mml[2 * m + 1] = l_tot;
     }
     __syncthreads();
+    FATTN_STAMP(4);
 
     constexpr int EPT = D / 16;  // outputs per thread: 16 rows x D over 256 threads
     const int tm = threadIdx.x / 16;
-    const int d0 = (threadIdx.x % 16) * EPT;
+    const int tj = threadIdx.x % 16;
+    const int d0 = tj * EPT;
     float M = kNegInf;
     float mw[kSplitWaves], lw[kSplitWaves];
 #pragma unroll
     for (int w = 0; w < kSplitWaves; w++) {
-        const float* ml = (const float*)(smem + w * C::waveBytes + kRows * D * 4);
+        const float* ml = (const float*)(smem + w * a.wave_bytes + kRows * MS * 4);
         mw[w] = ml[2 * tm];
         lw[w] = ml[2 * tm + 1];
         M = fmaxf(M, mw[w]);
@@ -540,75 +627,143 @@ __global__ __launch_bounds__(kSplitWaves * kWave, 2) void fattn_split_kernel(con
     for (int w = 0; w < kSplitWaves; w++) {
         const float wt = (mw[w] == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mw[w] - M);
         L += wt * lw[w];
-        const float* ow = (const float*)(smem + w * C::waveBytes) + tm * D + d0;
+        const float* ow = (const float*)(smem + w * a.wave_bytes) + tm * MS + d0;
 #pragma unroll
         for (int e = 0; e < EPT; e++) acc[e] += wt * ow[e];
     }
 
-    // row validity for the merged row tm
-    const int tq = tm / a.R;
-    const int th = hs * a.R + (tm % a.R);
-    const int tiq1 = qt * a.QPT + tq;
-    const int tiq2 = ik2 * a.rk2 + th;
-    const bool t_ok = (tm < a.QPT * a.R) && (tiq1 < a.NQ) && (th < a.rk2);
-    if (!t_ok) return;
+    // valid rows of this tile form a prefix [0, rv)
+    const int rv = tile_rows(a, qt, hs);
+    auto dst_row = [&](int r) -> float* {
+        const int rq = div_R(a, r);
+        const int riq1 = qt * a.QPT + rq;
+        const int riq2 = ik2 * a.rk2 + hs * a.R + (r - rq * a.R);
+        return a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D;
+    };
     if (a.n_chunks == 1) {
-        float* out = a.dst + (((int64_t)iq3 * a.NQ + tiq1) * a.H + tiq2) * D + d0;
-        const float inv = 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
+        if (tm < rv) {
+            float* out = dst_row(tm) + d0;
+            const float inv = 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
 #pragma unroll
-        for (int e = 0; e < EPT; e++) out[e] = (L == 0.0f) ? __builtin_nanf("") : acc[e] * inv;
-    } else {
-        const int64_t slot = (((int64_t)iq3 * gridDim.y + y) * a.n_chunks + chunk) * kRows + tm;
-        float* wo = a.ws_o + slot * D + d0;
-#pragma unroll
-        for (int e = 0; e < EPT; e++) wo[e] = acc[e];
-        if (d0 == 0) {
-            a.ws_ml[2 * slot] = M;
-            a.ws_ml[2 * slot + 1] = L;
+            for (int e = 0; e < EPT; e += 4) {
+                f32x4 v;
+                v.x = L == 0.0f ? __builtin_nanf("") : acc[e] * inv;
+                v.y = L == 0.0f ? __builtin_nanf("") : acc[e + 1] * inv;
+                v.z = L == 0.0f ? __builtin_nanf("") : acc[e + 2] * inv;
+                v.w = L == 0.0f ? __builtin_nanf("") : acc[e + 3] * inv;
+                *(f32x4*)(out + e) = v;
+            }
         }
+        return;
     }
+
+    // ---- several chunks: plain stores of this chunk's partial; fattn_combine_kernel
+    // (next launch on the stream) merges them -- the kernel boundary publishes.
+    if (tm < rv) {
+        const int64_t slot = (((int64_t)iq3 * gridDim.y + y) * a.n_chunks + chunk) * kRows + tm;
+#pragma unroll
+        for (int e = 0; e < EPT; e += 4) *(f32x4*)(a.ws_o + slot * D + d0 + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
+        if (tj == 0) *(float2*)(a.ws_ml + 2 * slot) = float2{M, L};
+    }
+    FATTN_STAMP(5);
 }
 
 // ---------------------------------------------------------------- combine
 // Log-sum-exp merge of the chunk partials (fa_reduce, flash_row_float.h:415-472,
-// in fp32 and parallel over the head dimension instead of one serial lane).
+// in fp32 and parallel).  One workgroup per (y, z) tile; only its rv valid rows.
+// 16 thread groups = rv rows x G chunk subsets; every thread issues all of its
+// loads (O partials + (m, l) pairs) before consuming any: one memory round trip.
 template <int D>
 __global__ __launch_bounds__(256) void fattn_combine_kernel(const SplitArgs a) {
     constexpr float kNegInf = -__builtin_inff();
     constexpr int EPT = D / 16;
-    const int y = blockIdx.x;
-    const int iq3 = blockIdx.y;
-    const int tm = threadIdx.x / 16;
-    const int d0 = (threadIdx.x % 16) * EPT;
-    const int qt = y % a.n_qt;
-    const int hs = (y / a.n_qt) % a.n_hsub;
-    const int ik2 = y / (a.n_qt * a.n_hsub);
-    const int tq = tm / a.R;
-    const int th = hs * a.R + (tm % a.R);
-    const int tiq1 = qt * a.QPT + tq;
-    const int tiq2 = ik2 * a.rk2 + th;
-    const bool t_ok = (tm < a.QPT * a.R) && (tiq1 < a.NQ) && (th < a.rk2);
-    if (!t_ok) return;
-    const int64_t base = ((int64_t)iq3 * gridDim.x + y) * a.n_chunks;
-    float M = kNegInf;
-    for (int c = 0; c < a.n_chunks; c++) M = fmaxf(M, a.ws_ml[2 * ((base + c) * kRows + tm)]);
-    float L = 0.0f;
-    float acc[EPT];
-#pragma unroll
-    for (int e = 0; e < EPT; e++) acc[e] = 0.0f;
-    for (int c = 0; c < a.n_chunks; c++) {
-        const int64_t slot = (base + c) * kRows + tm;
-        const float mc = a.ws_ml[2 * slot];
-        const float wt = (mc == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mc - M);
-        L += wt * a.ws_ml[2 * slot + 1];
-        const float* wo = a.ws_o + slot * D + d0;
-#pragma unroll
-        for (int e = 0; e < EPT; e++) acc[e] += wt * wo[e];
+    constexpr int MAXC = 64 / EPT * 2;  // max chunks one thread folds (register budget)
+    __shared__ float red[kRows][D];
+    __shared__ float wts[kRows][64];
+    __shared__ float rowML[kRows][2];
+    const int y = blockIdx.x, iq3 = blockIdx.y;
+    int qt = 0, hs = 0, ik2 = y;
+    if (a.n_qt != 1 || a.n_hsub != 1) {
+        qt = y % a.n_qt;
+        hs = (y / a.n_qt) % a.n_hsub;
+        ik2 = y / (a.n_qt * a.n_hsub);
     }
-    float* out = a.dst + (((int64_t)iq3 * a.NQ + tiq1) * a.H + tiq2) * D + d0;
-    const float inv = 1.0f / L;
+    const int rv = tile_rows(a, qt, hs);
+    const int NCH = a.n_chunks;
+    const int G = max(1, kRows / max(rv, 1));
+    const int grp = threadIdx.x / 16, tj = threadIdx.x % 16, d0 = tj * EPT;
+    const int64_t sb = ((int64_t)iq3 * gridDim.x + y) * NCH;
+    // (1) issue every load first
+    float v[MAXC][EPT];
+    const int r = grp / G, cg = grp % G;
+    const bool active = grp < rv * G;
+    // loads are unconditional (chunk index clamped, weight zeroed below): a
+    // guarded load would make hipcc branch + wait vmcnt(0) per load
+    const int kmax = active ? (NCH - cg + G - 1) / G : 0;
+    {
+        const int rr = active ? r : 0;
 #pragma unroll
-    for (int e = 0; e < EPT; e++) out[e] = (L == 0.0f) ? __builtin_nanf("") : acc[e] * inv;
+        for (int k = 0; k < MAXC; k++) {
+            const int c = min(cg + k * G, NCH - 1);
+            const float* wo = a.ws_o + ((sb + c) * kRows + rr) * D + d0;
+#pragma unroll
+            for (int e = 0; e < EPT; e += 4) {
+                const f32x4 x = *(const f32x4*)(wo + e);
+                v[k][e] = x.x; v[k][e + 1] = x.y; v[k][e + 2] = x.z; v[k][e + 3] = x.w;
+            }
+        }
+    }
+    // (2) (m, l) of chunk c of row r lives in thread r * NCP + c (NCP = next
+    // power of two >= NCH, <= 64): segmented xor-reductions inside one wave give
+    // each row's max and normaliser in a fixed order (deterministic).
+    const int NCP = a.ncp;
+    const int mr = threadIdx.x / NCP, mc = threadIdx.x % NCP;
+    float mv = kNegInf, lv = 0.0f;
+    if (mr < rv && mc < NCH) {
+        const float2 x = *(const float2*)(a.ws_ml + 2 * ((sb + mc) * kRows + mr));
+        mv = x.x;
+        lv = x.y;
+    }
+    float Mr = mv;
+    for (int o = 1; o < NCP; o <<= 1) Mr = fmaxf(Mr, __shfl_xor(Mr, o, kWave));
+    const float wt = (mv == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mv - Mr);
+    float Lr = wt * lv;
+    for (int o = 1; o < NCP; o <<= 1) Lr += __shfl_xor(Lr, o, kWave);
+    if (mr < rv) {
+        wts[mr][mc] = wt;
+        if (mc == 0) rowML[mr][1] = Lr;
+    }
+    __syncthreads();
+    // (3) fold this thread's chunks
+    if (active) {
+        float s8[EPT];
+#pragma unroll
+        for (int e = 0; e < EPT; e++) s8[e] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < MAXC; k++) {
+            const float wt = k < kmax ? wts[r][min(cg + k * G, NCH - 1)] : 0.0f;
+#pragma unroll
+            for (int e = 0; e < EPT; e++) s8[e] += wt * v[k][e];
+        }
+#pragma unroll
+        for (int e = 0; e < EPT; e++) red[grp][d0 + e] = s8[e];
+    }
+    __syncthreads();
+    // (4) sum the G subsets of each row, normalise, store
+    if (grp < rv) {
+        const float Lr = rowML[grp][1];
+        const float inv = 1.0f / Lr;
+        const int rq = div_R(a, grp);
+        const int riq1 = qt * a.QPT + rq;
+        const int riq2 = ik2 * a.rk2 + hs * a.R + (grp - rq * a.R);
+        float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + d0;
+#pragma unroll
+        for (int e = 0; e < EPT; e++) {
+            float x = 0.0f;
+            for (int k = 0; k < G; k++) x += red[grp * G + k][d0 + e];
+            out[e] = (Lr == 0.0f) ? __builtin_nanf("") : x * inv;
+        }
+    }
 }
 
 }  // namespace fattn

@@ -17,7 +17,7 @@ from dataclasses import dataclass
 from typing import Optional, Sequence
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_PKG_DIR, "..", "lib", "libfattn.so"))
+LIB_PATH = os.path.normpath(os.path.join(_PKG_DIR, "..", "lib", os.environ.get("FATTN_LIB", "libfattn.so")))
 
 # ggml_type numbering (include/fattn.h)
 TYPE_F32, TYPE_F16, TYPE_Q4_0, TYPE_Q8_0 = 0, 1, 2, 8
