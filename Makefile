@@ -23,8 +23,30 @@ $(LIB): $(CSRC) $(CHDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared $(CSRC) -o $@
 
-# diagnostic library with per-wave phase stamps (tools/stamps.py); never loaded by the product path
-stamps: $(LIBDIR)/libfattn_stamps.so $(LIBDIR)/libfattn_nocompute.so
+# diagnostic libraries (tools/stamps.py, tools/variants.py); never loaded by the product path
+stamps: $(LIBDIR)/libfattn_stamps.so $(LIBDIR)/libfattn_nocompute.so $(LIBDIR)/libfattn_nc.so \
+        $(LIBDIR)/libfattn_nctail.so $(LIBDIR)/libfattn_notail.so $(LIBDIR)/libfattn_nopub.so \
+        $(LIBDIR)/libfattn_noatomic.so
+
+$(LIBDIR)/libfattn_nopub.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DIAG_NOPUBLISH -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_noatomic.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DIAG_NOATOMIC -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_nc.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DIAG_NOCOMPUTE -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_nctail.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DIAG_NOCOMPUTE -DFATTN_DIAG_NOTAIL -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_notail.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DIAG_NOTAIL -shared $(CSRC) -o $@
 
 $(LIBDIR)/libfattn_nocompute.so: $(CSRC) $(CHDR)
 	@mkdir -p $(LIBDIR)

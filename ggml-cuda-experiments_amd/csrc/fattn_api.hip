@@ -31,7 +31,7 @@ struct Plan {
     int gran;
     dim3 grid;
     int lds;
-    size_t ws_bytes, ml_bytes;
+    size_t ws_bytes, cnt_bytes, ml_bytes;
 };
 
 // LDS geometry of one instantiation (type-erased for the planner)
@@ -63,14 +63,12 @@ Geom geom(int kt, int vt, int D) {
 
 constexpr int kLdsPerCU = 163840;
 
-// fattn_combine_kernel limits: one (chunk, row) pair per thread for the (m, l)
-// loads and at most MAXC chunks folded per thread
+// combine_tile limits: one (chunk, row) pair per thread for the (m, l) loads
 bool combine_ok(int64_t nch, int rv, int D) {
-    const int ept = D / 16, maxc = 64 / ept * 2;
-    const int G = std::max(1, kRows / std::max(rv, 1));
+    (void)D;
     int ncp = 1;
     while (ncp < nch) ncp <<= 1;
-    return nch <= 64 && ncp * rv <= 256 && (nch + G - 1) / G <= maxc;
+    return nch <= 64 && ncp * rv <= 256;
 }
 
 // Split-KV sizing for 256 CUs.  Every wave streams `spw` steps of 32 positions;
@@ -115,10 +113,16 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     pl.lds = G.lds_bytes(nbuf);
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     if (a.n_chunks > 1) {
+        // [arrival counters, one 256-B line per tile][(m, l) pairs][O partials];
+        // zero-filled once per allocation: each launch re-arms the counters
+        pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
         pl.ml_bytes = ((size_t)S * Y * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
-        pl.ws_bytes = pl.ml_bytes + (size_t)S * Y * a.n_chunks * kRows * pl.D * sizeof(float);
+        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + (size_t)S * Y * a.n_chunks * kRows * pl.D * 4;
+        // the chunk-0 merge reuses the kernel's LDS
+        const int need = pl.D == 128 ? combine_lds_bytes<128>() : combine_lds_bytes<64>();
+        if (pl.lds < need) return FATTN_ERR_INVALID_ARG;
     } else {
-        pl.ml_bytes = pl.ws_bytes = 0;
+        pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
     }
     return FATTN_OK;
 }
@@ -202,6 +206,18 @@ int make_plan(const fattn_params* p, Plan& pl) {
     a.has_mask = has_mask ? 1 : 0;
     a.scale_log2 = p->scale * 1.4426950408889634f;
 
+    // byte spans addressed through the 32-bit buffer descriptors
+    const int64_t k_span = (N - 1) * k.nb[1] + (int64_t)rowK;
+    const int64_t v_span = v_trans ? (D - 1) * v.nb[0] + N * 2 : (N - 1) * v.nb[1] + (int64_t)rowV;
+    const int64_t m_span = has_mask ? (NQ - 1) * mk.nb[1] + mk.ne[0] * 2 : 0;
+    const int64_t q_span = (NQ - 1) * q.nb[1] + (H - 1) * q.nb[2] + D * 4;
+    const int64_t span_max = (int64_t)0xFFFFFFF0;
+    if (k_span > span_max || v_span > span_max || m_span > span_max || q_span > span_max) return FATTN_ERR_BAD_STRIDE;
+    a.k_span = (uint32_t)k_span;
+    a.v_span = (uint32_t)v_span;
+    a.m_span = (uint32_t)m_span;
+    a.q_span = (uint32_t)q_span;
+
     const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
     if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
     pl.kt = k.type;
@@ -229,10 +245,6 @@ int launch_split_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     hipLaunchKernelGGL(kern, pl.grid, dim3(kSplitWaves * kWave), pl.lds, st, pl.a);
     if (hipGetLastError() != hipSuccess) return FATTN_ERR_LAUNCH;
     if (ev.end) (void)hipEventRecord(ev.end, st);
-    if (pl.a.n_chunks > 1) {
-        hipLaunchKernelGGL(fattn_combine_kernel<D>, dim3(pl.grid.y, pl.grid.z), dim3(256), 0, st, pl.a);
-        if (hipGetLastError() != hipSuccess) return FATTN_ERR_LAUNCH;
-    }
     return FATTN_OK;
 }
 
@@ -297,6 +309,13 @@ size_t fattn_row_size(int type, int64_t k) {
     }
 }
 
+int fattn_workspace_init(void* workspace, size_t workspace_bytes, void* stream) {
+    if (!workspace && workspace_bytes) return FATTN_ERR_INVALID_ARG;
+    if (!workspace_bytes) return FATTN_OK;
+    return hipMemsetAsync(workspace, 0, workspace_bytes, (hipStream_t)stream) == hipSuccess ? FATTN_OK
+                                                                                          : FATTN_ERR_LAUNCH;
+}
+
 size_t fattn_workspace_size(const fattn_params* p) {
     Plan pl;
     if (make_plan(p, pl) != FATTN_OK) return 0;
@@ -311,8 +330,10 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
     if (rc != FATTN_OK) return rc;
     if (pl.ws_bytes) {
         if (!p->workspace || p->workspace_bytes < pl.ws_bytes || (uintptr_t)p->workspace % 16) return FATTN_ERR_WORKSPACE;
-        pl.a.ws_ml = (float*)p->workspace;
-        pl.a.ws_o = (float*)((uint8_t*)p->workspace + pl.ml_bytes);
+        uint8_t* w = (uint8_t*)p->workspace;
+        pl.a.ws_cnt = (uint32_t*)w;
+        pl.a.ws_ml = (float*)(w + pl.cnt_bytes);
+        pl.a.ws_o = (float*)(w + pl.cnt_bytes + pl.ml_bytes);
     }
     hipStream_t st = (hipStream_t)stream;
     Events ev;

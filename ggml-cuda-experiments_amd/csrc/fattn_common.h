@@ -18,6 +18,7 @@ typedef _Float16 f16;
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -152,6 +153,38 @@ __device__ __forceinline__ float wave_sum(float x) {
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) x += __shfl_xor(x, m, kWave);
     return x;
+}
+
+// ---------------------------------------------------------------- sc1 memory ops
+// Write-through stores / L1-bypassing loads for data handed between workgroups
+// of one launch (MI355X_MICROARCH.md, inter-workgroup visibility).  Issued as
+// inline asm, so the compiler does not track them: callers drain with an
+// explicit s_waitcnt vmcnt(0) and pass every loaded value through reg_fence()
+// after that wait, so no use can be scheduled above it.
+__device__ __forceinline__ void st_sc1(float* p, f32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1(float* p, f32x2 v) {
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ f32x4 ld_sc1(const float* p) {
+    f32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ f32x2 ld_sc1_x2(const float* p) {
+    f32x2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ void reg_fence(T& v) {
+    asm volatile("" : "+v"(v));
 }
 
 __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {

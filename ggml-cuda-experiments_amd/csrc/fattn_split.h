@@ -38,6 +38,7 @@ constexpr int kSplitWaves = 4;
 constexpr int kStep = 32;   // KV positions per wave step (= one PV k-step)
 constexpr int kRows = 16;   // packed query rows per workgroup (MFMA N)
 constexpr int VT_F16T = 100;  // V f16 stored transposed ([D][N], flash_row_float.h:177)
+constexpr int kCntStride = 64;  // uint32 words between arrival counters (256 B: atomics to one line serialise)
 
 struct SplitArgs {
     const uint8_t* q;
@@ -45,12 +46,14 @@ struct SplitArgs {
     const uint8_t* v;
     const uint8_t* mask;
     float* dst;
-    float* ws_o;   // [S][Y][C][16][D]
-    float* ws_ml;  // [S][Y][C][16][2]
+    uint32_t* ws_cnt;   // [S][Y] chunk arrival counters, one per 256-B line (zero between launches)
+    float* ws_o;        // [S][Y][C][16][D] chunk partials
+    float* ws_ml;       // [S][Y][C][16][2]
     int64_t q_nb1, q_nb2, q_nb3;
     int64_t k_nb1, k_nb2, k_nb3;
     int64_t v_nb0, v_nb1, v_nb2, v_nb3;
     int64_t m_nb1;
+    uint32_t k_span, v_span, m_span, q_span;  // bytes addressed per (kv head, seq) / mask / seq of Q
     int NQ, H, S;       // q ne1, ne2, ne3
     int N;              // kv length
     int rk2, rk3;       // H/Hkv, S/Skv
@@ -107,81 +110,128 @@ __device__ __forceinline__ void wait_steps(int outstanding) {
 }
 
 // ---------------------------------------------------------------- HBM -> LDS
-// One step = [K rows | V rows | mask rows] for positions [n0, n0+32), copied
-// as raw bytes.  GRAN = 16: 16-B pieces (quantised rows contiguous, f16 rows
-// 16-B aligned); GRAN = 4: dword pieces for any ggml row stride.  Rows past N
-// are clamped to N-1 (masked out later), so the LDS image never holds garbage.
-// Mask rows use 16-B pieces on the fast path and 2-B pieces otherwise.
 template <int KT, int VT, int D, int GRAN>
 struct StepPlan {
     using C = SplitCfg<KT, VT, D>;
     static constexpr int PK = C::kBytes / GRAN;
     static constexpr int PV = C::vBytes / GRAN;
-    static constexpr int NIKV = (PK + PV + kWave - 1) / kWave;
+    // K and V come through different buffer descriptors: separate instructions
+    static constexpr int NIK = (PK + kWave - 1) / kWave;
+    static constexpr int NIV = (PV + kWave - 1) / kWave;
+    static constexpr int NIKV = NIK + NIV;
     // mask granule: LDS-DMA writes lane*4 bytes for sub-dword sizes, so the
     // generic path moves dwords (2 positions) and needs even-padded mask rows
     static constexpr int MG = GRAN == 16 ? 16 : 4;
     static constexpr int MPR = kStep * 2 / MG;           // mask pieces per row
-    // all 16 mask rows are always copied (rows past the tile clamp to a valid
-    // query row) so every step issues the same, compile-time instruction count
+    // all 16 mask rows are always requested so every step issues the same,
+    // compile-time instruction count; rows past n_q fall outside the mask
+    // descriptor and cost no memory traffic
     static constexpr int PM = kRows * MPR;
     static constexpr int NIM = PM / kWave;
     static_assert(PM % kWave == 0, "");
 };
 
+typedef __attribute__((address_space(3))) void lds_void;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Buffer descriptor (4 SGPRs): base, stride 0, num_records = bytes, raw dword
+// format.  Offsets at or past `bytes` fetch nothing and write ZEROS to LDS
+// (tests/test_gpu_prims.py::test_lds_dma_partial_exec).
+__device__ __forceinline__ i32x4 make_srd(const void* base, uint32_t bytes) {
+    const uint64_t p = (uint64_t)base;
+    i32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+    r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));
+    r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+    r.w = 0x00020000;
+    return r;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(const lds_void*)p; }
+
+// HBM -> LDS, one piece per lane at lds + lane*BYTES.  Inline asm: through the
+// builtin, hipcc treats the LDS base as a per-lane value, and around an
+// exec-masked (partial) instruction it built per-lane phis of (LDS base,
+// offset) pairs whose readfirstlane'd M0 no longer matched the inactive
+// lanes' offsets.  Here M0 comes from an SGPR operand in the same statement
+// (saved and restored: M0 is compiler-reserved; s_nop 0 = M0 -> LDS-DMA
+// hazard).  Not tracked by the compiler's s_waitcnt bookkeeping: every
+// consumer waits with an explicit vmcnt.
+template <int BYTES>
+__device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds, uint32_t off) {
+    uint32_t keep;
+    if constexpr (BYTES == 16) {
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(off), "s"(srd), "s"(lds)
+            : "memory");
+    } else {
+        static_assert(BYTES == 4, "");
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(off), "s"(srd), "s"(lds)
+            : "memory");
+    }
+}
+
+struct StepSrc {
+    i32x4 k, v, m;
+};
+
+// One step = [K rows | V rows | mask rows] for positions [n0, n0+32), copied
+// as raw bytes.  GRAN = 16: 16-B pieces (quantised rows contiguous, f16 rows
+// 16-B aligned); GRAN = 4: dword pieces for any ggml row stride.
 template <int KT, int VT, int D, int GRAN, bool HM>
-__device__ __forceinline__ void issue_step(const SplitArgs& a, const uint8_t* kbase, const uint8_t* vbase,
-                                           int n0, int mrow0, uint8_t* buf, int lane) {
+__device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs, int n0, int mrow0, uint8_t* buf,
+                                           int lane) {
     using C = SplitCfg<KT, VT, D>;
     using P = StepPlan<KT, VT, D, GRAN>;
+    const uint32_t kn1 = (uint32_t)a.k_nb1, vn1 = (uint32_t)a.v_nb1;
 #pragma unroll
-    for (int i = 0; i < P::NIKV; i++) {
+    for (int i = 0; i < P::NIK; i++) {
         const int p = i * kWave + lane;
-        const uint8_t* src;
-        if (p < P::PK) {
-            const int byte = p * GRAN;
-            if constexpr (KT == FATTN_TYPE_F16) {
-                // f16 rows: 16-B chunks XOR-swizzled by row (conflict-free ds_read_b128)
-                constexpr int CPR = C::rowK / 16;
-                const int row = byte / C::rowK;
-                const int chunk = ((byte % C::rowK) / 16) ^ (row & (CPR - 1));
-                const int rr = min(n0 + row, a.N - 1);
-                src = kbase + (int64_t)rr * a.k_nb1 + chunk * 16 + (byte & 15);
-            } else if constexpr (GRAN == 16) {
-                src = kbase + (int64_t)n0 * C::rowK + byte;
-            } else {
-                const int row = byte / C::rowK;
-                const int rr = min(n0 + row, a.N - 1);
-                src = kbase + (int64_t)rr * a.k_nb1 + (byte % C::rowK);
-            }
+        const int byte = p * GRAN;
+        uint32_t off;
+        if constexpr (KT == FATTN_TYPE_F16) {
+            // f16 rows: 16-B chunks XOR-swizzled by row (conflict-free ds_read_b128)
+            constexpr int CPR = C::rowK / 16;
+            const int row = byte / C::rowK;
+            const int chunk = ((byte % C::rowK) / 16) ^ (row & (CPR - 1));
+            off = (uint32_t)(n0 + row) * kn1 + chunk * 16 + (byte & 15);
+        } else if constexpr (GRAN == 16) {
+            off = (uint32_t)n0 * C::rowK + byte;
         } else {
-            const int byte = (p - P::PK) * GRAN;
-            if constexpr (VT == VT_F16T) {
-                // V^T tile: D rows (one per head dim) of kStep f16; needs N % 32 == 0
-                const int d = byte / (kStep * 2);
-                src = vbase + (int64_t)d * a.v_nb0 + (int64_t)n0 * 2 + (byte % (kStep * 2));
-            } else if constexpr (VT == FATTN_TYPE_F16) {
-                constexpr int CPR = C::rowV / 16;
-                const int row = byte / C::rowV;
-                const int chunk = ((byte % C::rowV) / 16) ^ (((row & 7) << 1) & (CPR - 1));
-                const int rr = min(n0 + row, a.N - 1);
-                src = vbase + (int64_t)rr * a.v_nb1 + chunk * 16 + (byte & 15);
-            } else if constexpr (GRAN == 16) {
-                src = vbase + (int64_t)n0 * C::rowV + byte;
-            } else {
-                const int row = byte / C::rowV;
-                const int rr = min(n0 + row, a.N - 1);
-                src = vbase + (int64_t)rr * a.v_nb1 + (byte % C::rowV);
-            }
+            const int row = byte / C::rowK;
+            off = (uint32_t)(n0 + row) * kn1 + (byte % C::rowK);
         }
-        if (p < P::PK + P::PV) {
-            // the size operand must be a literal
-            if constexpr (GRAN == 16) {
-                __builtin_amdgcn_global_load_lds((const void*)src, (void*)(buf + i * kWave * 16), 16, 0, 0);
-            } else {
-                __builtin_amdgcn_global_load_lds((const void*)src, (void*)(buf + i * kWave * 4), 4, 0, 0);
-            }
+        if (P::PK % kWave == 0 || p < P::PK) dma<GRAN>(rs.k, lds_addr(buf + i * kWave * GRAN), off);
+    }
+    uint8_t* vbuf = buf + C::kBytes;
+#pragma unroll
+    for (int i = 0; i < P::NIV; i++) {
+        const int p = i * kWave + lane;
+        const int byte = p * GRAN;
+        uint32_t off;
+        if constexpr (VT == VT_F16T) {
+            // V^T tile: D rows (one per head dim) of kStep f16; needs N % 32 == 0
+            const int d = byte / (kStep * 2);
+            off = (uint32_t)d * (uint32_t)a.v_nb0 + (uint32_t)n0 * 2 + (byte % (kStep * 2));
+        } else if constexpr (VT == FATTN_TYPE_F16) {
+            constexpr int CPR = C::rowV / 16;
+            const int row = byte / C::rowV;
+            const int chunk = ((byte % C::rowV) / 16) ^ (((row & 7) << 1) & (CPR - 1));
+            off = (uint32_t)(n0 + row) * vn1 + chunk * 16 + (byte & 15);
+        } else if constexpr (GRAN == 16) {
+            off = (uint32_t)n0 * C::rowV + byte;
+        } else {
+            const int row = byte / C::rowV;
+            off = (uint32_t)(n0 + row) * vn1 + (byte % C::rowV);
         }
+        if (P::PV % kWave == 0 || p < P::PV) dma<GRAN>(rs.v, lds_addr(vbuf + i * kWave * GRAN), off);
     }
     if constexpr (HM) {
         uint8_t* mbuf = buf + C::kBytes + C::vBytes;
@@ -190,15 +240,8 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const uint8_t* kb
             const int q = i * kWave + lane;
             const int mr = q / P::MPR;
             const int off = (q % P::MPR) * P::MG;
-            const int qrow = min(mrow0 + mr, a.NQ - 1);
-            int pos = n0 + off / 2;
-            if constexpr (P::MG == 4) pos = min(pos, (a.N - 1) & ~1);  // rows padded to even length
-            const uint8_t* src = a.mask + (int64_t)qrow * a.m_nb1 + (int64_t)pos * 2;
-            if constexpr (P::MG == 16) {
-                __builtin_amdgcn_global_load_lds((const void*)src, (void*)(mbuf + i * kWave * 16), 16, 0, 0);
-            } else {
-                __builtin_amdgcn_global_load_lds((const void*)src, (void*)(mbuf + i * kWave * 4), 4, 0, 0);
-            }
+            const uint32_t moff = (uint32_t)(mrow0 + mr) * (uint32_t)a.m_nb1 + (uint32_t)n0 * 2 + off;
+            dma<P::MG>(rs.m, lds_addr(mbuf + i * kWave * P::MG), moff);
         }
     }
 }
@@ -329,7 +372,10 @@ __device__ __forceinline__ int tile_rows(const SplitArgs& a, int qt, int hs) {
 // ---------------------------------------------------------------- diagnostics
 // Diagnostic build only (-DFATTN_STAMPS, libfattn_stamps.so): lane 0 of every
 // wave records s_memrealtime (100 MHz) at phase boundaries into g_stamps
-// [block][wave][8].  No stamp executes in the product library.
+// [block][wave][16]: 0 start, 1 first steps issued, 2+s data of step s in LDS
+// (s < 8), 10 loop done, 11 4-wave merge done, 12 partial published (or output
+// stored), 13 tile merge done (last workgroup).  No stamp executes in
+// the product library.
 #ifdef FATTN_STAMPS
 __device__ unsigned long long* g_stamps;
 #define FATTN_STAMP(k)                                                                          \
@@ -337,7 +383,7 @@ __device__ unsigned long long* g_stamps;
         if (lane == 0 && g_stamps) {                                                            \
             const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                     \
             const int64_t blk_ = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
-            g_stamps[(blk_ * kSplitWaves + wave) * 8 + (k)] = t_;                                \
+            g_stamps[(blk_ * kSplitWaves + wave) * 16 + (k)] = t_;                                \
         }                                                                                       \
     } while (0)
 #else
@@ -345,6 +391,20 @@ __device__ unsigned long long* g_stamps;
 #endif
 
 // ---------------------------------------------------------------- kernel
+
+// LDS carve of the chunk-0 merge: [red 16 x D][wts 16 x 64][rowL 16] | own O [16 x D] + own (m, l) [16 x 2]
+template <int D>
+constexpr int own_off() {
+    return (kRows * D * 4 + kRows * 64 * 4 + kRows * 4 + 127) / 128 * 128;
+}
+template <int D>
+constexpr int combine_lds_bytes() {
+    return own_off<D>() + kRows * D * 4 + kRows * 2 * 4 + 16;  // + last-arriver flag
+}
+
+template <int D>
+__device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
+                                             int rv, int own_chunk, uint8_t* smem);
 
 template <int KT, int VT, int D, int GRAN, bool HM>
 __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4) ? 2 : 4) void fattn_split_kernel(
@@ -359,7 +419,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     constexpr bool kVQ8 = C::VTT == FATTN_TYPE_Q8_0;
 
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    // wave-uniform by construction; readfirstlane lets the compiler see it, so the
+    // slice bounds, loop counts and LDS-DMA bases (M0) stay scalar
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4;
     const int i16 = lane & 15;
     FATTN_STAMP(0);
@@ -392,30 +454,46 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     const int nsteps = w_hi > w_lo ? (w_hi - w_lo + kStep - 1) / kStep : 0;
     const int nbuf = a.nbuf;
 
-    const uint8_t* kbase = a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3;
-    const uint8_t* vbase = a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3;
+    StepSrc rs;
+    rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
+    rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
+    rs.m = make_srd(a.mask, HM ? a.m_span : 0);
     uint8_t* wbuf = smem + wave * a.wave_bytes;
     const int mrow0 = qt * a.QPT;
 
+    // Staggered priorities: the waves of a CU otherwise interleave their DMA
+    // issue, so every wave's last piece lands near the end of the burst and
+    // all compute starts late; by priority the first waves' steps land first
+    // and their compute overlaps the rest of the stream.
+    switch (__builtin_amdgcn_readfirstlane(wave)) {
+        case 0: __builtin_amdgcn_s_setprio(3); break;
+        case 1: __builtin_amdgcn_s_setprio(2); break;
+        case 2: __builtin_amdgcn_s_setprio(1); break;
+        default: break;
+    }
+
     for (int s = 0; s < nbuf && s < nsteps; s++) {
-        issue_step<KT, VT, D, GRAN, HM>(a, kbase, vbase, w_lo + s * kStep, mrow0, wbuf + s * C::stepBytes, lane);
+        issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + s * kStep, mrow0, wbuf + s * C::stepBytes, lane);
     }
 
     FATTN_STAMP(1);
     // ---- Q^T operand (B of S^T = K.Q^T), rounded to f16 like src/utils.h:10
+    // (lanes of unused columns point past the descriptor: zeros, no traffic)
     f16x8 qop[NB];
     {
-        const float* qrow = (const float*)(a.q + (int64_t)(row_ok ? iq1 : 0) * a.q_nb1 +
-                                           (int64_t)(row_ok ? iq2 : 0) * a.q_nb2 + (int64_t)iq3 * a.q_nb3);
+        const auto qs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.q + (int64_t)iq3 * a.q_nb3), 0,
+                                                          a.q_span, 0x00020000);
+        const uint32_t qoff = row_ok ? (uint32_t)iq1 * (uint32_t)a.q_nb1 + (uint32_t)iq2 * (uint32_t)a.q_nb2 + 32 * g
+                                     : a.q_span;
 #pragma unroll
         for (int b = 0; b < NB; b++) {
-            const f32x4 x0 = *(const f32x4*)(qrow + 32 * b + 8 * g);
-            const f32x4 x1 = *(const f32x4*)(qrow + 32 * b + 8 * g + 4);
+            const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qoff + 128 * b, 0, 0));
+            const f32x4 x1 =
+                __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qoff + 128 * b + 16, 0, 0));
             f16x8 h;
             h.s0 = (f16)x0.x; h.s1 = (f16)x0.y; h.s2 = (f16)x0.z; h.s3 = (f16)x0.w;
             h.s4 = (f16)x1.x; h.s5 = (f16)x1.y; h.s6 = (f16)x1.z; h.s7 = (f16)x1.w;
-            const f16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-            qop[b] = row_ok ? h : z;
+            qop[b] = h;
         }
     }
     // Q is loaded after the first steps' LDS-DMA is in flight, so the HBM stream
@@ -432,11 +510,11 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     int cur = 0;  // buffer of step s
     for (int s = 0; s < nsteps; s++) {
         wait_steps<NI>(min(nbuf - 1, nsteps - 1 - s));
-        if (s == 0) FATTN_STAMP(2);
+        if (s < 8) FATTN_STAMP(2 + s);
 #ifdef FATTN_DIAG_NOCOMPUTE
         // diagnostic build only: memory-side ceiling of this access pattern
         if (s + nbuf < nsteps) {
-            issue_step<KT, VT, D, GRAN, HM>(a, kbase, vbase, w_lo + (s + nbuf) * kStep, mrow0,
+            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf) * kStep, mrow0,
                                             wbuf + cur * C::stepBytes, lane);
         }
         cur = (cur + 1 == nbuf) ? 0 : cur + 1;
@@ -511,18 +589,20 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
             for (int c = 0; c < NC; c++) o[c] = mfma16(v_operand_f16<VT, D>(vb, c, g, i16), pb, o[c]);
         } else {
             const int rA = 4 * g, rB = 16 + 4 * g;
-            // scales of this lane's 8 rows (4g..4g+3, 16+4g..16+4g+3), all blocks
-            RowScales<C::VTT, D> vs[8];
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                vs[r] = row_scales<C::VTT, D>(vb + (rA + r) * C::rowV);
-                vs[4 + r] = row_scales<C::VTT, D>(vb + (rB + r) * C::rowV);
-            }
 #pragma unroll
             for (int b = 0; b < NB; b++) {
-                const f16x2 d01 = scale_pair(vs[0], vs[1], b), d23 = scale_pair(vs[2], vs[3], b);
-                const f16x2 d45 = scale_pair(vs[4], vs[5], b), d67 = scale_pair(vs[6], vs[7], b);
                 constexpr int BB = TypeInfo<C::VTT>::block_bytes;
+                // block-b scales of this lane's 8 rows (4g..4g+3, 16+4g..16+4g+3):
+                // the dword holding each, then f16 pairs {row r, row r+1}
+                uint32_t sw[8];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    sw[r] = *(const uint32_t*)(vb + (rA + r) * C::rowV + ((BB * b) & ~3));
+                    sw[4 + r] = *(const uint32_t*)(vb + (rB + r) * C::rowV + ((BB * b) & ~3));
+                }
+                const uint32_t sel = ((BB * b) & 2) ? 0x07060302u : 0x05040100u;  // b is unrolled
+                const f16x2 d01 = as_h2(perm_b32(sw[1], sw[0], sel)), d23 = as_h2(perm_b32(sw[3], sw[2], sel));
+                const f16x2 d45 = as_h2(perm_b32(sw[5], sw[4], sel)), d67 = as_h2(perm_b32(sw[7], sw[6], sel));
                 if constexpr (kVQ8) {
                     // one u16 per row carries columns 2i (-> tile E_b) and 2i+1 (-> tile O_b)
                     const uint8_t* cp = vb + b * BB + 2 + 2 * i16;
@@ -574,13 +654,18 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
         // -- refill this buffer with step s + nbuf
         if (s + nbuf < nsteps) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            issue_step<KT, VT, D, GRAN, HM>(a, kbase, vbase, w_lo + (s + nbuf) * kStep, mrow0,
+            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf) * kStep, mrow0,
                                             wbuf + cur * C::stepBytes, lane);
         }
         cur = (cur + 1 == nbuf) ? 0 : cur + 1;
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    FATTN_STAMP(3);
+#ifdef FATTN_DIAG_NOTAIL
+    // diagnostic build only: stop before the merge / publish tail
+    if (m_run == 12345.0f) a.dst[0] = l_run;  // keep the loop's results alive
+    return;
+#endif
+    FATTN_STAMP(10);
 
     // ---- per-wave state -> LDS (this wave's own region), then merge the 4 waves
     const float l_tot = grp4_sum(l_run);
@@ -604,7 +689,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
         mml[2 * m + 1] = l_tot;
     }
     __syncthreads();
-    FATTN_STAMP(4);
+    FATTN_STAMP(11);
 
     constexpr int EPT = D / 16;  // outputs per thread: 16 rows x D over 256 threads
     const int tm = threadIdx.x / 16;
@@ -654,114 +739,181 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
                 *(f32x4*)(out + e) = v;
             }
         }
+        FATTN_STAMP(12);
         return;
     }
 
-    // ---- several chunks: plain stores of this chunk's partial; fattn_combine_kernel
-    // (next launch on the stream) merges them -- the kernel boundary publishes.
+#ifdef FATTN_DIAG_NOPUBLISH
+    // diagnostic build only: stop after the 4-wave merge
+    if (acc[0] == 12345.0f) a.dst[0] = L;
+    return;
+#endif
+    // ---- several chunks: the workgroup that arrives last for the tile merges
+    // all partials (no second launch).  Hand-off (MI355X_MICROARCH.md,
+    // inter-workgroup visibility, first row of the sc1 table): partial bytes
+    // stored sc1 (write-through), each storing wave drains vmcnt, barrier, ONE
+    // agent-scope atomic add per workgroup on the tile's own 256-B line; the
+    // last adder reads the others' partials with sc1 loads -- all of them in
+    // one round trip -- while its own stays in LDS.
+    const int64_t tile = (int64_t)iq3 * gridDim.y + y;
     if (tm < rv) {
-        const int64_t slot = (((int64_t)iq3 * gridDim.y + y) * a.n_chunks + chunk) * kRows + tm;
+        const int64_t slot = (tile * a.n_chunks + chunk) * kRows + tm;
 #pragma unroll
-        for (int e = 0; e < EPT; e += 4) *(f32x4*)(a.ws_o + slot * D + d0 + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
-        if (tj == 0) *(float2*)(a.ws_ml + 2 * slot) = float2{M, L};
+        for (int e = 0; e < EPT; e += 4)
+            st_sc1(a.ws_o + slot * D + d0 + e, f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]});
+        if (tj == 0) st_sc1(a.ws_ml + 2 * slot, f32x2{M, L});
     }
-    FATTN_STAMP(5);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef FATTN_DIAG_NOATOMIC
+    return;  // diagnostic build only: stop after the published stores drained
+#endif
+    __syncthreads();  // every storing wave has drained; every wave is done reading the merge image
+    float* own_o = (float*)(smem + own_off<D>());
+    float* own_ml = own_o + kRows * D;
+    int* last_flag = (int*)(own_ml + kRows * 2);
+    if (threadIdx.x == 0) {
+        uint32_t* cnt = a.ws_cnt + tile * kCntStride;
+        const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (uint32_t)(a.n_chunks - 1);
+        // every chunk has arrived: re-arm the counter for the next launch
+        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *last_flag = last;
+    }
+    // own partial -> LDS meanwhile (used only if this workgroup merges)
+    if (tm < rv) {
+#pragma unroll
+        for (int e = 0; e < EPT; e += 4) *(f32x4*)(own_o + tm * D + d0 + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
+        if (tj == 0) *(f32x2*)(own_ml + 2 * tm) = f32x2{M, L};
+    }
+    __syncthreads();
+    FATTN_STAMP(12);
+    if (!*last_flag) return;
+    combine_tile<D>(a, tile, qt, hs, ik2, iq3, rv, chunk, smem);
+    FATTN_STAMP(13);
 }
 
 // ---------------------------------------------------------------- combine
-// Log-sum-exp merge of the chunk partials (fa_reduce, flash_row_float.h:415-472,
-// in fp32 and parallel).  One workgroup per (y, z) tile; only its rv valid rows.
-// 16 thread groups = rv rows x G chunk subsets; every thread issues all of its
-// loads (O partials + (m, l) pairs) before consuming any: one memory round trip.
+// Log-sum-exp merge of a tile's chunk partials (fa_reduce,
+// flash_row_float.h:415-472, in fp32 and parallel), run by the tile's last
+// workgroup; its own partial comes from LDS.  16 thread groups = rv rows x G
+// chunk subsets.  Every thread issues its (m, l) load and its first batch of
+// partial loads before one wait (one memory round trip for the common case
+// ceil(n_chunks / G) <= CB); the (m, l) pairs reduce with segmented
+// xor-shuffles in a fixed order (deterministic).
 template <int D>
-__global__ __launch_bounds__(256) void fattn_combine_kernel(const SplitArgs a) {
+__device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
+                                             int rv, int own_chunk, uint8_t* smem) {
     constexpr float kNegInf = -__builtin_inff();
     constexpr int EPT = D / 16;
-    constexpr int MAXC = 64 / EPT * 2;  // max chunks one thread folds (register budget)
-    __shared__ float red[kRows][D];
-    __shared__ float wts[kRows][64];
-    __shared__ float rowML[kRows][2];
-    const int y = blockIdx.x, iq3 = blockIdx.y;
-    int qt = 0, hs = 0, ik2 = y;
-    if (a.n_qt != 1 || a.n_hsub != 1) {
-        qt = y % a.n_qt;
-        hs = (y / a.n_qt) % a.n_hsub;
-        ik2 = y / (a.n_qt * a.n_hsub);
-    }
-    const int rv = tile_rows(a, qt, hs);
+    constexpr int CB = 2;  // chunks per load batch (register budget of the split kernel)
+    float(*red)[D] = (float(*)[D])smem;                                // [16][D]
+    float(*wts)[64] = (float(*)[64])(smem + kRows * D * 4);            // [16][64]
+    float* rowL = (float*)(smem + kRows * D * 4 + kRows * 64 * 4);     // [16]
+    const float* own_o = (const float*)(smem + own_off<D>());          // [16][D]
+    const float* own_ml = own_o + kRows * D;                           // [16][2]
     const int NCH = a.n_chunks;
     const int G = max(1, kRows / max(rv, 1));
     const int grp = threadIdx.x / 16, tj = threadIdx.x % 16, d0 = tj * EPT;
-    const int64_t sb = ((int64_t)iq3 * gridDim.x + y) * NCH;
-    // (1) issue every load first
-    float v[MAXC][EPT];
+    const int64_t sb = tile * NCH;
     const int r = grp / G, cg = grp % G;
     const bool active = grp < rv * G;
-    // loads are unconditional (chunk index clamped, weight zeroed below): a
-    // guarded load would make hipcc branch + wait vmcnt(0) per load
     const int kmax = active ? (NCH - cg + G - 1) / G : 0;
-    {
-        const int rr = active ? r : 0;
+
+    // partial loads of chunks cg + (k0 + kk) * G (clamped index, zero weight
+    // past kmax; the own chunk is read from LDS instead)
+    auto issue = [&](f32x4 (&v)[CB][EPT / 4], int k0) {
 #pragma unroll
-        for (int k = 0; k < MAXC; k++) {
-            const int c = min(cg + k * G, NCH - 1);
-            const float* wo = a.ws_o + ((sb + c) * kRows + rr) * D + d0;
+        for (int kk = 0; kk < CB; kk++) {
+            const int c = min(cg + (k0 + kk) * G, NCH - 1);
+            const float* wo = a.ws_o + ((sb + c) * kRows + (active ? r : 0)) * D + d0;
 #pragma unroll
-            for (int e = 0; e < EPT; e += 4) {
-                const f32x4 x = *(const f32x4*)(wo + e);
-                v[k][e] = x.x; v[k][e + 1] = x.y; v[k][e + 2] = x.z; v[k][e + 3] = x.w;
-            }
+            for (int e = 0; e < EPT / 4; e++) v[kk][e] = ld_sc1(wo + 4 * e);
         }
-    }
-    // (2) (m, l) of chunk c of row r lives in thread r * NCP + c (NCP = next
-    // power of two >= NCH, <= 64): segmented xor-reductions inside one wave give
-    // each row's max and normaliser in a fixed order (deterministic).
+    };
+    f32x4 v[CB][EPT / 4];
+    issue(v, 0);
+    // (m, l) of chunk c of row r in thread r * NCP + c (NCP = next power of
+    // two >= NCH, <= 64)
     const int NCP = a.ncp;
     const int mr = threadIdx.x / NCP, mc = threadIdx.x % NCP;
-    float mv = kNegInf, lv = 0.0f;
-    if (mr < rv && mc < NCH) {
-        const float2 x = *(const float2*)(a.ws_ml + 2 * ((sb + mc) * kRows + mr));
-        mv = x.x;
-        lv = x.y;
+    const bool has_ml = mr < rv && mc < NCH;
+    f32x2 ml = ld_sc1_x2(a.ws_ml + 2 * ((sb + min(mc, NCH - 1)) * kRows + (has_ml ? mr : 0)));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    reg_fence(ml);
+#pragma unroll
+    for (int kk = 0; kk < CB; kk++) {
+#pragma unroll
+        for (int e = 0; e < EPT / 4; e++) reg_fence(v[kk][e]);
     }
-    float Mr = mv;
+    if (has_ml && mc == own_chunk) ml = *(const f32x2*)(own_ml + 2 * mr);
+    if (!has_ml) ml = f32x2{kNegInf, 0.0f};
+    float Mr = ml.x;
     for (int o = 1; o < NCP; o <<= 1) Mr = fmaxf(Mr, __shfl_xor(Mr, o, kWave));
-    const float wt = (mv == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mv - Mr);
-    float Lr = wt * lv;
+    const float wt = (ml.x == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(ml.x - Mr);
+    float Lr = wt * ml.y;
     for (int o = 1; o < NCP; o <<= 1) Lr += __shfl_xor(Lr, o, kWave);
     if (mr < rv) {
         wts[mr][mc] = wt;
-        if (mc == 0) rowML[mr][1] = Lr;
+        if (mc == 0) rowL[mr] = Lr;
     }
     __syncthreads();
-    // (3) fold this thread's chunks
+
+    // fold this thread's chunks
     if (active) {
         float s8[EPT];
 #pragma unroll
         for (int e = 0; e < EPT; e++) s8[e] = 0.0f;
+        for (int k0 = 0; k0 < kmax; k0 += CB) {
+            if (k0 > 0) {
+                issue(v, k0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int k = 0; k < MAXC; k++) {
-            const float wt = k < kmax ? wts[r][min(cg + k * G, NCH - 1)] : 0.0f;
+                for (int kk = 0; kk < CB; kk++) {
 #pragma unroll
-            for (int e = 0; e < EPT; e++) s8[e] += wt * v[k][e];
+                    for (int e = 0; e < EPT / 4; e++) reg_fence(v[kk][e]);
+                }
+            }
+#pragma unroll
+            for (int kk = 0; kk < CB; kk++) {
+                const int c = cg + (k0 + kk) * G;
+                const float w = (k0 + kk < kmax) ? wts[r][min(c, NCH - 1)] : 0.0f;
+                if (c == own_chunk) {
+#pragma unroll
+                    for (int e = 0; e < EPT; e++) s8[e] += w * own_o[r * D + d0 + e];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < EPT / 4; e++) {
+                        s8[4 * e] += w * v[kk][e].x;
+                        s8[4 * e + 1] += w * v[kk][e].y;
+                        s8[4 * e + 2] += w * v[kk][e].z;
+                        s8[4 * e + 3] += w * v[kk][e].w;
+                    }
+                }
+            }
         }
 #pragma unroll
         for (int e = 0; e < EPT; e++) red[grp][d0 + e] = s8[e];
     }
     __syncthreads();
-    // (4) sum the G subsets of each row, normalise, store
+
+    // sum the G subsets of each row, normalise, store
     if (grp < rv) {
-        const float Lr = rowML[grp][1];
-        const float inv = 1.0f / Lr;
+        const float Lrow = rowL[grp];
+        const float inv = 1.0f / Lrow;
         const int rq = div_R(a, grp);
         const int riq1 = qt * a.QPT + rq;
         const int riq2 = ik2 * a.rk2 + hs * a.R + (grp - rq * a.R);
         float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + d0;
 #pragma unroll
-        for (int e = 0; e < EPT; e++) {
-            float x = 0.0f;
-            for (int k = 0; k < G; k++) x += red[grp * G + k][d0 + e];
-            out[e] = (Lr == 0.0f) ? __builtin_nanf("") : x * inv;
+        for (int e = 0; e < EPT; e += 4) {
+            f32x4 o4;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float x = 0.0f;
+                for (int k = 0; k < G; k++) x += red[grp * G + k][d0 + e + j];
+                o4[j] = (Lrow == 0.0f) ? __builtin_nanf("") : x * inv;
+            }
+            *(f32x4*)(out + e) = o4;
         }
     }
 }

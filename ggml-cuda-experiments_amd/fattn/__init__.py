@@ -32,7 +32,7 @@ ERRORS = {
 
 # every symbol include/fattn.h declares
 EXPORTS = (
-    "fattn_workspace_size", "fattn_ext", "fattn_ext_events", "fattn_ext_f16_launch", "fattn_row_workspace_size", "fattn_row",
+    "fattn_workspace_size", "fattn_workspace_init", "fattn_ext", "fattn_ext_events", "fattn_ext_f16_launch", "fattn_row_workspace_size", "fattn_row",
     "fattn_dequantize", "fattn_quantize", "fattn_strerror", "fattn_row_size", "fattn_version",
 )
 
@@ -67,6 +67,8 @@ def lib() -> C.CDLL:
         vp, i64, sz = C.c_void_p, C.c_int64, C.c_size_t
         L.fattn_workspace_size.restype = sz
         L.fattn_workspace_size.argtypes = [C.POINTER(FattnParams)]
+        L.fattn_workspace_init.restype = C.c_int
+        L.fattn_workspace_init.argtypes = [vp, sz, vp]
         L.fattn_ext.restype = C.c_int
         L.fattn_ext.argtypes = [C.POINTER(FattnParams), vp]
         L.fattn_ext_events.restype = C.c_int
@@ -202,7 +204,8 @@ class Attention:
         import torch
         self.p = ext_params(q, k, v, mask, _tptr(dst), scale, 0, 0, kv_chunk)
         ws = workspace_size(self.p)
-        self.workspace = torch.empty(max(ws, 16), dtype=torch.uint8, device=dst.device)
+        # zero-filled once: the chunk-arrival counters at its front must start at 0
+        self.workspace = torch.zeros(max(ws, 16), dtype=torch.uint8, device=dst.device)
         self.p.workspace = _tptr(self.workspace)
         self.p.workspace_bytes = self.workspace.numel()
         self.dst = dst
@@ -250,7 +253,7 @@ def row(query, key, value_t, mask, qkv, head_dim: int, kv_size: int, num_heads: 
     import torch
     need = int(lib().fattn_row_workspace_size(head_dim, kv_size, num_heads))
     if tmp is None:
-        tmp = torch.empty(max(need, 16), dtype=torch.uint8, device=qkv.device)
+        tmp = torch.zeros(max(need, 16), dtype=torch.uint8, device=qkv.device)
     _check(lib().fattn_row(_tptr(query), _tptr(key), _tptr(value_t), _tptr(mask) if mask is not None else None,
                            _tptr(tmp), tmp.numel() * tmp.element_size(), _tptr(qkv), head_dim, kv_size, num_heads,
                            float(scale), head_stride, r_kv_heads, _stream(stream)), "fattn_row")

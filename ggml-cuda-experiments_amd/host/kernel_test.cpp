@@ -264,6 +264,10 @@ int main(int argc, const char* argv[]) {
     HIP_CHECK(hipMalloc(&d_ws, std::max<size_t>(ws, 16)));
     p.workspace = d_ws;
     p.workspace_bytes = std::max<size_t>(ws, 16);
+    if (int zr = fattn_workspace_init(d_ws, p.workspace_bytes, stream)) {
+        fprintf(stderr, "fattn_workspace_init failed: %s\n", fattn_strerror(zr));
+        return 2;
+    }
 
     int rc = fattn_ext(&p, stream);
     if (rc) {

@@ -93,11 +93,17 @@ typedef struct fattn_params {
     float* dst;
     float scale;
     int32_t kv_chunk;      /* split-KV chunk length in positions; 0 = auto */
-    void* workspace;       /* split-KV scratch, >= fattn_workspace_size() bytes */
+    void* workspace;       /* split-KV scratch, >= fattn_workspace_size() bytes, zero-filled
+                              before its first use (fattn_workspace_init); every launch
+                              leaves it re-armed, so zero it once per allocation */
     size_t workspace_bytes;
 } fattn_params;
 
 size_t fattn_workspace_size(const fattn_params* p);
+/* Zero a freshly allocated workspace (hipMemsetAsync on `stream`).  Needed once
+ * per allocation: the split-KV chunks of a tile meet through arrival counters
+ * kept at the front of the workspace, and each launch leaves them at zero. */
+int fattn_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 int fattn_ext(const fattn_params* p, void* stream);
 
 /* Same as fattn_ext, additionally recording the hipEvent_t `ev_begin` / `ev_end`
@@ -116,7 +122,8 @@ int fattn_ext_f16_launch(const void* q, const void* k, const void* v, const void
 
 /* flash_attn_row + fa_reduce (flash_row_float.h): query f32 [H][D], key f16
  * [Hkv][N][D] (head_stride = D*N elements), value f16 [Hkv][D][N], mask f16 [N],
- * qkv f32 [H][D]; r_kv_heads = H / Hkv.  tmp: >= fattn_row_workspace_size(). */
+ * qkv f32 [H][D]; r_kv_heads = H / Hkv.  tmp: >= fattn_row_workspace_size(),
+ * zero-filled once after allocation (as for fattn_params.workspace). */
 size_t fattn_row_workspace_size(int head_dim, int kv_size, int num_heads);
 int fattn_row(const float* query, const void* key, const void* value, const void* mask, void* tmp,
               size_t tmp_bytes, float* qkv, int head_dim, int kv_size, int num_heads, float scale,

@@ -174,7 +174,7 @@ def test_ext_f16_launch_positional(dev):
     p = make_problem(D=128, NQ=1, H=32, Hkv=8, N=512, kv_type="f16", mask="random", seed=12, mask_pad=512)
     t = upload(p, dev)
     L = fattn.lib()
-    ws = torch.empty(1 << 22, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(1 << 22, dtype=torch.uint8, device=dev)
     D, N = 128, 512
     mrows = p.mask_bits.shape[0]
     rc = L.fattn_ext_f16_launch(
@@ -204,3 +204,46 @@ def test_graph_capture(dev):
     g.replay()
     torch.cuda.synchronize()
     assert attn_rel_err(t["dst"].cpu().numpy(), p.oracle()) <= RTOL
+
+
+def test_chunk_merge_handoff_stress(dev):
+    """The last-arriving workgroup of a tile merges the chunk partials of the
+    others (sc1 stores -> drain -> agent atomic add -> sc1 loads).  Stress the
+    hand-off the way MI355X_MICROARCH.md asks: one workspace reused across
+    plans with different chunk counts (the arrival counters must re-arm to
+    zero), a competing copy stream for uneven load, and every output word
+    checked on every launch."""
+    import torch
+    p = make_problem(D=128, NQ=1, H=32, Hkv=8, N=4096, kv_type="q8_0", seed=21)
+    ref = p.oracle()
+    t = upload(p, dev)
+    qv, kv, vv, mv = views(p, t)
+    ws_bytes = 0
+    atts = []
+    for chunk in (128, 256, 512, 1024, 0):
+        a = fattn.Attention(qv, kv, vv, mv, t["dst"], p.scale, kv_chunk=chunk)
+        atts.append(a)
+        ws_bytes = max(ws_bytes, a.workspace.numel())
+    shared = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
+    for a in atts:
+        a.workspace = shared
+        a.p.workspace = shared.data_ptr()
+        a.p.workspace_bytes = shared.numel()
+    noise_src = torch.randn(1 << 26, device=dev)
+    noise_dst = torch.empty_like(noise_src)
+    side = torch.cuda.Stream()
+    multi = 0
+    for it in range(40):
+        with torch.cuda.stream(side):
+            for _ in range(it % 4):
+                noise_dst.copy_(noise_src)
+        t["dst"].fill_(float("nan"))
+        att = atts[it % len(atts)]
+        att()
+        torch.cuda.synchronize()
+        multi += fattn.workspace_size(att.p) > 0
+        got = t["dst"].cpu().numpy()
+        assert attn_rel_err(got, ref) <= RTOL, f"iteration {it} (plan {it % len(atts)})"
+    assert multi > 0
+    # counters re-armed: the 8 tiles' counters (one 256-B line each) are zero again
+    assert int(shared[: 8 * 256].view(torch.int32).abs().sum()) == 0

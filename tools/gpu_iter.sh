@@ -7,4 +7,4 @@ run sweep 600 python tools/sweep_chunk.py
 run stamps_auto 200 python tools/stamps.py
 run nocomp_auto 200 python tools/stamps.py --nocompute
 run prof_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline
-run bench 600 python bench.py
+run bench 600 python bench.py --cpu-seconds 3

@@ -1,6 +1,8 @@
 #!/bin/bash
+# stamp timelines for several split geometries (compute and memory-only builds)
 source tools/gpu_round.sh
-run stamps_auto 200 python tools/stamps.py
-run stamps_256 200 python tools/stamps.py --kv-chunk 256
-run stamps_512 200 python tools/stamps.py --kv-chunk 512
-run stamps_4096 200 python tools/stamps.py --kv-chunk 4096
+export TMPDIR=/tmp
+for ch in 0 256 512 1024; do
+  run stamps_c$ch 200 python tools/stamps.py --kv-chunk $ch
+  run nocomp_c$ch 200 python tools/stamps.py --kv-chunk $ch --nocompute
+done

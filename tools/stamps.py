@@ -1,9 +1,10 @@
 """Per-wave phase timeline of the split kernel (diagnostic build libfattn_stamps.so).
 
-Stamps (s_memrealtime, 100 MHz = 10 ns) per wave:
- 0 start  1 first LDS-DMA issued  2 first step's data in LDS  3 loop done
- 4 4-wave merge barrier passed  5 end (partial or output stored)
-Usage: python tools/stamps.py [--kv-chunk N] [--kv-type q8_0] ...
+Stamps (s_memrealtime, 100 MHz = 10 ns) per wave, see fattn_split.h:
+ 0 start  1 first steps issued  2+s data of step s in LDS (s < 8)
+ 10 loop done  11 4-wave merge done  12 partial published / output stored
+ 13 tile merge done (last workgroup of a tile only)
+Usage: python tools/stamps.py [--kv-chunk N] [--kv-type q8_0] [--nocompute] ...
 """
 import argparse
 import ctypes as C
@@ -18,6 +19,25 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import fattn  # noqa: E402
+
+NS = 16
+
+
+def att_chunks(att):
+    """n_chunks of the plan: workspace = epochs + tagged partials (fattn_api.hip)."""
+    ws = fattn.workspace_size(att.p)
+    if ws == 0:
+        return 1
+    q = att.p.q
+    D, NQ, H = q.ne[0], q.ne[1], q.ne[2]
+    Hkv = att.p.k.ne[2]
+    r = H // Hkv
+    R = min(r, 16)
+    QPT = 16 // R
+    Y = Hkv * ((r + R - 1) // R) * ((NQ + QPT - 1) // QPT)
+    S = q.ne[3]
+    per_chunk = S * Y * 16 * (D // 2 + 1) * 16
+    return (ws - S * Y * 256) // per_chunk
 
 
 def main():
@@ -52,7 +72,7 @@ def main():
                           fattn.kv_view(sets[0][1], typ, D, N, Hkv), fattn.mask_view(mask), out, D ** -0.5,
                           kv_chunk=args.kv_chunk)
     nblk = 65536 * 4
-    st = torch.zeros(nblk * 4 * 8, dtype=torch.int64, device=dev)
+    st = torch.zeros(nblk * 4 * NS, dtype=torch.int64, device=dev)
     for i in range(6):
         att.retarget(k=sets[i][0].data_ptr(), v=sets[i][1].data_ptr())
         att()
@@ -65,23 +85,44 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     L.fattn_debug_set_stamps(None)
-    s = st.cpu().numpy().reshape(-1, 8).astype(np.int64)
+    s = st.cpu().numpy().reshape(-1, NS).astype(np.int64)
     s = s[s[:, 0] != 0]
     t0 = s[:, 0].min()
-    rel = lambda k: (s[:, k] - t0) * 0.01  # us
+    us = lambda k: (s[:, k] - t0) * 0.01
+    have = lambda k: s[:, k] > 0
     print(f"waves {len(s)}  event time {e0.elapsed_time(e1) * 1e3:.1f} us  "
-          f"stamp span {(s[:, :6].max() - t0) * 0.01:.2f} us")
-    pct = lambda a: " ".join(f"{np.percentile(a, p):6.2f}" for p in (0, 10, 50, 90, 100))
-    print("                          min    p10    p50    p90    max  (us)")
-    print("start                    ", pct(rel(0)))
-    print("dma issued   (1-0)       ", pct((s[:, 1] - s[:, 0]) * 0.01))
-    print("data arrival (2)         ", pct(rel(2)[s[:, 2] > 0]))
-    print("wait data    (2-1)       ", pct(((s[:, 2] - s[:, 1]) * 0.01)[s[:, 2] > 0]))
-    print("loop         (3-2)       ", pct(((s[:, 3] - s[:, 2]) * 0.01)[s[:, 2] > 0]))
-    print("loop done    (3)         ", pct(rel(3)))
-    print("merge barrier(4-3)       ", pct((s[:, 4] - s[:, 3]) * 0.01))
-    print("store       (5-4)       ", pct((s[:, 5] - s[:, 4]) * 0.01))
-    print("end          (5)         ", pct(rel(5)))
+          f"stamp span {(s.max() - t0) * 0.01:.2f} us")
+    pct = lambda a: " ".join(f"{np.percentile(a, p):6.2f}" for p in (0, 10, 50, 90, 100)) if len(a) else "   -"
+    print("                          min    p10    p50    p90    max  (us since first wave start)")
+    print("start                    ", pct(us(0)))
+    print("steps issued             ", pct(us(1)))
+    for k in range(8):
+        if have(2 + k).any():
+            print(f"data step {k}              ", pct(us(2 + k)[have(2 + k)]))
+    print("loop done                ", pct(us(10)))
+    print("merge done               ", pct(us(11)[have(11)]))
+    print("published/stored         ", pct(us(12)[have(12)]))
+    print("tile merge done (last wg)", pct(us(13)[have(13)]))
+    # chunk hand-off, per tile (grid x = chunk; block-major stamp layout)
+    nch = att_chunks(att)
+    if nch > 1:
+        blk = st.cpu().numpy().reshape(-1, 4, NS).astype(np.int64)
+        nb = (blk[:, 0, 0] != 0).sum()
+        blk = blk[:nb].reshape(-1, nch, 4, NS)
+        w = lambda k: (blk[..., k].max(axis=2) - t0) * 0.01   # latest wave of each block
+        last_pub = w(12)[:, 1:].max(axis=1)
+        merger_ready = w(11)[:, 0]
+        done = w(13)[:, 0]
+        print(f"tiles {len(blk)} x {nch} chunks")
+        print("last producer published   ", pct(last_pub))
+        print("merger own work done      ", pct(merger_ready))
+        print("merge done                ", pct(done))
+        print("done - max(pub, ready)    ", pct(done - np.maximum(last_pub, merger_ready)))
+    # per-step compute: gap between consecutive step arrivals
+    for k in range(1, 8):
+        m = have(2 + k) & have(1 + k)
+        if m.any():
+            print(f"step {k - 1}->{k} gap          ", pct((s[m, 2 + k] - s[m, 1 + k]) * 0.01))
 
 
 if __name__ == "__main__":
