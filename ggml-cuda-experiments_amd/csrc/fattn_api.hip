@@ -281,6 +281,16 @@ extern "C" {
 int fattn_debug_set_stamps(void* dev_ptr) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(void*)) == hipSuccess ? 0 : -1;
 }
+// grid of the plan: out[0..2] = chunks, Y, S
+int fattn_debug_plan(const fattn_params* p, int* out) {
+    Plan pl;
+    const int rc = make_plan(p, pl);
+    if (rc) return rc;
+    out[0] = (int)pl.grid.x;
+    out[1] = (int)pl.grid.y;
+    out[2] = (int)pl.grid.z;
+    return 0;
+}
 #endif
 
 const char* fattn_version(void) { return "fattn-gfx950 0.1"; }

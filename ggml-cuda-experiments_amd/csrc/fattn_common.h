@@ -161,19 +161,22 @@ __device__ __forceinline__ float wave_sum(float x) {
 // inline asm, so the compiler does not track them: callers drain with an
 // explicit s_waitcnt vmcnt(0) and pass every loaded value through reg_fence()
 // after that wait, so no use can be scheduled above it.
-__device__ __forceinline__ void st_sc1(float* p, f32x4 v) {
+__device__ __forceinline__ void st_sc1(void* p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
-__device__ __forceinline__ void st_sc1(float* p, f32x2 v) {
+__device__ __forceinline__ void st_sc1_x2(void* p, u32x2 v) {
     asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
-__device__ __forceinline__ f32x4 ld_sc1(const float* p) {
-    f32x4 v;
+// Integer vector operands only: with a float-vector "+v"/"=v" operand hipcc
+// (ROCm 7.2) mis-assigned the elements of the result (a bit_cast of .y read
+// the register of .x), caught by the chunk-merge stress test.
+__device__ __forceinline__ u32x4 ld_sc1(const void* p) {
+    u32x4 v;
     asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
     return v;
 }
-__device__ __forceinline__ f32x2 ld_sc1_x2(const float* p) {
-    f32x2 v;
+__device__ __forceinline__ u32x2 ld_sc1_x2(const void* p) {
+    u32x2 v;
     asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
     return v;
 }
@@ -182,8 +185,11 @@ __device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
     asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
     return v;
 }
+// keeps uses of an asm-loaded value below the preceding explicit wait
+// (integer scalars / vectors only, see ld_sc1)
 template <typename T>
 __device__ __forceinline__ void reg_fence(T& v) {
+    static_assert(!__is_same(T, f32x4) && !__is_same(T, f32x2), "float vector asm operands are miscompiled");
     asm volatile("" : "+v"(v));
 }
 

@@ -386,8 +386,17 @@ __device__ unsigned long long* g_stamps;
             g_stamps[(blk_ * kSplitWaves + wave) * 16 + (k)] = t_;                                \
         }                                                                                       \
     } while (0)
+// any lane: slot k of wave 0's record = max(slot, v)
+#define FATTN_STAMP_MAX(k, v)                                                                   \
+    do {                                                                                        \
+        if (g_stamps) {                                                                         \
+            const int64_t blk_ = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
+            atomicMax(&g_stamps[blk_ * kSplitWaves * 16 + (k)], (unsigned long long)(v));      \
+        }                                                                                       \
+    } while (0)
 #else
 #define FATTN_STAMP(k) do { } while (0)
+#define FATTN_STAMP_MAX(k, v) do { } while (0)
 #endif
 
 // ---------------------------------------------------------------- kernel
@@ -399,7 +408,7 @@ constexpr int own_off() {
 }
 template <int D>
 constexpr int combine_lds_bytes() {
-    return own_off<D>() + kRows * D * 4 + kRows * 2 * 4 + 16;  // + last-arriver flag
+    return own_off<D>() + kRows * D * 4 + kRows * 2 * 4 + 16;  // + arrival info
 }
 
 template <int D>
@@ -758,10 +767,11 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     const int64_t tile = (int64_t)iq3 * gridDim.y + y;
     if (tm < rv) {
         const int64_t slot = (tile * a.n_chunks + chunk) * kRows + tm;
+        auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
 #pragma unroll
         for (int e = 0; e < EPT; e += 4)
-            st_sc1(a.ws_o + slot * D + d0 + e, f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]});
-        if (tj == 0) st_sc1(a.ws_ml + 2 * slot, f32x2{M, L});
+            st_sc1(a.ws_o + slot * D + d0 + e, u32x4{bits(acc[e]), bits(acc[e + 1]), bits(acc[e + 2]), bits(acc[e + 3])});
+        if (tj == 0) st_sc1_x2(a.ws_ml + 2 * slot, u32x2{bits(M), bits(L)});
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef FATTN_DIAG_NOATOMIC
@@ -797,9 +807,10 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
 // flash_row_float.h:415-472, in fp32 and parallel), run by the tile's last
 // workgroup; its own partial comes from LDS.  16 thread groups = rv rows x G
 // chunk subsets.  Every thread issues its (m, l) load and its first batch of
-// partial loads before one wait (one memory round trip for the common case
+// partial loads before one wait (one memory round trip when
 // ceil(n_chunks / G) <= CB); the (m, l) pairs reduce with segmented
-// xor-shuffles in a fixed order (deterministic).
+// xor-shuffles (compile-time lane offsets: DPP, not LDS permutes) in a fixed
+// order (deterministic).
 template <int D>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
                                              int rv, int own_chunk, uint8_t* smem) {
@@ -818,10 +829,10 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
     const int r = grp / G, cg = grp % G;
     const bool active = grp < rv * G;
     const int kmax = active ? (NCH - cg + G - 1) / G : 0;
-
+    auto fl = [](uint32_t x) { return __builtin_bit_cast(float, x); };
     // partial loads of chunks cg + (k0 + kk) * G (clamped index, zero weight
     // past kmax; the own chunk is read from LDS instead)
-    auto issue = [&](f32x4 (&v)[CB][EPT / 4], int k0) {
+    auto issue = [&](u32x4 (&v)[CB][EPT / 4], int k0) {
 #pragma unroll
         for (int kk = 0; kk < CB; kk++) {
             const int c = min(cg + (k0 + kk) * G, NCH - 1);
@@ -830,28 +841,36 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
             for (int e = 0; e < EPT / 4; e++) v[kk][e] = ld_sc1(wo + 4 * e);
         }
     };
-    f32x4 v[CB][EPT / 4];
+    auto fence_all = [&](u32x4 (&v)[CB][EPT / 4]) {
+#pragma unroll
+        for (int kk = 0; kk < CB; kk++) {
+#pragma unroll
+            for (int e = 0; e < EPT / 4; e++) reg_fence(v[kk][e]);
+        }
+    };
+    u32x4 v[CB][EPT / 4];
     issue(v, 0);
     // (m, l) of chunk c of row r in thread r * NCP + c (NCP = next power of
     // two >= NCH, <= 64)
     const int NCP = a.ncp;
     const int mr = threadIdx.x / NCP, mc = threadIdx.x % NCP;
     const bool has_ml = mr < rv && mc < NCH;
-    f32x2 ml = ld_sc1_x2(a.ws_ml + 2 * ((sb + min(mc, NCH - 1)) * kRows + (has_ml ? mr : 0)));
+    u32x2 mlb = ld_sc1_x2(a.ws_ml + 2 * ((sb + min(mc, NCH - 1)) * kRows + (has_ml ? mr : 0)));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    reg_fence(ml);
-#pragma unroll
-    for (int kk = 0; kk < CB; kk++) {
-#pragma unroll
-        for (int e = 0; e < EPT / 4; e++) reg_fence(v[kk][e]);
-    }
+    reg_fence(mlb);
+    fence_all(v);
+    f32x2 ml = {fl(mlb.x), fl(mlb.y)};
     if (has_ml && mc == own_chunk) ml = *(const f32x2*)(own_ml + 2 * mr);
     if (!has_ml) ml = f32x2{kNegInf, 0.0f};
     float Mr = ml.x;
-    for (int o = 1; o < NCP; o <<= 1) Mr = fmaxf(Mr, __shfl_xor(Mr, o, kWave));
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+        if (o < NCP) Mr = fmaxf(Mr, __shfl_xor(Mr, o, kWave));
     const float wt = (ml.x == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(ml.x - Mr);
     float Lr = wt * ml.y;
-    for (int o = 1; o < NCP; o <<= 1) Lr += __shfl_xor(Lr, o, kWave);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+        if (o < NCP) Lr += __shfl_xor(Lr, o, kWave);
     if (mr < rv) {
         wts[mr][mc] = wt;
         if (mc == 0) rowL[mr] = Lr;
@@ -867,11 +886,7 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
             if (k0 > 0) {
                 issue(v, k0);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                for (int kk = 0; kk < CB; kk++) {
-#pragma unroll
-                    for (int e = 0; e < EPT / 4; e++) reg_fence(v[kk][e]);
-                }
+                fence_all(v);
             }
 #pragma unroll
             for (int kk = 0; kk < CB; kk++) {
@@ -883,20 +898,20 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
                 } else {
 #pragma unroll
                     for (int e = 0; e < EPT / 4; e++) {
-                        s8[4 * e] += w * v[kk][e].x;
-                        s8[4 * e + 1] += w * v[kk][e].y;
-                        s8[4 * e + 2] += w * v[kk][e].z;
-                        s8[4 * e + 3] += w * v[kk][e].w;
+                        s8[4 * e] += w * fl(v[kk][e].x);
+                        s8[4 * e + 1] += w * fl(v[kk][e].y);
+                        s8[4 * e + 2] += w * fl(v[kk][e].z);
+                        s8[4 * e + 3] += w * fl(v[kk][e].w);
                     }
                 }
             }
         }
 #pragma unroll
-        for (int e = 0; e < EPT; e++) red[grp][d0 + e] = s8[e];
+        for (int e = 0; e < EPT; e += 4) *(f32x4*)&red[grp][d0 + e] = f32x4{s8[e], s8[e + 1], s8[e + 2], s8[e + 3]};
     }
     __syncthreads();
 
-    // sum the G subsets of each row, normalise, store
+    // sum the G subsets of each row (16-B LDS reads), normalise, store
     if (grp < rv) {
         const float Lrow = rowL[grp];
         const float inv = 1.0f / Lrow;
@@ -906,13 +921,13 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
         float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + d0;
 #pragma unroll
         for (int e = 0; e < EPT; e += 4) {
+            f32x4 x = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int k = 0; k < kRows; k++)
+                if (k < G) x += *(const f32x4*)&red[grp * G + k][d0 + e];
             f32x4 o4;
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                float x = 0.0f;
-                for (int k = 0; k < G; k++) x += red[grp * G + k][d0 + e + j];
-                o4[j] = (Lrow == 0.0f) ? __builtin_nanf("") : x * inv;
-            }
+            for (int j = 0; j < 4; j++) o4[j] = (Lrow == 0.0f) ? __builtin_nanf("") : x[j] * inv;
             *(f32x4*)(out + e) = o4;
         }
     }

@@ -104,20 +104,24 @@ def main():
     print("published/stored         ", pct(us(12)[have(12)]))
     print("tile merge done (last wg)", pct(us(13)[have(13)]))
     # chunk hand-off, per tile (grid x = chunk; block-major stamp layout)
-    nch = att_chunks(att)
+    L.fattn_debug_plan.argtypes = [C.c_void_p, C.c_void_p]
+    g = (C.c_int * 3)()
+    assert L.fattn_debug_plan(C.byref(att.p), g) == 0
+    nch, ny, nz = g[0], g[1], g[2]
     if nch > 1:
-        blk = st.cpu().numpy().reshape(-1, 4, NS).astype(np.int64)
-        nb = (blk[:, 0, 0] != 0).sum()
-        blk = blk[:nb].reshape(-1, nch, 4, NS)
-        w = lambda k: (blk[..., k].max(axis=2) - t0) * 0.01   # latest wave of each block
-        last_pub = w(12)[:, 1:].max(axis=1)
-        merger_ready = w(11)[:, 0]
-        done = w(13)[:, 0]
+        blk = st.cpu().numpy().reshape(-1, 4, NS)[: nch * ny * nz].astype(np.int64)
+        blk = blk.reshape(-1, nch, 4, NS)
+        wmax = lambda k: (blk[..., k].max(axis=2) - t0) * 0.01   # latest wave of each block
+        last = blk[..., 0, 13] > 0                                 # the merging block of each tile
+        t11, t12, t13 = wmax(11), wmax(12), wmax(13)
         print(f"tiles {len(blk)} x {nch} chunks")
-        print("last producer published   ", pct(last_pub))
-        print("merger own work done      ", pct(merger_ready))
-        print("merge done                ", pct(done))
-        print("done - max(pub, ready)    ", pct(done - np.maximum(last_pub, merger_ready)))
+        print("4-wave merge done, all    ", pct(t11.reshape(-1)))
+        print("published+atomic, all     ", pct(t12.reshape(-1)))
+        print("  (12-11) drain+atomic    ", pct((t12 - t11).reshape(-1)))
+        print("last wg: merge done (13)  ", pct(t13[last]))
+        print("last wg: 13-12 combine    ", pct((t13 - t12)[last]))
+        print("last wg: 12 - max others11", pct(np.array([t12[i][last[i]].max() - np.delete(t11[i], np.where(last[i])[0]).max()
+                                                          for i in range(len(blk))])))
     # per-step compute: gap between consecutive step arrivals
     for k in range(1, 8):
         m = have(2 + k) & have(1 + k)
