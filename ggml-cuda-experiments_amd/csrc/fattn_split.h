@@ -426,6 +426,11 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     constexpr int NC = D / 16;   // 16-wide output column groups (MFMA tiles of O^T)
     constexpr float kNegInf = -__builtin_inff();
     constexpr bool kVQ8 = C::VTT == FATTN_TYPE_Q8_0;
+    constexpr bool kVQ = C::VTT != FATTN_TYPE_F16;
+    // quantised V: the A operand is the exact integer code plus the magic-number
+    // offset (1152 for Q8_0, 1032 for Q4_0) with the block scale folded into P;
+    // corr[b] accumulates sum(P * d_b) so the offset comes off once at the end
+    constexpr float kVOff = kVQ8 ? 1152.0f : 1032.0f;
 
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane lets the compiler see it, so the
@@ -514,6 +519,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     f32x4 o[NC];
 #pragma unroll
     for (int c = 0; c < NC; c++) o[c] = f32x4{0, 0, 0, 0};
+    float corr[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) corr[b] = 0.0f;
 
     const float log2e = 1.4426950408889634f;
     int cur = 0;  // buffer of step s
@@ -564,10 +572,12 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
                 mk[0] = (float)m01.x; mk[1] = (float)m01.y; mk[2] = (float)m23.x; mk[3] = (float)m23.y;
             }
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const float x = st[t][r] * a.scale_log2 + mk[r] * log2e;
-                sv[4 * t + r] = (16 * t + 4 * g + r) < nvalid ? x : kNegInf;
-            }
+            for (int r = 0; r < 4; r++) sv[4 * t + r] = st[t][r] * a.scale_log2 + mk[r] * log2e;
+        }
+        if (nvalid < kStep) {  // wave-uniform: only a slice's partial last step
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (16 * (j >> 2) + 4 * g + (j & 3) >= nvalid) sv[j] = kNegInf;
         }
 
         // -- online softmax for column m (the 4 lanes l, l^16, l^32, l^48 share it)
@@ -576,11 +586,16 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
         tmax = grp4_max(tmax);
         const float m_new = fmaxf(m_run, tmax);
         const float m_use = (m_new == kNegInf) ? 0.0f : m_new;
-        if (__builtin_amdgcn_ballot_w64(m_new != m_run)) {  // rescale only when a max moved
+        // rescale only when a max moved (never at the first step: o, l are still 0)
+        if (s > 0 && __builtin_amdgcn_ballot_w64(m_new != m_run)) {
             const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
             l_run *= alpha;
 #pragma unroll
             for (int c = 0; c < NC; c++) o[c] *= alpha;
+            if constexpr (kVQ) {
+#pragma unroll
+                for (int b = 0; b < NB; b++) corr[b] *= alpha;
+            }
         }
         m_run = m_new;
         float pv[8];
@@ -612,6 +627,17 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
                 const uint32_t sel = ((BB * b) & 2) ? 0x07060302u : 0x05040100u;  // b is unrolled
                 const f16x2 d01 = as_h2(perm_b32(sw[1], sw[0], sel)), d23 = as_h2(perm_b32(sw[3], sw[2], sel));
                 const f16x2 d45 = as_h2(perm_b32(sw[5], sw[4], sel)), d67 = as_h2(perm_b32(sw[7], sw[6], sel));
+                // P'_b = P * d_b (element j <-> row of element j of the A operand)
+                f16x8 pbd;
+                pbd.s01 = pb.s01 * d01;
+                pbd.s23 = pb.s23 * d23;
+                pbd.s45 = pb.s45 * d45;
+                pbd.s67 = pb.s67 * d67;
+                const f16x2 one2 = {(f16)1.0f, (f16)1.0f};
+                corr[b] = __builtin_amdgcn_fdot2(pbd.s01, one2, corr[b], false);
+                corr[b] = __builtin_amdgcn_fdot2(pbd.s23, one2, corr[b], false);
+                corr[b] = __builtin_amdgcn_fdot2(pbd.s45, one2, corr[b], false);
+                corr[b] = __builtin_amdgcn_fdot2(pbd.s67, one2, corr[b], false);
                 if constexpr (kVQ8) {
                     // one u16 per row carries columns 2i (-> tile E_b) and 2i+1 (-> tile O_b)
                     const uint8_t* cp = vb + b * BB + 2 + 2 * i16;
@@ -621,20 +647,16 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
                         w[r] = *(const uint16_t*)(cp + (rA + r) * C::rowV);
                         w[4 + r] = *(const uint16_t*)(cp + (rB + r) * C::rowV);
                     }
-                    f16x8 ae, ao;
-                    const f16x2 off = {(f16)-1152.0f, (f16)-1152.0f};
-                    const f16x2 dd[4] = {d01, d23, d45, d67};
+                    u32x4 ae, ao;  // f16 pairs 1152 + q (exact)
 #pragma unroll
                     for (int pr = 0; pr < 4; pr++) {
                         // bytes [e_r, o_r, e_r+1, o_r+1] -> xor 0x80 -> f16 magic 0x64xx
                         const uint32_t t2 = (w[2 * pr] | (w[2 * pr + 1] << 16)) ^ 0x80808080u;
-                        const f16x2 ve = (as_h2(perm_b32(0x64646464u, t2, 0x04020400u)) + off) * dd[pr];
-                        const f16x2 vo = (as_h2(perm_b32(0x64646464u, t2, 0x04030401u)) + off) * dd[pr];
-                        ae[2 * pr] = ve.x; ae[2 * pr + 1] = ve.y;
-                        ao[2 * pr] = vo.x; ao[2 * pr + 1] = vo.y;
+                        ae[pr] = perm_b32(0x64646464u, t2, 0x04020400u);
+                        ao[pr] = perm_b32(0x64646464u, t2, 0x04030401u);
                     }
-                    o[2 * b] = mfma16(ae, pb, o[2 * b]);
-                    o[2 * b + 1] = mfma16(ao, pb, o[2 * b + 1]);
+                    o[2 * b] = mfma16(__builtin_bit_cast(f16x8, ae), pbd, o[2 * b]);
+                    o[2 * b + 1] = mfma16(__builtin_bit_cast(f16x8, ao), pbd, o[2 * b + 1]);
                 } else {  // Q4_0: byte i carries column i (low nibble) and 16+i (high nibble)
                     const uint8_t* cp = vb + b * BB + 2 + i16;
                     uint32_t w[8];
@@ -643,19 +665,15 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
                         w[r] = cp[(rA + r) * C::rowV];
                         w[4 + r] = cp[(rB + r) * C::rowV];
                     }
-                    f16x8 al, ah;
-                    const f16x2 off = {(f16)-1032.0f, (f16)-1032.0f};
-                    const f16x2 dd[4] = {d01, d23, d45, d67};
+                    u32x4 al, ah;  // f16 pairs 1032 + (nib - 8) (exact)
 #pragma unroll
                     for (int pr = 0; pr < 4; pr++) {
                         const uint32_t x = w[2 * pr] | (w[2 * pr + 1] << 16);
-                        const f16x2 vl = (as_h2((x & 0x000F000Fu) | 0x64006400u) + off) * dd[pr];
-                        const f16x2 vh = (as_h2(((x >> 4) & 0x000F000Fu) | 0x64006400u) + off) * dd[pr];
-                        al[2 * pr] = vl.x; al[2 * pr + 1] = vl.y;
-                        ah[2 * pr] = vh.x; ah[2 * pr + 1] = vh.y;
+                        al[pr] = (x & 0x000F000Fu) | 0x64006400u;
+                        ah[pr] = ((x >> 4) & 0x000F000Fu) | 0x64006400u;
                     }
-                    o[2 * b] = mfma16(al, pb, o[2 * b]);
-                    o[2 * b + 1] = mfma16(ah, pb, o[2 * b + 1]);
+                    o[2 * b] = mfma16(__builtin_bit_cast(f16x8, al), pbd, o[2 * b]);
+                    o[2 * b + 1] = mfma16(__builtin_bit_cast(f16x8, ah), pbd, o[2 * b + 1]);
                 }
             }
         }
@@ -678,6 +696,15 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
 
     // ---- per-wave state -> LDS (this wave's own region), then merge the 4 waves
     const float l_tot = grp4_sum(l_run);
+    if constexpr (kVQ) {
+        // O^T tiles of block b (columns 32b..32b+31) carry kVOff * sum(P'_b) too
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const float cb = kVOff * grp4_sum(corr[b]);
+            o[2 * b] -= cb;
+            o[2 * b + 1] -= cb;
+        }
+    }
     constexpr int MS = C::kMergeStride;
     float* mo = (float*)wbuf;                      // [16][MS]
     float* mml = (float*)(wbuf + kRows * MS * 4);  // [16][2]
