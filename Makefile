@@ -26,7 +26,24 @@ $(LIB): $(CSRC) $(CHDR)
 # diagnostic libraries (tools/stamps.py, tools/variants.py); never loaded by the product path
 stamps: $(LIBDIR)/libfattn_stamps.so $(LIBDIR)/libfattn_nocompute.so $(LIBDIR)/libfattn_nc.so \
         $(LIBDIR)/libfattn_nctail.so $(LIBDIR)/libfattn_notail.so $(LIBDIR)/libfattn_nopub.so \
-        $(LIBDIR)/libfattn_noatomic.so
+        $(LIBDIR)/libfattn_noatomic.so $(LIBDIR)/libfattn_nomem.so $(LIBDIR)/libfattn_nomem_notail.so \
+        $(LIBDIR)/libfattn_nomem_nopub.so $(LIBDIR)/libfattn_stamps_nomem.so
+
+$(LIBDIR)/libfattn_nomem_notail.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DIAG_NOMEM -DFATTN_DIAG_NOTAIL -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_nomem_nopub.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DIAG_NOMEM -DFATTN_DIAG_NOPUBLISH -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_stamps_nomem.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_STAMPS -DFATTN_DIAG_NOMEM -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_nomem.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DIAG_NOMEM -shared $(CSRC) -o $@
 
 $(LIBDIR)/libfattn_nopub.so: $(CSRC) $(CHDR)
 	@mkdir -p $(LIBDIR)

@@ -118,9 +118,6 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
         pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
         pl.ml_bytes = ((size_t)S * Y * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + (size_t)S * Y * a.n_chunks * kRows * pl.D * 4;
-        // the chunk-0 merge reuses the kernel's LDS
-        const int need = pl.D == 128 ? combine_lds_bytes<128>() : combine_lds_bytes<64>();
-        if (pl.lds < need) return FATTN_ERR_INVALID_ARG;
     } else {
         pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
     }

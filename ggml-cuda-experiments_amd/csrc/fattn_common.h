@@ -144,6 +144,27 @@ __device__ __forceinline__ float xor32_pair(float x, bool is_max) {
 __device__ __forceinline__ float grp4_max(float x) { return xor32_pair(xor16_pair(x, true), true); }
 __device__ __forceinline__ float grp4_sum(float x) { return xor32_pair(xor16_pair(x, false), false); }
 
+// Segmented reductions over contiguous power-of-two lane groups of `seg`
+// lanes (seg <= 64, wave-uniform), entirely on the VALU: DPP quad_perm (xor 1,
+// xor 2), row_half_mirror / row_mirror (pair the 4- / 8-lane halves once
+// those are uniform), then the permlane swaps for rows / halves.  Every lane
+// ends with its group's result.  EXEC must be full.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+template <bool IS_MAX>
+__device__ __forceinline__ float seg_reduce(float x, int seg) {
+    auto op = [](float a, float b) { return IS_MAX ? fmaxf(a, b) : a + b; };
+    if (seg > 1) x = op(x, dpp_mov<0xB1>(x));   // quad_perm [1,0,3,2]
+    if (seg > 2) x = op(x, dpp_mov<0x4E>(x));   // quad_perm [2,3,0,1]
+    if (seg > 4) x = op(x, dpp_mov<0x141>(x));  // row_half_mirror
+    if (seg > 8) x = op(x, dpp_mov<0x140>(x));  // row_mirror
+    if (seg > 16) x = xor16_pair(x, IS_MAX);
+    if (seg > 32) x = xor32_pair(x, IS_MAX);
+    return x;
+}
+
 __device__ __forceinline__ float wave_max(float x) {
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) x = fmaxf(x, __shfl_xor(x, m, kWave));

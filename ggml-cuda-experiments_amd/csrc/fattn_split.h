@@ -188,6 +188,9 @@ struct StepSrc {
 template <int KT, int VT, int D, int GRAN, bool HM>
 __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs, int n0, int mrow0, uint8_t* buf,
                                            int lane) {
+#ifdef FATTN_DIAG_NOMEM
+    return;  // diagnostic build only: compute on whatever LDS holds (compute latency)
+#endif
     using C = SplitCfg<KT, VT, D>;
     using P = StepPlan<KT, VT, D, GRAN>;
     const uint32_t kn1 = (uint32_t)a.k_nb1, vn1 = (uint32_t)a.v_nb1;
@@ -401,19 +404,9 @@ __device__ unsigned long long* g_stamps;
 
 // ---------------------------------------------------------------- kernel
 
-// LDS carve of the chunk-0 merge: [red 16 x D][wts 16 x 64][rowL 16] | own O [16 x D] + own (m, l) [16 x 2]
-template <int D>
-constexpr int own_off() {
-    return (kRows * D * 4 + kRows * 64 * 4 + kRows * 4 + 127) / 128 * 128;
-}
-template <int D>
-constexpr int combine_lds_bytes() {
-    return own_off<D>() + kRows * D * 4 + kRows * 2 * 4 + 16;  // + arrival info
-}
-
 template <int D>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
-                                             int rv, int own_chunk, uint8_t* smem);
+                                             int rv, uint8_t* smem);
 
 template <int KT, int VT, int D, int GRAN, bool HM>
 __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4) ? 2 : 4) void fattn_split_kernel(
@@ -689,7 +682,12 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #ifdef FATTN_DIAG_NOTAIL
     // diagnostic build only: stop before the merge / publish tail
-    if (m_run == 12345.0f) a.dst[0] = l_run;  // keep the loop's results alive
+    {
+        float keep = l_run + m_run;  // keep the loop's results (all of O) alive
+#pragma unroll
+        for (int c = 0; c < NC; c++) keep += o[c].x + o[c].y + o[c].z + o[c].w;
+        if (keep == 12345.0f) a.dst[0] = keep;
+    }
     return;
 #endif
     FATTN_STAMP(10);
@@ -800,14 +798,13 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
             st_sc1(a.ws_o + slot * D + d0 + e, u32x4{bits(acc[e]), bits(acc[e + 1]), bits(acc[e + 2]), bits(acc[e + 3])});
         if (tj == 0) st_sc1_x2(a.ws_ml + 2 * slot, u32x2{bits(M), bits(L)});
     }
+    // every storing wave drains: the merging workgroup reads its own partial back too
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef FATTN_DIAG_NOATOMIC
     return;  // diagnostic build only: stop after the published stores drained
 #endif
     __syncthreads();  // every storing wave has drained; every wave is done reading the merge image
-    float* own_o = (float*)(smem + own_off<D>());
-    float* own_ml = own_o + kRows * D;
-    int* last_flag = (int*)(own_ml + kRows * 2);
+    int* last_flag = (int*)smem;
     if (threadIdx.x == 0) {
         uint32_t* cnt = a.ws_cnt + tile * kCntStride;
         const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -816,39 +813,31 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
         if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *last_flag = last;
     }
-    // own partial -> LDS meanwhile (used only if this workgroup merges)
-    if (tm < rv) {
-#pragma unroll
-        for (int e = 0; e < EPT; e += 4) *(f32x4*)(own_o + tm * D + d0 + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
-        if (tj == 0) *(f32x2*)(own_ml + 2 * tm) = f32x2{M, L};
-    }
     __syncthreads();
     FATTN_STAMP(12);
     if (!*last_flag) return;
-    combine_tile<D>(a, tile, qt, hs, ik2, iq3, rv, chunk, smem);
+    combine_tile<D>(a, tile, qt, hs, ik2, iq3, rv, smem);
     FATTN_STAMP(13);
 }
 
 // ---------------------------------------------------------------- combine
 // Log-sum-exp merge of a tile's chunk partials (fa_reduce,
 // flash_row_float.h:415-472, in fp32 and parallel), run by the tile's last
-// workgroup; its own partial comes from LDS.  16 thread groups = rv rows x G
-// chunk subsets.  Every thread issues its (m, l) load and its first batch of
-// partial loads before one wait (one memory round trip when
-// ceil(n_chunks / G) <= CB); the (m, l) pairs reduce with segmented
-// xor-shuffles (compile-time lane offsets: DPP, not LDS permutes) in a fixed
-// order (deterministic).
+// workgroup.  16 thread groups = rv rows x G chunk subsets.  Every thread
+// issues its (m, l) load and its first batch of partial loads before one wait
+// (one memory round trip when ceil(n_chunks / G) <= CB); the (m, l) pairs
+// reduce with VALU segmented reductions (DPP + permlane swaps); the G subsets
+// of a row are summed with all LDS reads in flight at once.  Fixed order:
+// deterministic.
 template <int D>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
-                                             int rv, int own_chunk, uint8_t* smem) {
+                                             int rv, uint8_t* smem) {
     constexpr float kNegInf = -__builtin_inff();
     constexpr int EPT = D / 16;
     constexpr int CB = 2;  // chunks per load batch (register budget of the split kernel)
     float(*red)[D] = (float(*)[D])smem;                                // [16][D]
     float(*wts)[64] = (float(*)[64])(smem + kRows * D * 4);            // [16][64]
     float* rowL = (float*)(smem + kRows * D * 4 + kRows * 64 * 4);     // [16]
-    const float* own_o = (const float*)(smem + own_off<D>());          // [16][D]
-    const float* own_ml = own_o + kRows * D;                           // [16][2]
     const int NCH = a.n_chunks;
     const int G = max(1, kRows / max(rv, 1));
     const int grp = threadIdx.x / 16, tj = threadIdx.x % 16, d0 = tj * EPT;
@@ -857,8 +846,7 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
     const bool active = grp < rv * G;
     const int kmax = active ? (NCH - cg + G - 1) / G : 0;
     auto fl = [](uint32_t x) { return __builtin_bit_cast(float, x); };
-    // partial loads of chunks cg + (k0 + kk) * G (clamped index, zero weight
-    // past kmax; the own chunk is read from LDS instead)
+    // partial loads of chunks cg + (k0 + kk) * G (clamped index, zero weight past kmax)
     auto issue = [&](u32x4 (&v)[CB][EPT / 4], int k0) {
 #pragma unroll
         for (int kk = 0; kk < CB; kk++) {
@@ -886,18 +874,10 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     reg_fence(mlb);
     fence_all(v);
-    f32x2 ml = {fl(mlb.x), fl(mlb.y)};
-    if (has_ml && mc == own_chunk) ml = *(const f32x2*)(own_ml + 2 * mr);
-    if (!has_ml) ml = f32x2{kNegInf, 0.0f};
-    float Mr = ml.x;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1)
-        if (o < NCP) Mr = fmaxf(Mr, __shfl_xor(Mr, o, kWave));
-    const float wt = (ml.x == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(ml.x - Mr);
-    float Lr = wt * ml.y;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1)
-        if (o < NCP) Lr += __shfl_xor(Lr, o, kWave);
+    const float mlm = has_ml ? fl(mlb.x) : kNegInf;
+    const float Mr = seg_reduce<true>(mlm, NCP);
+    const float wt = (mlm == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mlm - Mr);
+    const float Lr = seg_reduce<false>(has_ml ? wt * fl(mlb.y) : 0.0f, NCP);
     if (mr < rv) {
         wts[mr][mc] = wt;
         if (mc == 0) rowL[mr] = Lr;
@@ -919,17 +899,12 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
             for (int kk = 0; kk < CB; kk++) {
                 const int c = cg + (k0 + kk) * G;
                 const float w = (k0 + kk < kmax) ? wts[r][min(c, NCH - 1)] : 0.0f;
-                if (c == own_chunk) {
 #pragma unroll
-                    for (int e = 0; e < EPT; e++) s8[e] += w * own_o[r * D + d0 + e];
-                } else {
-#pragma unroll
-                    for (int e = 0; e < EPT / 4; e++) {
-                        s8[4 * e] += w * fl(v[kk][e].x);
-                        s8[4 * e + 1] += w * fl(v[kk][e].y);
-                        s8[4 * e + 2] += w * fl(v[kk][e].z);
-                        s8[4 * e + 3] += w * fl(v[kk][e].w);
-                    }
+                for (int e = 0; e < EPT / 4; e++) {
+                    s8[4 * e] += w * fl(v[kk][e].x);
+                    s8[4 * e + 1] += w * fl(v[kk][e].y);
+                    s8[4 * e + 2] += w * fl(v[kk][e].z);
+                    s8[4 * e + 3] += w * fl(v[kk][e].w);
                 }
             }
         }
@@ -938,25 +913,25 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
     }
     __syncthreads();
 
-    // sum the G subsets of each row (16-B LDS reads), normalise, store
-    if (grp < rv) {
-        const float Lrow = rowL[grp];
+    // sum the G subsets of each row, normalise, store: thread -> (row, 4 dims),
+    // all of its 16-B LDS reads issued before any is consumed
+    for (int t = threadIdx.x; t < rv * (D / 4); t += kSplitWaves * kWave) {
+        const int rr = t / (D / 4), dq = (t % (D / 4)) * 4;
+        f32x4 part[kRows];
+#pragma unroll
+        for (int k = 0; k < kRows; k++) part[k] = *(const f32x4*)&red[min(rr * G + k, kRows - 1)][dq];
+        f32x4 x = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < kRows; k++) x += (k < G) ? part[k] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const float Lrow = rowL[rr];
         const float inv = 1.0f / Lrow;
-        const int rq = div_R(a, grp);
+        const int rq = div_R(a, rr);
         const int riq1 = qt * a.QPT + rq;
-        const int riq2 = ik2 * a.rk2 + hs * a.R + (grp - rq * a.R);
-        float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + d0;
+        const int riq2 = ik2 * a.rk2 + hs * a.R + (rr - rq * a.R);
+        f32x4 o4;
 #pragma unroll
-        for (int e = 0; e < EPT; e += 4) {
-            f32x4 x = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int k = 0; k < kRows; k++)
-                if (k < G) x += *(const f32x4*)&red[grp * G + k][d0 + e];
-            f32x4 o4;
-#pragma unroll
-            for (int j = 0; j < 4; j++) o4[j] = (Lrow == 0.0f) ? __builtin_nanf("") : x[j] * inv;
-            *(f32x4*)(out + e) = o4;
-        }
+        for (int j = 0; j < 4; j++) o4[j] = (Lrow == 0.0f) ? __builtin_nanf("") : x[j] * inv;
+        *(f32x4*)(a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + dq) = o4;
     }
 }
 

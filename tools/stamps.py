@@ -11,7 +11,8 @@ import ctypes as C
 import os
 import sys
 
-os.environ["FATTN_LIB"] = "libfattn_nocompute.so" if "--nocompute" in sys.argv else "libfattn_stamps.so"
+os.environ["FATTN_LIB"] = ("libfattn_nocompute.so" if "--nocompute" in sys.argv else
+                           "libfattn_stamps_nomem.so" if "--nomem" in sys.argv else "libfattn_stamps.so")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "ggml-cuda-experiments_amd"), ROOT]
 
@@ -49,6 +50,7 @@ def main():
     ap.add_argument("--kv-len", type=int, default=4096)
     ap.add_argument("--n-q", type=int, default=1)
     ap.add_argument("--nocompute", action="store_true", help="memory-only diagnostic build")
+    ap.add_argument("--nomem", action="store_true", help="compute-only diagnostic build")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     D, H, N, NQ = 128, args.heads, args.kv_len, args.n_q
@@ -120,6 +122,10 @@ def main():
         print("  (12-11) drain+atomic    ", pct((t12 - t11).reshape(-1)))
         print("last wg: merge done (13)  ", pct(t13[last]))
         print("last wg: 13-12 combine    ", pct((t13 - t12)[last]))
+        t14, t15 = wmax(14), wmax(15)
+        print("  14-12 loads RT          ", pct((t14 - t12)[last]))
+        print("  15-14 weights+barrier   ", pct((t15 - t14)[last]))
+        print("  13-15 fold+sum+store    ", pct((t13 - t15)[last]))
         print("last wg: 12 - max others11", pct(np.array([t12[i][last[i]].max() - np.delete(t11[i], np.where(last[i])[0]).max()
                                                           for i in range(len(blk))])))
     # per-step compute: gap between consecutive step arrivals
