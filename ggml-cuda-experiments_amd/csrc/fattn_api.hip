@@ -91,6 +91,16 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
             spw++;
         }
     } else {
+        // Quantised K/V: about one 4-wave workgroup per CU, each wave streaming
+        // its slice with two steps in flight -- the measured optimum on the
+        // decode shapes (config 3: 4 steps per wave, config 4: 2), which also
+        // keeps the chunk count per tile (the cross-workgroup merge) small.
+        // f16 (one step in flight): every wave's work co-resident.
+        if (pl.kt != FATTN_TYPE_F16) {
+            const int64_t total = steps * Y * S;
+            spw = (int)std::max<int64_t>(1, (total + (int64_t)kCUs * kSplitWaves / 2) / ((int64_t)kCUs * kSplitWaves));
+            spw = (int)std::min<int64_t>(spw, (steps + kSplitWaves - 1) / kSplitWaves);
+        }
         for (;;) {
             nbuf = (spw == 1 || pl.kt == FATTN_TYPE_F16) ? 1 : 2;
             const int wgs_cu = std::max(1, std::min(vgpr_wgs, kLdsPerCU / G.lds_bytes(nbuf)));
