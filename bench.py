@@ -44,6 +44,7 @@ def hip_events(n):
     hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
     hip.hipEventSynchronize.argtypes = [C.c_void_p]
     hip.hipEventDestroy.argtypes = [C.c_void_p]
+    hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
     evs = []
     for _ in range(n):
         e = C.c_void_p()
@@ -179,7 +180,11 @@ def main():
 
     # 2) the timed job: the K steps (step i reads KV cache i % R) captured
     #    back-to-back into one HIP graph -- the launch-bound inner loop lives on
-    #    the device, not in Python -- and replayed once inside the timed region
+    #    the device, not in Python -- and replayed once inside the timed region.
+    #    One step is exactly one launch of fattn_split_kernel (the chunk merge is
+    #    fused), so HIP events around the replay on the launch stream give the
+    #    kernel's average in-stream duration over the timed region; it agrees
+    #    with rocprofv3's per-dispatch average (profiles/).
     K = args.steps
     gs = torch.cuda.Stream(dev)
     gs.wait_stream(torch.cuda.current_stream(dev))
@@ -197,8 +202,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     gathered = torch.empty((world,) + tuple(outs.shape), dtype=torch.float32, device=dev) if world > 1 else None
+    ev0, ev1 = evs[0], evs[1]
     t0 = time.perf_counter()
+    hip.hipEventRecord(ev0, gs.cuda_stream)
     graph.replay()
+    hip.hipEventRecord(ev1, gs.cuda_stream)
     if world > 1:
         dist.all_gather_into_tensor(gathered, outs)   # the single RCCL gather over xGMI
     torch.cuda.synchronize()
@@ -207,6 +215,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
+    hip.hipEventSynchronize(ev1)
+    kern_ms_eager = kern_ms_avg
+    if hip.hipEventElapsedTime(C.byref(f), ev0, ev1) == 0:
+        kern_ms_avg = f.value / K          # in-stream average over the timed region
     if world > 1:
         t = torch.tensor([elapsed, kern_ms_avg], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -217,6 +229,16 @@ def main():
     total_bytes = bytes_step * args.steps * world
     value = total_bytes / elapsed / 1e9
     achieved = bytes_step / (kern_ms_avg * 1e-3) / 1e9
+    achieved_tf = flops_step / (kern_ms_avg * 1e-3) / 1e12
+    # which kernel the planner picks (fattn_api.hip make_plan): the multi-query
+    # kernel for quantised K/V with >= 32 query rows per kv head (16-B layout)
+    rk2 = H // Hkv
+    mq = (args.kv_type != "f16" and args.layout == "head" and NQ * rk2 >= 32 and rk2 <= 64
+          and rk2 & (rk2 - 1) == 0 and N % 32 == 0)
+    kname = (f"fattn_mq_kernel<{args.kv_type},D{D}>" if mq
+             else f"fattn_split_kernel<{args.kv_type},{args.kv_type},D{D}>")
+    # compute-bound once arithmetic intensity passes the ridge (peak flops / peak bytes)
+    mfma_bound = flops_step / bytes_step > MFMA_F16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
 
     if rank == 0:
         traffic = None
@@ -247,12 +269,15 @@ def main():
                        "bytes_per_step": bytes_step, "flops_per_step": flops_step},
             "tflops": round(flops_step * args.steps * world / elapsed / 1e12, 4),
             "kernel_ms_avg": round(kern_ms_avg, 5),
-            "kernel_ms_median": round(kms[len(kms) // 2], 5),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": f"fattn_split_kernel<{args.kv_type},{args.kv_type},D{D}>"},
+            "kernel_ms_eager_avg": round(kern_ms_eager, 5),
+            "kernel_timing": "HIP events around the timed graph replay on the launch stream, / steps",
+            "roofline": ({"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": MFMA_F16_PEAK_TFLOPS,
+                          "unit": "TFLOP/s", "frac": round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic,
+                          "kernel": kname} if mfma_bound else
+                         {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname}),
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and NQ == 1:  # kernel_test.h's CPU path is one query row
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, min(args.cpu_threads, os.cpu_count() or 1))
         print(json.dumps(res), flush=True)
     for e in evs:
