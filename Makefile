@@ -29,6 +29,20 @@ stamps: $(LIBDIR)/libfattn_stamps.so $(LIBDIR)/libfattn_nocompute.so $(LIBDIR)/l
         $(LIBDIR)/libfattn_noatomic.so $(LIBDIR)/libfattn_nomem.so $(LIBDIR)/libfattn_nomem_notail.so \
         $(LIBDIR)/libfattn_nomem_nopub.so $(LIBDIR)/libfattn_stamps_nomem.so
 
+mqdiag: $(LIBDIR)/libfattn_mq_nomem.so $(LIBDIR)/libfattn_mq_nodeq.so $(LIBDIR)/libfattn_mq_nocomp.so
+
+$(LIBDIR)/libfattn_mq_nomem.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_MQ_NOMEM -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_mq_nodeq.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_MQ_NODEQ -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_mq_nocomp.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_MQ_NOCOMPUTE -shared $(CSRC) -o $@
+
 $(LIBDIR)/libfattn_nomem_notail.so: $(CSRC) $(CHDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DFATTN_DIAG_NOMEM -DFATTN_DIAG_NOTAIL -shared $(CSRC) -o $@

@@ -196,7 +196,8 @@ def main():
     with torch.cuda.graph(graph, stream=gs):
         for i in range(K):
             step(i)
-    graph.replay()   # untimed warm replay
+    with torch.cuda.stream(gs):
+        graph.replay()   # untimed warm replay
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -205,7 +206,8 @@ def main():
     ev0, ev1 = evs[0], evs[1]
     t0 = time.perf_counter()
     hip.hipEventRecord(ev0, gs.cuda_stream)
-    graph.replay()
+    with torch.cuda.stream(gs):
+        graph.replay()   # launches on the current stream: gs, between the events
     hip.hipEventRecord(ev1, gs.cuda_stream)
     if world > 1:
         dist.all_gather_into_tensor(gathered, outs)   # the single RCCL gather over xGMI

@@ -9,10 +9,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
 #include "fattn_quant.h"
+#include "fattn_mq.h"
 #include "fattn_split.h"
 
 using namespace fattn;
@@ -20,6 +23,10 @@ using namespace fattn;
 namespace {
 
 constexpr int kCUs = 256;
+
+// fattn_set_option overrides
+int g_opt_mq_rpw = 0;
+int g_opt_mq_disable = 0;
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -32,6 +39,8 @@ struct Plan {
     dim3 grid;
     int lds;
     size_t ws_bytes, cnt_bytes, ml_bytes;
+    bool mq;  // multi-query kernel (fattn_mq.h)
+    int rpw;  // its packed rows per wave (16 or 64)
 };
 
 // LDS geometry of one instantiation (type-erased for the planner)
@@ -134,6 +143,55 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     return FATTN_OK;
 }
 
+template <int RPW>
+int mq_lds_bytes_r(int kt, int D) {
+    if (kt == FATTN_TYPE_Q8_0)
+        return D == 128 ? MQCfg<FATTN_TYPE_Q8_0, 128, RPW>::ldsBytes : MQCfg<FATTN_TYPE_Q8_0, 64, RPW>::ldsBytes;
+    return D == 128 ? MQCfg<FATTN_TYPE_Q4_0, 128, RPW>::ldsBytes : MQCfg<FATTN_TYPE_Q4_0, 64, RPW>::ldsBytes;
+}
+int mq_lds_bytes(int kt, int D, int rpw) { return rpw == 64 ? mq_lds_bytes_r<64>(kt, D) : mq_lds_bytes_r<16>(kt, D); }
+
+// Multi-query sizing: 4*rpw packed rows per workgroup, KV split only when the
+// (kv head x query tile x seq) workgroups cannot fill the chip (two per CU at
+// rpw 16, one at rpw 64).
+int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
+    SplitArgs& a = pl.a;
+    const int64_t tiles = N / kStep;  // N % kStep == 0 (16-B path)
+    const int64_t base = Y * S;
+    int64_t nch;
+    if (kv_chunk > 0) {
+        nch = (N + kv_chunk - 1) / kv_chunk;
+    } else {
+        const int64_t want = pl.rpw == 64 ? kCUs : 2 * kCUs;
+        nch = (want + base - 1) / base;
+        nch = std::min<int64_t>(nch, std::max<int64_t>(1, tiles / 4));  // >= 4 tiles per workgroup
+    }
+    nch = std::max<int64_t>(1, std::min<int64_t>(nch, tiles));
+    int64_t tpc = (tiles + nch - 1) / nch;
+    for (;;) {  // the merge takes at most 16 chunks for 16-row subtiles
+        nch = (tiles + tpc - 1) / tpc;
+        if (nch == 1 || combine_ok(nch, kRows, pl.D)) break;
+        tpc++;
+    }
+    a.chunk_len = (int)(tpc * kStep);
+    a.n_chunks = (int)nch;
+    a.ncp = 1;
+    while (a.ncp < a.n_chunks) a.ncp <<= 1;
+    a.nbuf = 0;
+    a.wave_bytes = 0;
+    pl.lds = mq_lds_bytes(pl.kt, pl.D, pl.rpw);
+    pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
+    if (a.n_chunks > 1) {
+        const size_t subs = (size_t)S * Y * kSplitWaves * (pl.rpw / kRows);
+        pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
+        pl.ml_bytes = (subs * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
+        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + subs * a.n_chunks * kRows * pl.D * 4;
+    } else {
+        pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
+    }
+    return FATTN_OK;
+}
+
 // Validate and build the launch plan.  Returns FATTN_OK or an error.
 int make_plan(const fattn_params* p, Plan& pl) {
     if (!p || !p->q.data || !p->k.data || !p->v.data || !p->dst) return FATTN_ERR_INVALID_ARG;
@@ -225,13 +283,28 @@ int make_plan(const fattn_params* p, Plan& pl) {
     a.m_span = (uint32_t)m_span;
     a.q_span = (uint32_t)q_span;
 
-    const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
-    if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
     pl.kt = k.type;
     pl.vt = v_trans ? VT_F16T : v.type;
     pl.D = (int)D;
     pl.gran = g16 ? 16 : 4;
-    const int rc = size_split(pl, p->kv_chunk, Y, S, N, NQ);
+    // many query rows per kv head (batched decode, prefill): the multi-query
+    // kernel dequantises each K/V tile once for 64 rows.  Whole head groups
+    // are packed (R = rk2, a power of two <= 64).
+    pl.mq = !g_opt_mq_disable && is_quant(k.type) && g16 && NQ * a.rk2 >= 32 && a.rk2 <= 64 &&
+            (a.rk2 & (a.rk2 - 1)) == 0;
+    if (pl.mq) {
+        // 256 rows per workgroup once that still gives one workgroup per CU
+        const int64_t wg256 = Hkv * S * ((NQ * a.rk2 + 255) / 256);
+        pl.rpw = g_opt_mq_rpw ? g_opt_mq_rpw : wg256 >= kCUs ? 64 : 16;
+        a.R = a.rk2;
+        a.QPT = kSplitWaves * pl.rpw / a.R;
+        a.R_inv = 1.0f / (float)a.R;
+        a.n_hsub = 1;
+        a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
+    }
+    const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
+    if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
+    const int rc = pl.mq ? size_mq(pl, p->kv_chunk, Y, S, N) : size_split(pl, p->kv_chunk, Y, S, N, NQ);
     if (rc != FATTN_OK) return rc;
     return FATTN_OK;
 }
@@ -240,19 +313,43 @@ struct Events {
     hipEvent_t begin = nullptr, end = nullptr;
 };
 
+// Launch with errors attributed to this launch only: a pending error left on
+// the thread by other code is cleared first; FATTN_DEBUG=1 names a failure.
+template <typename F>
+int launch_kernel(const void* kern, const Plan& pl, hipStream_t st, const Events& ev, F&& go) {
+    (void)hipGetLastError();
+    static int lds_set = 65536;  // per kernel instantiation (F is unique per launch site); benign race
+    if (pl.lds > lds_set) {
+        // the query loads the code object (HIP loads kernels lazily; setting an
+        // attribute of a kernel whose module is not loaded yet fails)
+        hipFuncAttributes fa;
+        (void)hipFuncGetAttributes(&fa, kern);
+        if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, pl.lds) == hipSuccess) {
+            lds_set = pl.lds;
+        } else if (std::getenv("FATTN_DEBUG")) {
+            std::fprintf(stderr, "fattn: hipFuncSetAttribute(%d B LDS) failed; launching anyway\n", pl.lds);
+        }
+        (void)hipGetLastError();
+    }
+    if (ev.begin) (void)hipEventRecord(ev.begin, st);
+    go();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        if (std::getenv("FATTN_DEBUG"))
+            std::fprintf(stderr, "fattn: launch grid (%u,%u,%u) lds %d failed: %s\n", pl.grid.x, pl.grid.y, pl.grid.z,
+                         pl.lds, hipGetErrorString(e));
+        return FATTN_ERR_LAUNCH;
+    }
+    if (ev.end) (void)hipEventRecord(ev.end, st);
+    return FATTN_OK;
+}
+
 template <int KT, int VT, int D, int GRAN, bool HM>
 int launch_split_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     auto kern = fattn_split_kernel<KT, VT, D, GRAN, HM>;
-    static bool attr_set = false;  // idempotent; benign race
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsPerCU);
-        attr_set = true;
-    }
-    if (ev.begin) (void)hipEventRecord(ev.begin, st);
-    hipLaunchKernelGGL(kern, pl.grid, dim3(kSplitWaves * kWave), pl.lds, st, pl.a);
-    if (hipGetLastError() != hipSuccess) return FATTN_ERR_LAUNCH;
-    if (ev.end) (void)hipEventRecord(ev.end, st);
-    return FATTN_OK;
+    return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        hipLaunchKernelGGL(kern, pl.grid, dim3(kSplitWaves * kWave), pl.lds, st, pl.a);
+    });
 }
 
 template <int KT, int VT, int D, int GRAN>
@@ -270,8 +367,28 @@ int launch_gran(const Plan& pl, hipStream_t st, const Events& ev) {
     }
 }
 
+template <int KT, int D, int RPW, bool HM>
+int launch_mq_hm(const Plan& pl, hipStream_t st, const Events& ev) {
+    auto kern = fattn_mq_kernel<KT, D, RPW, HM>;
+    return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        hipLaunchKernelGGL(kern, pl.grid, dim3(kSplitWaves * kWave), pl.lds, st, pl.a);
+    });
+}
+
+template <int KT, int D>
+int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
+    if (pl.rpw == 64)
+        return pl.a.has_mask ? launch_mq_hm<KT, D, 64, true>(pl, st, ev) : launch_mq_hm<KT, D, 64, false>(pl, st, ev);
+    return pl.a.has_mask ? launch_mq_hm<KT, D, 16, true>(pl, st, ev) : launch_mq_hm<KT, D, 16, false>(pl, st, ev);
+}
+
 template <int D>
 int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
+    if (pl.mq) {
+        if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_mq<FATTN_TYPE_Q8_0, D>(pl, st, ev);
+        if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_mq<FATTN_TYPE_Q4_0, D>(pl, st, ev);
+        return FATTN_ERR_UNSUPPORTED_TYPE;
+    }
     if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_gran<FATTN_TYPE_Q8_0, FATTN_TYPE_Q8_0, D>(pl, st, ev);
     if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_gran<FATTN_TYPE_Q4_0, FATTN_TYPE_Q4_0, D>(pl, st, ev);
     if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_gran<FATTN_TYPE_F16, FATTN_TYPE_F16, D>(pl, st, ev);
@@ -299,6 +416,19 @@ int fattn_debug_plan(const fattn_params* p, int* out) {
     return 0;
 }
 #endif
+
+int fattn_set_option(int option, int value) {
+    switch (option) {
+        case FATTN_OPT_MQ_ROWS_PER_WAVE:
+            if (value != 0 && value != 16 && value != 64) return FATTN_ERR_INVALID_ARG;
+            g_opt_mq_rpw = value;
+            return FATTN_OK;
+        case FATTN_OPT_MQ_DISABLE:
+            g_opt_mq_disable = value ? 1 : 0;
+            return FATTN_OK;
+        default: return FATTN_ERR_INVALID_ARG;
+    }
+}
 
 const char* fattn_version(void) { return "fattn-gfx950 0.1"; }
 

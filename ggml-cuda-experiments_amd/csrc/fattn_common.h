@@ -182,8 +182,13 @@ __device__ __forceinline__ float wave_sum(float x) {
 // inline asm, so the compiler does not track them: callers drain with an
 // explicit s_waitcnt vmcnt(0) and pass every loaded value through reg_fence()
 // after that wait, so no use can be scheduled above it.
+// The trailing s_nop covers the VMEM-store-data hazard (a store of more than 8
+// bytes must not have its data VGPRs overwritten by the next VALU instruction):
+// hipcc's hazard recognizer does not see inside inline asm, and with the
+// multi-query kernel's register pressure it reused the data registers of one
+// store as the address of the next at once (elements .x/.y corrupted).
 __device__ __forceinline__ void st_sc1(void* p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 __device__ __forceinline__ void st_sc1_x2(void* p, u32x2 v) {
     asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");

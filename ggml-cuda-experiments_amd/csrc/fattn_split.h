@@ -406,7 +406,7 @@ __device__ unsigned long long* g_stamps;
 
 template <int D>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
-                                             int rv, uint8_t* smem);
+                                             int rv, int row_base, uint8_t* smem);
 
 template <int KT, int VT, int D, int GRAN, bool HM>
 __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4) ? 2 : 4) void fattn_split_kernel(
@@ -816,7 +816,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     __syncthreads();
     FATTN_STAMP(12);
     if (!*last_flag) return;
-    combine_tile<D>(a, tile, qt, hs, ik2, iq3, rv, smem);
+    combine_tile<D>(a, tile, qt, hs, ik2, iq3, rv, 0, smem);
     FATTN_STAMP(13);
 }
 
@@ -828,10 +828,11 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
 // (one memory round trip when ceil(n_chunks / G) <= CB); the (m, l) pairs
 // reduce with VALU segmented reductions (DPP + permlane swaps); the G subsets
 // of a row are summed with all LDS reads in flight at once.  Fixed order:
-// deterministic.
+// deterministic.  Partial row rr is packed row row_base + rr of the tile
+// (row_base != 0: the multi-query kernel's 16-row subtiles).
 template <int D>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
-                                             int rv, uint8_t* smem) {
+                                             int rv, int row_base, uint8_t* smem) {
     constexpr float kNegInf = -__builtin_inff();
     constexpr int EPT = D / 16;
     constexpr int CB = 2;  // chunks per load batch (register budget of the split kernel)
@@ -925,9 +926,10 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
         for (int k = 0; k < kRows; k++) x += (k < G) ? part[k] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         const float Lrow = rowL[rr];
         const float inv = 1.0f / Lrow;
-        const int rq = div_R(a, rr);
+        const int pr = row_base + rr;  // packed row within the tile
+        const int rq = div_R(a, pr);
         const int riq1 = qt * a.QPT + rq;
-        const int riq2 = ik2 * a.rk2 + hs * a.R + (rr - rq * a.R);
+        const int riq2 = ik2 * a.rk2 + hs * a.R + (pr - rq * a.R);
         f32x4 o4;
 #pragma unroll
         for (int j = 0; j < 4; j++) o4[j] = (Lrow == 0.0f) ? __builtin_nanf("") : x[j] * inv;

@@ -33,8 +33,10 @@ ERRORS = {
 # every symbol include/fattn.h declares
 EXPORTS = (
     "fattn_workspace_size", "fattn_workspace_init", "fattn_ext", "fattn_ext_events", "fattn_ext_f16_launch", "fattn_row_workspace_size", "fattn_row",
-    "fattn_dequantize", "fattn_quantize", "fattn_strerror", "fattn_row_size", "fattn_version",
+    "fattn_dequantize", "fattn_quantize", "fattn_strerror", "fattn_row_size", "fattn_version", "fattn_set_option",
 )
+OPT_MQ_ROWS_PER_WAVE = 1
+OPT_MQ_DISABLE = 2
 
 
 class FattnError(RuntimeError):
@@ -63,10 +65,17 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libfattn.so not built at {LIB_PATH}; run `make lib` (or __graft_entry__.build())")
+        # torch's HIP runtime must be the process's one: libfattn.so's
+        # libamdhip64.so.7 dependency then binds to it.  Loaded first, the
+        # library would pull in /opt/rocm's runtime beside torch's and see no
+        # device through it.
+        import torch  # noqa: F401
         L = C.CDLL(LIB_PATH)
         vp, i64, sz = C.c_void_p, C.c_int64, C.c_size_t
         L.fattn_workspace_size.restype = sz
         L.fattn_workspace_size.argtypes = [C.POINTER(FattnParams)]
+        L.fattn_set_option.restype = C.c_int
+        L.fattn_set_option.argtypes = [C.c_int, C.c_int]
         L.fattn_workspace_init.restype = C.c_int
         L.fattn_workspace_init.argtypes = [vp, sz, vp]
         L.fattn_ext.restype = C.c_int
@@ -97,6 +106,12 @@ def lib() -> C.CDLL:
 def _check(rc: int, what: str):
     if rc != FATTN_OK:
         raise FattnError(rc, what)
+
+
+def set_option(option: int, value: int):
+    """Planner override (include/fattn.h fattn_set_option): OPT_MQ_ROWS_PER_WAVE
+    (0 auto, 16, 64) or OPT_MQ_DISABLE (1 = split-KV kernel only)."""
+    _check(lib().fattn_set_option(option, value), "fattn_set_option")
 
 
 def row_size(typ: int, k: int) -> int:

@@ -35,7 +35,8 @@
  *     allocates on the hot path; `stream` is a hipStream_t (NULL = default).
  *   - return value: FATTN_OK (0) or a negative fattn_status; nothing is launched
  *     when an error is returned.  fattn_strerror() names the code.
- *   - stream-ordered and asynchronous; no global mutable state (thread-compatible).
+ *   - stream-ordered and asynchronous; thread-compatible (the only global state is
+ *     fattn_set_option's planner overrides, meant for tests and benchmarks).
  */
 #ifndef FATTN_H
 #define FATTN_H
@@ -111,6 +112,14 @@ int fattn_ext(const fattn_params* p, void* stream);
  * the split-KV combine), so a caller can time the dominant kernel alone with
  * hipEventElapsedTime.  Either event may be NULL. */
 int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* ev_end);
+
+/* Process-wide planner overrides (tests, benchmarks).  Not thread-safe against
+ * concurrent launches.  Returns FATTN_OK or FATTN_ERR_INVALID_ARG. */
+enum {
+    FATTN_OPT_MQ_ROWS_PER_WAVE = 1, /* multi-query kernel rows per wave: 0 = auto, 16, 64 */
+    FATTN_OPT_MQ_DISABLE = 2        /* 1 = never pick the multi-query kernel (split-KV kernel only) */
+};
+int fattn_set_option(int option, int value);
 
 /* flash-llama.h:7-32 argument list (K and V share nb11..nb13, flash-llama.h:123-125;
  * mask rows padded to ne31, nb31 bytes per row). */

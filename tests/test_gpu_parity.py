@@ -89,6 +89,100 @@ def test_config5_batch64_shard(dev):
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
+# ------------------------------------------------------------------ multi-query kernel (fattn_mq.h)
+# Quantised K/V with >= 32 query rows per kv head and the 16-B layout route to
+# the multi-query kernel (64 packed rows per workgroup, tile dequantised once).
+
+def test_config5_full_batch64(dev):
+    """Config 5 on one GPU: 64 query rows x 32 heads, N=4096, Q8_0 (split-KV merge)."""
+    p = make_problem(D=128, NQ=64, H=32, N=4096, kv_type="q8_0", seed=51)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+MQ_CASES = [
+    dict(D=128, kv_type="q8_0", NQ=256, H=4, Hkv=4, N=256, mask="causal"),      # prefill, no split
+    dict(D=64, kv_type="q4_0", NQ=256, H=4, Hkv=4, N=256, mask="causal"),
+    dict(D=128, kv_type="q4_0", NQ=40, H=16, Hkv=4, N=320, mask="random"),      # R=4, ragged query tile
+    dict(D=64, kv_type="q8_0", NQ=9, H=16, Hkv=2, N=96, mask="random"),         # R=8, QPT=8, 2 tiles
+    dict(D=128, kv_type="q8_0", NQ=1, H=64, Hkv=1, N=64, mask="none"),          # R=64, QPT=1
+    dict(D=128, kv_type="q4_0", NQ=33, H=2, Hkv=2, N=2048, mask="neginf_blocks"),
+    dict(D=64, kv_type="q8_0", NQ=70, H=2, Hkv=2, N=32, mask="random", S=2),     # one tile, 2 sequences
+    dict(D=128, kv_type="q8_0", NQ=300, H=2, Hkv=2, N=256, mask="none"),        # no mask: DMA budget w/o mask
+    dict(D=128, kv_type="q4_0", NQ=64, H=8, Hkv=8, N=1024, mask="none"),
+]
+
+
+@pytest.mark.parametrize("case", MQ_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_mq_sweep(dev, case):
+    p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+@pytest.fixture
+def rpw64():
+    """Force 64 rows per wave (256-row workgroups) on small problems."""
+    fattn.set_option(fattn.OPT_MQ_ROWS_PER_WAVE, 64)
+    yield
+    fattn.set_option(fattn.OPT_MQ_ROWS_PER_WAVE, 0)
+
+
+MQ64_CASES = [
+    dict(D=128, kv_type="q8_0", NQ=300, H=2, Hkv=2, N=256, mask="causal"),      # ragged 256-row tile
+    dict(D=128, kv_type="q4_0", NQ=64, H=16, Hkv=2, N=512, mask="random"),      # R=8: 32 queries x 8 heads
+    dict(D=64, kv_type="q8_0", NQ=256, H=2, Hkv=2, N=128, mask="none"),
+    dict(D=64, kv_type="q4_0", NQ=100, H=4, Hkv=4, N=96, mask="neginf_blocks", S=2),
+    dict(D=128, kv_type="q8_0", NQ=300, H=2, Hkv=2, N=256, mask="none"),
+]
+
+
+@pytest.mark.parametrize("case", MQ64_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_mq_rpw64_sweep(dev, rpw64, case):
+    p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("chunk", [64, 1000])
+def test_mq_rpw64_split(dev, rpw64, chunk):
+    """256-row workgroups with split-KV partials (16 subtiles merged per tile)."""
+    p = make_problem(D=128, NQ=260, H=2, N=1024, kv_type="q8_0", seed=23)
+    assert attn_rel_err(run_gpu(p, kv_chunk=chunk), p.oracle()) <= RTOL
+
+
+def test_mq_matches_split_kernel(dev):
+    """The two kernels on one problem (multi-query vs split-KV forced)."""
+    p = make_problem(D=128, NQ=64, H=4, Hkv=2, N=512, kv_type="q4_0", seed=24)
+    a = run_gpu(p)
+    fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
+    try:
+        b = run_gpu(p)
+    finally:
+        fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
+    assert attn_rel_err(a, b) <= RTOL
+    assert attn_rel_err(a, p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("chunk", [32, 96, 512, 100000])
+def test_mq_chunking_invariance(dev, chunk):
+    p = make_problem(D=128, NQ=48, H=8, Hkv=2, N=1024, kv_type="q8_0", seed=17)
+    assert attn_rel_err(run_gpu(p, kv_chunk=chunk), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
+def test_mq_extreme_rescale(dev, kt):
+    p = make_problem(D=128, NQ=64, H=2, N=1024, kv_type=kt, seed=18, extreme=True)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+def test_mq_fully_masked_rows_are_nan(dev):
+    p = make_problem(D=128, NQ=40, H=2, N=256, kv_type="q4_0", mask="zero", seed=19)
+    m = orc.f16_bits_to_f32(p.mask_bits)
+    m[5, :] = -np.inf
+    p.mask_bits = orc.f32_to_f16_bits(m)
+    got, ref = run_gpu(p), p.oracle()
+    assert np.isnan(ref[:, 5]).all() and np.isnan(got[:, 5]).all()
+    assert attn_rel_err(got, ref) <= RTOL
+
+
 # ------------------------------------------------------------------ sweep
 
 CASES = []
