@@ -40,7 +40,7 @@ struct Plan {
     int lds;
     size_t ws_bytes, cnt_bytes, ml_bytes;
     bool mq;  // multi-query kernel (fattn_mq.h)
-    int rpw;  // its packed rows per wave (16 or 64)
+    int nw;   // its waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
 };
 
 // LDS geometry of one instantiation (type-erased for the planner)
@@ -143,17 +143,17 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     return FATTN_OK;
 }
 
-template <int RPW>
+template <int NW, int RPW>
 int mq_lds_bytes_r(int kt, int D) {
     if (kt == FATTN_TYPE_Q8_0)
-        return D == 128 ? MQCfg<FATTN_TYPE_Q8_0, 128, RPW>::ldsBytes : MQCfg<FATTN_TYPE_Q8_0, 64, RPW>::ldsBytes;
-    return D == 128 ? MQCfg<FATTN_TYPE_Q4_0, 128, RPW>::ldsBytes : MQCfg<FATTN_TYPE_Q4_0, 64, RPW>::ldsBytes;
+        return D == 128 ? MQCfg<FATTN_TYPE_Q8_0, 128, NW, RPW>::ldsBytes : MQCfg<FATTN_TYPE_Q8_0, 64, NW, RPW>::ldsBytes;
+    return D == 128 ? MQCfg<FATTN_TYPE_Q4_0, 128, NW, RPW>::ldsBytes : MQCfg<FATTN_TYPE_Q4_0, 64, NW, RPW>::ldsBytes;
 }
-int mq_lds_bytes(int kt, int D, int rpw) { return rpw == 64 ? mq_lds_bytes_r<64>(kt, D) : mq_lds_bytes_r<16>(kt, D); }
+int mq_lds_bytes(int kt, int D, int nw) { return nw == 8 ? mq_lds_bytes_r<8, 32>(kt, D) : mq_lds_bytes_r<4, 16>(kt, D); }
 
-// Multi-query sizing: 4*rpw packed rows per workgroup, KV split only when the
+// Multi-query sizing: 64 or 256 packed rows per workgroup, KV split only when the
 // (kv head x query tile x seq) workgroups cannot fill the chip (two per CU at
-// rpw 16, one at rpw 64).
+// 64 rows, one at 256).
 int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     SplitArgs& a = pl.a;
     const int64_t tiles = N / kStep;  // N % kStep == 0 (16-B path)
@@ -162,7 +162,7 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     if (kv_chunk > 0) {
         nch = (N + kv_chunk - 1) / kv_chunk;
     } else {
-        const int64_t want = pl.rpw == 64 ? kCUs : 2 * kCUs;
+        const int64_t want = pl.nw == 8 ? kCUs : 2 * kCUs;
         nch = (want + base - 1) / base;
         nch = std::min<int64_t>(nch, std::max<int64_t>(1, tiles / 4));  // >= 4 tiles per workgroup
     }
@@ -179,10 +179,10 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     a.nbuf = 0;
     a.wave_bytes = 0;
-    pl.lds = mq_lds_bytes(pl.kt, pl.D, pl.rpw);
+    pl.lds = mq_lds_bytes(pl.kt, pl.D, pl.nw);
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     if (a.n_chunks > 1) {
-        const size_t subs = (size_t)S * Y * kSplitWaves * (pl.rpw / kRows);
+        const size_t subs = (size_t)S * Y * (pl.nw == 8 ? 16 : 4);  // 16-row subtiles per tile
         pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
         pl.ml_bytes = (subs * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + subs * a.n_chunks * kRows * pl.D * 4;
@@ -295,9 +295,9 @@ int make_plan(const fattn_params* p, Plan& pl) {
     if (pl.mq) {
         // 256 rows per workgroup once that still gives one workgroup per CU
         const int64_t wg256 = Hkv * S * ((NQ * a.rk2 + 255) / 256);
-        pl.rpw = g_opt_mq_rpw ? g_opt_mq_rpw : wg256 >= kCUs ? 64 : 16;
+        pl.nw = g_opt_mq_rpw ? (g_opt_mq_rpw == 32 ? 8 : 4) : wg256 >= kCUs ? 8 : 4;
         a.R = a.rk2;
-        a.QPT = kSplitWaves * pl.rpw / a.R;
+        a.QPT = (pl.nw == 8 ? 256 : 64) / a.R;
         a.R_inv = 1.0f / (float)a.R;
         a.n_hsub = 1;
         a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
@@ -367,19 +367,19 @@ int launch_gran(const Plan& pl, hipStream_t st, const Events& ev) {
     }
 }
 
-template <int KT, int D, int RPW, bool HM>
+template <int KT, int D, int NW, bool HM>
 int launch_mq_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    auto kern = fattn_mq_kernel<KT, D, RPW, HM>;
+    auto kern = fattn_mq_kernel<KT, D, NW, HM>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
-        hipLaunchKernelGGL(kern, pl.grid, dim3(kSplitWaves * kWave), pl.lds, st, pl.a);
+        hipLaunchKernelGGL(kern, pl.grid, dim3(NW * kWave), pl.lds, st, pl.a);
     });
 }
 
 template <int KT, int D>
 int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
-    if (pl.rpw == 64)
-        return pl.a.has_mask ? launch_mq_hm<KT, D, 64, true>(pl, st, ev) : launch_mq_hm<KT, D, 64, false>(pl, st, ev);
-    return pl.a.has_mask ? launch_mq_hm<KT, D, 16, true>(pl, st, ev) : launch_mq_hm<KT, D, 16, false>(pl, st, ev);
+    if (pl.nw == 8)
+        return pl.a.has_mask ? launch_mq_hm<KT, D, 8, true>(pl, st, ev) : launch_mq_hm<KT, D, 8, false>(pl, st, ev);
+    return pl.a.has_mask ? launch_mq_hm<KT, D, 4, true>(pl, st, ev) : launch_mq_hm<KT, D, 4, false>(pl, st, ev);
 }
 
 template <int D>
@@ -420,7 +420,7 @@ int fattn_debug_plan(const fattn_params* p, int* out) {
 int fattn_set_option(int option, int value) {
     switch (option) {
         case FATTN_OPT_MQ_ROWS_PER_WAVE:
-            if (value != 0 && value != 16 && value != 64) return FATTN_ERR_INVALID_ARG;
+            if (value != 0 && value != 16 && value != 32) return FATTN_ERR_INVALID_ARG;
             g_opt_mq_rpw = value;
             return FATTN_OK;
         case FATTN_OPT_MQ_DISABLE:

@@ -38,9 +38,10 @@
 
 namespace fattn {
 
-template <int KT, int D, int RPW>
+template <int KT, int D, int NW, int RPW>
 struct MQCfg {
-    static constexpr int rows = kSplitWaves * RPW;                   // packed rows per workgroup
+    static constexpr int NT = NW * kWave;                            // threads per workgroup
+    static constexpr int rows = NW * RPW;                            // packed rows per workgroup
     static constexpr int rowB = row_bytes<KT, D>();
     static constexpr int kvRaw = kStep * rowB;                       // K (or V) raw bytes per tile
     static constexpr int mRaw = rows * kStep * 2;                    // mask rows x 32 f16
@@ -50,10 +51,10 @@ struct MQCfg {
     static constexpr int imgOff = nRaw * rawBytes;
     static constexpr int ldsBytes = imgOff + 2 * 2 * img;            // + (K16, V16) x 2
     static constexpr int PKV = kvRaw / 16;                           // 16-B pieces of K (or V)
-    static constexpr int NIKV = (PKV + kSplitWaves * kWave - 1) / (kSplitWaves * kWave);
+    static constexpr int NIKV = (PKV + NT - 1) / NT;
     static constexpr int PM = mRaw / 16;
-    static constexpr int NIM = PM / (kSplitWaves * kWave);
-    static_assert(PM % (kSplitWaves * kWave) == 0, "");
+    static constexpr int NIM = PM / NT;
+    static_assert(PM % NT == 0, "");
     static_assert(ldsBytes <= 163840, "");
     // DMA instructions wave w issues per tile (mask pieces only with a mask):
     // the last K/V instruction is partial (e.g. 272 pieces of a Q8_0 D=128
@@ -61,7 +62,7 @@ struct MQCfg {
     // vmcnt budget differs
     static constexpr int ni_wave(int w, bool hm) {
         int n = hm ? NIM : 0;
-        for (int i = 0; i < NIKV; i++) n += (i * kSplitWaves * kWave + w * kWave < PKV) ? 2 : 0;
+        for (int i = 0; i < NIKV; i++) n += (i * NT + w * kWave < PKV) ? 2 : 0;
         return n;
     }
 };
@@ -69,14 +70,14 @@ struct MQCfg {
 // Copy tile [n0, n0 + 32) (raw K rows | raw V rows | mask rows) into `buf`;
 // all 256 threads, 16-B pieces, lane-linear.  Rows past N / query rows past
 // the tile's fall outside the descriptors: zeros, no traffic.
-template <int KT, int D, int RPW, bool HM>
+template <int KT, int D, int NW, int RPW, bool HM>
 __device__ __forceinline__ void mq_issue(const SplitArgs& a, const StepSrc& rs, int n0, int mrow0, uint8_t* buf,
                                          int wave, int lane) {
 #ifdef FATTN_MQ_NOMEM
     return;  // diagnostic build only: no HBM traffic (compute on whatever LDS holds)
 #endif
-    using C = MQCfg<KT, D, RPW>;
-    constexpr int NT = kSplitWaves * kWave;
+    using C = MQCfg<KT, D, NW, RPW>;
+    constexpr int NT = C::NT;
     const int tid = wave * kWave + lane;
     // LDS base of this wave's 1-KiB slot in each 4-KiB instruction group (M0: scalar)
     const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(buf) + wave * kWave * 16);
@@ -105,95 +106,104 @@ __device__ __forceinline__ void mq_issue(const SplitArgs& a, const StepSrc& rs, 
 
 // wait until this wave's pieces of all but the `pending` youngest in-flight
 // tiles have landed (pending = 0, 1, 2)
-template <int KT, int D, int RPW, bool HM>
-__device__ __forceinline__ void mq_wait_tiles(int wave, int pending) {
-    using C = MQCfg<KT, D, RPW>;
+template <int NI>
+__device__ __forceinline__ void wait_tiles_n(int pending) {
     if (pending <= 0) {
         wait_vmcnt_c<0>();
     } else if (pending == 1) {
-        switch (wave) {
-            case 0: wait_vmcnt_c<C::ni_wave(0, HM)>(); break;
-            case 1: wait_vmcnt_c<C::ni_wave(1, HM)>(); break;
-            case 2: wait_vmcnt_c<C::ni_wave(2, HM)>(); break;
-            default: wait_vmcnt_c<C::ni_wave(3, HM)>(); break;
-        }
+        wait_vmcnt_c<NI>();
     } else {
-        switch (wave) {
-            case 0: wait_vmcnt_c<2 * C::ni_wave(0, HM)>(); break;
-            case 1: wait_vmcnt_c<2 * C::ni_wave(1, HM)>(); break;
-            case 2: wait_vmcnt_c<2 * C::ni_wave(2, HM)>(); break;
-            default: wait_vmcnt_c<2 * C::ni_wave(3, HM)>(); break;
-        }
+        wait_vmcnt_c<2 * NI>();
+    }
+}
+template <int KT, int D, int NW, int RPW, bool HM>
+__device__ __forceinline__ void mq_wait_tiles(int wave, int pending) {
+    using C = MQCfg<KT, D, NW, RPW>;
+    switch (wave) {
+        case 0: wait_tiles_n<C::ni_wave(0, HM)>(pending); break;
+        case 1: wait_tiles_n<C::ni_wave(1, HM)>(pending); break;
+        case 2: wait_tiles_n<C::ni_wave(2, HM)>(pending); break;
+        case 3: wait_tiles_n<C::ni_wave(3, HM)>(pending); break;
+        case 4: wait_tiles_n<C::ni_wave(4, HM)>(pending); break;
+        case 5: wait_tiles_n<C::ni_wave(5, HM)>(pending); break;
+        case 6: wait_tiles_n<C::ni_wave(6, HM)>(pending); break;
+        default: wait_tiles_n<C::ni_wave(7, HM)>(pending); break;
     }
 }
 
-// Dequantise one ggml block (32 elements) of raw row `row`, block b, into the
-// four 16-B f16 chunks 4b..4b+3: h(q * d), one f16 rounding (src/utils.h:10-11
-// dequantise-then-round).  One thread per block: the block's dwords are read
-// once (the qs bytes are only 2-byte aligned: v_alignbyte with a runtime shift).
+// Dequantise half h (elements 16h..16h+15) of ggml block b of raw row `row`
+// into the two 16-B f16 chunks 4b+2h, 4b+2h+1: h(q * d), one f16 rounding
+// (src/utils.h:10-11 dequantise-then-round).  The qs bytes are only 2-byte
+// aligned: dword reads + v_alignbyte with a runtime shift.
 template <int KT, int D>
-__device__ __forceinline__ void dequant_block(const uint8_t* raw, int row, int b, u32x4 (&out)[4]) {
+__device__ __forceinline__ void dequant_half(const uint8_t* raw, int row, int b, int h, u32x4 (&out)[2]) {
     constexpr int RB = row_bytes<KT, D>();
     constexpr int BB = TypeInfo<KT>::block_bytes;
-    constexpr int NQW = KT == FATTN_TYPE_Q8_0 ? 8 : 4;  // qs dwords
     const uint32_t blk = row * RB + BB * b;
-    const uint32_t qb = (blk + 2) & ~3u, sh = (blk + 2) & 3u;
-    uint32_t u[NQW + 1];
+    // Q8_0: qs bytes 16h..16h+15; Q4_0: all 16 qs bytes (low / high nibbles)
+    const uint32_t q0 = blk + 2 + (KT == FATTN_TYPE_Q8_0 ? 16 * h : 0);
+    const uint32_t qb = q0 & ~3u, sh = q0 & 3u;
+    uint32_t u[5];
 #pragma unroll
-    for (int j = 0; j <= NQW; j++) u[j] = *(const uint32_t*)(raw + qb + 4 * j);
-    uint32_t q[NQW];
+    for (int j = 0; j < 5; j++) u[j] = *(const uint32_t*)(raw + qb + 4 * j);
+    uint32_t q[4];
 #pragma unroll
-    for (int j = 0; j < NQW; j++) q[j] = alignbyte(u[j + 1], u[j], sh);
+    for (int j = 0; j < 4; j++) q[j] = alignbyte(u[j + 1], u[j], sh);
     const uint32_t dw = *(const uint32_t*)(raw + (blk & ~3u));
     const f16x2 d = bcast_h((blk & 2) ? (dw >> 16) : dw);
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < 2; k++) {
         f16x2 h0, h1, h2, h3;
         if constexpr (KT == FATTN_TYPE_Q8_0) {
             i8x4_to_h2x2(q[2 * k], h0, h1);
             i8x4_to_h2x2(q[2 * k + 1], h2, h3);
         } else {  // elements 0-15: low nibbles of bytes 0-15; 16-31: high nibbles
-            const uint32_t sft = (k >> 1) * 4;
-            const int w = (k & 1) * 2;
-            u4x4_to_h2x2((q[w] >> sft) & 0x0F0F0F0Fu, h0, h1);
-            u4x4_to_h2x2((q[w + 1] >> sft) & 0x0F0F0F0Fu, h2, h3);
+            const uint32_t sft = 4 * h;
+            u4x4_to_h2x2((q[2 * k] >> sft) & 0x0F0F0F0Fu, h0, h1);
+            u4x4_to_h2x2((q[2 * k + 1] >> sft) & 0x0F0F0F0Fu, h2, h3);
         }
         h0 *= d; h1 *= d; h2 *= d; h3 *= d;
         out[k] = u32x4{as_u32(h0), as_u32(h1), as_u32(h2), as_u32(h3)};
     }
 }
 
-// Tile `rb` (raw) -> f16 images k16 / v16 (decode kernel's swizzles); one
-// block per thread: threads [0, 32*NB) take K, [32*NB, 64*NB) take V.
-template <int KT, int D>
+// Tile `rb` (raw) -> f16 images k16 / v16 (decode kernel's swizzles).  Units
+// of half a ggml block: [0, 64*NB) are K's, [64*NB, 128*NB) V's, dealt
+// round-robin over the NT threads.
+template <int KT, int D, int NT>
 __device__ __forceinline__ void mq_dequant(const uint8_t* rb, int kv_raw, uint8_t* k16, uint8_t* v16, int tid) {
 #ifdef FATTN_MQ_NODEQ
     return;  // diagnostic build only
 #endif
     constexpr int NB = D / QK;
     constexpr int CPR = D * 2 / 16;
-    constexpr int NBLK = kStep * NB;
-    static_assert(2 * NBLK <= kSplitWaves * kWave, "");
-    if (2 * NBLK < kSplitWaves * kWave && tid >= 2 * NBLK) return;
-    const bool is_v = tid >= NBLK;
-    const int t = is_v ? tid - NBLK : tid;
-    const int row = t / NB, b = t % NB;
-    u32x4 ch[4];
-    dequant_block<KT, D>(rb + (is_v ? kv_raw : 0), row, b, ch);
-    uint8_t* dst = (is_v ? v16 : k16) + row * (D * 2);
-    const int sw = is_v ? (((row & 7) << 1) & (CPR - 1)) : (row & (CPR - 1));
+    constexpr int NU = 2 * kStep * NB;  // half blocks per image
 #pragma unroll
-    for (int k = 0; k < 4; k++) *(u32x4*)(dst + (((4 * b + k) ^ sw) * 16)) = ch[k];
+    for (int i = 0; i < (2 * NU + NT - 1) / NT; i++) {
+        const int unit = i * NT + tid;
+        if ((2 * NU) % NT != 0 && unit >= 2 * NU) break;
+        const bool is_v = unit >= NU;
+        const int t = is_v ? unit - NU : unit;
+        const int row = t / (2 * NB), b = (t / 2) % NB, h = t & 1;
+        u32x4 ch[2];
+        dequant_half<KT, D>(rb + (is_v ? kv_raw : 0), row, b, h, ch);
+        uint8_t* dst = (is_v ? v16 : k16) + row * (D * 2);
+        const int sw = is_v ? (((row & 7) << 1) & (CPR - 1)) : (row & (CPR - 1));
+#pragma unroll
+        for (int k = 0; k < 2; k++) *(u32x4*)(dst + (((4 * b + 2 * h + k) ^ sw) * 16)) = ch[k];
+    }
 }
 
-template <int KT, int D, int RPW, bool HM>
-__global__ __launch_bounds__(kSplitWaves * kWave, RPW >= 64 ? 1 : 2) void fattn_mq_kernel(const SplitArgs a) {
-    using C = MQCfg<KT, D, RPW>;
+template <int KT, int D, int NW, bool HM>
+__global__ __launch_bounds__(NW * kWave, NW == 8 ? 1 : 2) void fattn_mq_kernel(const SplitArgs a) {
+    constexpr int RPW = NW == 8 ? 32 : 16;  // packed rows per wave
+    using C = MQCfg<KT, D, NW, RPW>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NB = D / QK;
     constexpr int NC = D / 16;
     constexpr int NG = RPW / kRows;  // 16-column MFMA groups per wave
     constexpr float kNegInf = -__builtin_inff();
+    constexpr float kDeferLog2 = 8.0f;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -262,7 +272,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, RPW >= 64 ? 1 : 2) void fattn_
     // three tiles in flight behind Q (loads retire in order: the first tile
     // wait covers Q too)
     for (int s = 0; s < 3 && s < ntiles; s++)
-        mq_issue<KT, D, RPW, HM>(a, rs, c_lo + s * kStep, mrow0, raw(s), wave, lane);
+        mq_issue<KT, D, NW, RPW, HM>(a, rs, c_lo + s * kStep, mrow0, raw(s), wave, lane);
 
     // this lane's mask values of a tile: rows mq[gi], positions 16t + 4g + r
     auto mask_regs = [&](const uint8_t* rb, u32x2 (&mk)[NG][2]) {
@@ -280,9 +290,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave, RPW >= 64 ? 1 : 2) void fattn_
 #pragma unroll
     for (int gi = 0; gi < NG; gi++) mk_cur[gi][0] = mk_cur[gi][1] = u32x2{0, 0};
     if (ntiles > 0) {
-        mq_wait_tiles<KT, D, RPW, HM>(wave, min(2, ntiles - 1));
+        mq_wait_tiles<KT, D, NW, RPW, HM>(wave, min(2, ntiles - 1));
         __syncthreads();
-        mq_dequant<KT, D>(raw(0), C::kvRaw, k16_of(0), k16_of(0) + C::img, tid);
+        mq_dequant<KT, D, C::NT>(raw(0), C::kvRaw, k16_of(0), k16_of(0) + C::img, tid);
         mask_regs(raw(0), mk_cur);
     }
 
@@ -302,14 +312,14 @@ __global__ __launch_bounds__(kSplitWaves * kWave, RPW >= 64 ? 1 : 2) void fattn_
     // consumed in iteration s - 1) takes tile s + 3; the workgroup then
     // dequantises tile s + 1 into the other image while each wave runs tile s.
     for (int s = 0; s < ntiles; s++) {
-        if (s + 1 < ntiles) mq_wait_tiles<KT, D, RPW, HM>(wave, min(1, ntiles - 2 - s));
+        if (s + 1 < ntiles) mq_wait_tiles<KT, D, NW, RPW, HM>(wave, min(1, ntiles - 2 - s));
         __syncthreads();
-        if (s + 3 < ntiles) mq_issue<KT, D, RPW, HM>(a, rs, c_lo + (s + 3) * kStep, mrow0, raw(s + 3), wave, lane);
+        if (s + 3 < ntiles) mq_issue<KT, D, NW, RPW, HM>(a, rs, c_lo + (s + 3) * kStep, mrow0, raw(s + 3), wave, lane);
         u32x2 mk_next[NG][2];
 #pragma unroll
         for (int gi = 0; gi < NG; gi++) mk_next[gi][0] = mk_next[gi][1] = u32x2{0, 0};
         if (s + 1 < ntiles) {
-            mq_dequant<KT, D>(raw(s + 1), C::kvRaw, k16_of(s + 1), k16_of(s + 1) + C::img, tid);
+            mq_dequant<KT, D, C::NT>(raw(s + 1), C::kvRaw, k16_of(s + 1), k16_of(s + 1) + C::img, tid);
             mask_regs(raw(s + 1), mk_next);
         }
 #ifdef FATTN_MQ_NOCOMPUTE
@@ -345,15 +355,20 @@ __global__ __launch_bounds__(kSplitWaves * kWave, RPW >= 64 ? 1 : 2) void fattn_
             float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
                                fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
             tmax = grp4_max(tmax);
-            const float m_new = fmaxf(m_run[gi], tmax);
-            const float m_use = (m_new == kNegInf) ? 0.0f : m_new;
-            if (s > 0 && __builtin_amdgcn_ballot_w64(m_new != m_run[gi])) {
-                const float alpha = __builtin_amdgcn_exp2f(m_run[gi] - m_use);
+            // deferred max (cdna_hip_programming.md T13): the reference max moves
+            // only when a column's tile max passes it by more than kDeferLog2, so
+            // the O-wide rescale is rare; meanwhile P <= 2^kDeferLog2 (exact in
+            // f16's range, same relative precision).  The decision precedes this
+            // tile's exponentials, and O, l are scaled together.
+            if (__builtin_amdgcn_ballot_w64(tmax > m_run[gi] + kDeferLog2)) {
+                const float m_new = fmaxf(m_run[gi], tmax);
+                const float alpha = (m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[gi] - m_new);
                 l_run[gi] *= alpha;
 #pragma unroll
                 for (int c = 0; c < NC; c++) o[gi][c] *= alpha;
+                m_run[gi] = m_new;
             }
-            m_run[gi] = m_new;
+            const float m_use = (m_run[gi] == kNegInf) ? 0.0f : m_run[gi];
             float pv[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) pv[j] = __builtin_amdgcn_exp2f(sv[j] - m_use);
@@ -399,7 +414,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, RPW >= 64 ? 1 : 2) void fattn_
     // ---- several chunks: publish each column group's 16 rows as subtile
     // (tile, 4*NG) in the decode kernel's partial layout; the last workgroup
     // of the tile merges the subtiles (same hand-off as fattn_split_kernel)
-    constexpr int SUBS = kSplitWaves * NG;
+    constexpr int SUBS = NW * NG;
     const int64_t tile = (int64_t)iq3 * gridDim.y + y;
     {
         auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };

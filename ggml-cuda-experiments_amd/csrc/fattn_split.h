@@ -829,7 +829,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
 // reduce with VALU segmented reductions (DPP + permlane swaps); the G subsets
 // of a row are summed with all LDS reads in flight at once.  Fixed order:
 // deterministic.  Partial row rr is packed row row_base + rr of the tile
-// (row_base != 0: the multi-query kernel's 16-row subtiles).
+// (row_base != 0: the multi-query kernel's 16-row subtiles).  Written for
+// 256 threads; in a 512-thread workgroup the upper half only joins the
+// barriers (its groups, rows and chunks are all out of range).
 template <int D>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
                                              int rv, int row_base, uint8_t* smem) {
@@ -916,7 +918,8 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
 
     // sum the G subsets of each row, normalise, store: thread -> (row, 4 dims),
     // all of its 16-B LDS reads issued before any is consumed
-    for (int t = threadIdx.x; t < rv * (D / 4); t += kSplitWaves * kWave) {
+    // (a 512-thread workgroup's upper half takes no part)
+    for (int t = threadIdx.x; t < rv * (D / 4) && threadIdx.x < kSplitWaves * kWave; t += kSplitWaves * kWave) {
         const int rr = t / (D / 4), dq = (t % (D / 4)) * 4;
         f32x4 part[kRows];
 #pragma unroll

@@ -110,7 +110,7 @@ def _check(rc: int, what: str):
 
 def set_option(option: int, value: int):
     """Planner override (include/fattn.h fattn_set_option): OPT_MQ_ROWS_PER_WAVE
-    (0 auto, 16, 64) or OPT_MQ_DISABLE (1 = split-KV kernel only)."""
+    (0 auto, 16, 32) or OPT_MQ_DISABLE (1 = split-KV kernel only)."""
     _check(lib().fattn_set_option(option, value), "fattn_set_option")
 
 

@@ -116,7 +116,7 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
 /* Process-wide planner overrides (tests, benchmarks).  Not thread-safe against
  * concurrent launches.  Returns FATTN_OK or FATTN_ERR_INVALID_ARG. */
 enum {
-    FATTN_OPT_MQ_ROWS_PER_WAVE = 1, /* multi-query kernel rows per wave: 0 = auto, 16, 64 */
+    FATTN_OPT_MQ_ROWS_PER_WAVE = 1, /* multi-query kernel: 0 = auto, 16 (4 waves x 16 rows), 32 (8 waves x 32 rows) */
     FATTN_OPT_MQ_DISABLE = 2        /* 1 = never pick the multi-query kernel (split-KV kernel only) */
 };
 int fattn_set_option(int option, int value);

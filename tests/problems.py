@@ -98,7 +98,8 @@ class Problem:
 
 
 def make_problem(D=128, NQ=1, H=32, Hkv=None, N=4096, kv_type="q8_0", S=1, Skv=None, layout="head",
-                 mask="random", seed=0, scale=None, v_trans=False, mask_pad=64, extreme=False) -> Problem:
+                 mask="random", seed=0, scale=None, v_trans=False, mask_pad=64, extreme=False,
+                 ramp=0.0) -> Problem:
     """Random problem.  mask: "none" | "random" (U[-1,1], like kernel_test.h:48) |
     "zero" | "causal" (query i sees positions <= N - NQ + i) | "neginf_blocks"
     (some 32-position blocks fully -inf for every row)."""
@@ -114,6 +115,11 @@ def make_problem(D=128, NQ=1, H=32, Hkv=None, N=4096, kv_type="q8_0", S=1, Skv=N
         # large-magnitude scores force many online-softmax rescales
         q *= 8.0
         k[..., ::7, :] *= 4.0
+    if ramp:
+        # key magnitude growing along the sequence: the running max keeps
+        # rising in small steps (the deferred-rescale path) with jumps between
+        q *= 4.0
+        k *= (1.0 + ramp * np.arange(N, dtype=np.float32) / max(N, 1))[:, None]
     scale = 1.0 / np.sqrt(np.float32(D)) if scale is None else scale
     rb = row_bytes(typ, D)
     k_rows = encode_rows(k, typ)   # [Skv][Hkv][N][rb]

@@ -120,8 +120,8 @@ def test_mq_sweep(dev, case):
 
 @pytest.fixture
 def rpw64():
-    """Force 64 rows per wave (256-row workgroups) on small problems."""
-    fattn.set_option(fattn.OPT_MQ_ROWS_PER_WAVE, 64)
+    """Force the 256-row workgroups (8 waves x 32 rows) on small problems."""
+    fattn.set_option(fattn.OPT_MQ_ROWS_PER_WAVE, 32)
     yield
     fattn.set_option(fattn.OPT_MQ_ROWS_PER_WAVE, 0)
 
@@ -171,6 +171,19 @@ def test_mq_chunking_invariance(dev, chunk):
 def test_mq_extreme_rescale(dev, kt):
     p = make_problem(D=128, NQ=64, H=2, N=1024, kv_type=kt, seed=18, extreme=True)
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("rpw", [0, 32])
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
+def test_mq_rescale_ramp(dev, kt, rpw):
+    """Scores rising along the sequence: many deferred-max steps and rescales."""
+    fattn.set_option(fattn.OPT_MQ_ROWS_PER_WAVE, rpw)
+    try:
+        p = make_problem(D=128, NQ=64, H=4, N=2048, kv_type=kt, seed=25, ramp=12.0, mask="none")
+        got = run_gpu(p)
+    finally:
+        fattn.set_option(fattn.OPT_MQ_ROWS_PER_WAVE, 0)
+    assert attn_rel_err(got, p.oracle()) <= RTOL
 
 
 def test_mq_fully_masked_rows_are_nan(dev):
