@@ -29,6 +29,16 @@ stamps: $(LIBDIR)/libfattn_stamps.so $(LIBDIR)/libfattn_nocompute.so $(LIBDIR)/l
         $(LIBDIR)/libfattn_noatomic.so $(LIBDIR)/libfattn_nomem.so $(LIBDIR)/libfattn_nomem_notail.so \
         $(LIBDIR)/libfattn_nomem_nopub.so $(LIBDIR)/libfattn_stamps_nomem.so
 
+$(LIBDIR)/libfattn_nt.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DMA_NT -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_nt_stamps.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DMA_NT -DFATTN_STAMPS -shared $(CSRC) -o $@
+
+ntdiag: $(LIBDIR)/libfattn_nt.so $(LIBDIR)/libfattn_nt_stamps.so
+
 mqdiag: $(LIBDIR)/libfattn_mq_nomem.so $(LIBDIR)/libfattn_mq_nodeq.so $(LIBDIR)/libfattn_mq_nocomp.so
 
 $(LIBDIR)/libfattn_mq_nomem.so: $(CSRC) $(CHDR)

@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--head-dim", type=int, default=128)
     ap.add_argument("--layout", default="head", choices=["head", "pos"])
     ap.add_argument("--kv-chunk", type=int, default=0)
+    ap.add_argument("--spw", type=int, default=0, help="split kernel: steps per wave (0 = planner)")
+    ap.add_argument("--inflight", type=int, default=0, help="split kernel: steps in flight per wave (0 = planner)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,6 +117,10 @@ def main():
     import torch.distributed as dist
     import fattn
 
+    if args.spw:
+        fattn.set_option(fattn.OPT_SPLIT_STEPS, args.spw)
+    if args.inflight:
+        fattn.set_option(fattn.OPT_SPLIT_INFLIGHT, args.inflight)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -27,6 +27,8 @@ constexpr int kCUs = 256;
 // fattn_set_option overrides
 int g_opt_mq_rpw = 0;
 int g_opt_mq_disable = 0;
+int g_opt_split_spw = 0;
+int g_opt_split_nbuf = 0;
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -122,6 +124,16 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
         }
     }
     nbuf = std::min(spw, (pl.kt == FATTN_TYPE_F16) ? 1 : 2);
+    if (kv_chunk <= 0 && g_opt_split_spw > 0) {
+        spw = (int)std::min<int64_t>(g_opt_split_spw, (steps + kSplitWaves - 1) / kSplitWaves);
+        nbuf = std::min(spw, 2);
+        const int64_t nch = (N + (int64_t)spw * quantum - 1) / ((int64_t)spw * quantum);
+        if (nch > 1 && !combine_ok(nch, rv_max, pl.D)) return FATTN_ERR_INVALID_ARG;
+    }
+    if (g_opt_split_nbuf > 0) {
+        nbuf = std::min(spw, g_opt_split_nbuf);
+        while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
+    }
     a.nbuf = nbuf;
     a.wave_bytes = G.wave_bytes(nbuf);
     a.chunk_len = spw * quantum;
@@ -425,6 +437,14 @@ int fattn_set_option(int option, int value) {
             return FATTN_OK;
         case FATTN_OPT_MQ_DISABLE:
             g_opt_mq_disable = value ? 1 : 0;
+            return FATTN_OK;
+        case FATTN_OPT_SPLIT_STEPS:
+            if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_spw = value;
+            return FATTN_OK;
+        case FATTN_OPT_SPLIT_INFLIGHT:
+            if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_nbuf = value;
             return FATTN_OK;
         default: return FATTN_ERR_INVALID_ARG;
     }

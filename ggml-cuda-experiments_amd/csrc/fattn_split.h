@@ -157,12 +157,17 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(
 // (saved and restored: M0 is compiler-reserved; s_nop 0 = M0 -> LDS-DMA
 // hazard).  Not tracked by the compiler's s_waitcnt bookkeeping: every
 // consumer waits with an explicit vmcnt.
+#ifdef FATTN_DMA_NT
+#define FATTN_DMA_MOD " nt"
+#else
+#define FATTN_DMA_MOD ""
+#endif
 template <int BYTES>
 __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds, uint32_t off) {
     uint32_t keep;
     if constexpr (BYTES == 16) {
         asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" FATTN_DMA_MOD " lds\n\t"
             "s_mov_b32 m0, %0"
             : "=&s"(keep)
             : "v"(off), "s"(srd), "s"(lds)
@@ -170,7 +175,7 @@ __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds, uint32_t off
     } else {
         static_assert(BYTES == 4, "");
         asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen" FATTN_DMA_MOD " lds\n\t"
             "s_mov_b32 m0, %0"
             : "=&s"(keep)
             : "v"(off), "s"(srd), "s"(lds)
@@ -706,7 +711,11 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     constexpr int MS = C::kMergeStride;
     float* mo = (float*)wbuf;                      // [16][MS]
     float* mml = (float*)(wbuf + kRows * MS * 4);  // [16][2]
-    if constexpr (kVQ8) {
+    // valid rows of this tile form a prefix [0, rv); only those are merged
+    const int rv = tile_rows(a, qt, hs);
+    if (m >= rv) {
+        // nothing of this column is needed
+    } else if constexpr (kVQ8) {
         // tile E_b holds columns 32b + 2(4g+reg), O_b the odd neighbours
 #pragma unroll
         for (int b = 0; b < NB; b++) {
@@ -718,7 +727,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
 #pragma unroll
         for (int c = 0; c < NC; c++) *(f32x4*)(mo + m * MS + 16 * c + 4 * g) = o[c];
     }
-    if (g == 0) {
+    if (g == 0 && m < rv) {
         mml[2 * m] = m_run;
         mml[2 * m + 1] = l_tot;
     }
@@ -734,25 +743,24 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
 #pragma unroll
     for (int w = 0; w < kSplitWaves; w++) {
         const float* ml = (const float*)(smem + w * a.wave_bytes + kRows * MS * 4);
-        mw[w] = ml[2 * tm];
-        lw[w] = ml[2 * tm + 1];
+        mw[w] = tm < rv ? ml[2 * tm] : kNegInf;
+        lw[w] = tm < rv ? ml[2 * tm + 1] : 0.0f;
         M = fmaxf(M, mw[w]);
     }
     float L = 0.0f;
     float acc[EPT];
 #pragma unroll
     for (int e = 0; e < EPT; e++) acc[e] = 0.0f;
+    if (tm < rv) {
 #pragma unroll
-    for (int w = 0; w < kSplitWaves; w++) {
-        const float wt = (mw[w] == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mw[w] - M);
-        L += wt * lw[w];
-        const float* ow = (const float*)(smem + w * a.wave_bytes) + tm * MS + d0;
+        for (int w = 0; w < kSplitWaves; w++) {
+            const float wt = (mw[w] == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mw[w] - M);
+            L += wt * lw[w];
+            const float* ow = (const float*)(smem + w * a.wave_bytes) + tm * MS + d0;
 #pragma unroll
-        for (int e = 0; e < EPT; e++) acc[e] += wt * ow[e];
+            for (int e = 0; e < EPT; e++) acc[e] += wt * ow[e];
+        }
     }
-
-    // valid rows of this tile form a prefix [0, rv)
-    const int rv = tile_rows(a, qt, hs);
     auto dst_row = [&](int r) -> float* {
         const int rq = div_R(a, r);
         const int riq1 = qt * a.QPT + rq;

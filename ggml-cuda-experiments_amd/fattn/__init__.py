@@ -37,6 +37,8 @@ EXPORTS = (
 )
 OPT_MQ_ROWS_PER_WAVE = 1
 OPT_MQ_DISABLE = 2
+OPT_SPLIT_STEPS = 3
+OPT_SPLIT_INFLIGHT = 4
 
 
 class FattnError(RuntimeError):
@@ -110,7 +112,8 @@ def _check(rc: int, what: str):
 
 def set_option(option: int, value: int):
     """Planner override (include/fattn.h fattn_set_option): OPT_MQ_ROWS_PER_WAVE
-    (0 auto, 16, 32) or OPT_MQ_DISABLE (1 = split-KV kernel only)."""
+    (0 auto, 16, 32), OPT_MQ_DISABLE (1 = split-KV kernel only), OPT_SPLIT_STEPS
+    (32-position steps per wave, 0 auto) or OPT_SPLIT_INFLIGHT (steps in flight, 0 auto)."""
     _check(lib().fattn_set_option(option, value), "fattn_set_option")
 
 

@@ -117,7 +117,9 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
  * concurrent launches.  Returns FATTN_OK or FATTN_ERR_INVALID_ARG. */
 enum {
     FATTN_OPT_MQ_ROWS_PER_WAVE = 1, /* multi-query kernel: 0 = auto, 16 (4 waves x 16 rows), 32 (8 waves x 32 rows) */
-    FATTN_OPT_MQ_DISABLE = 2        /* 1 = never pick the multi-query kernel (split-KV kernel only) */
+    FATTN_OPT_MQ_DISABLE = 2,       /* 1 = never pick the multi-query kernel (split-KV kernel only) */
+    FATTN_OPT_SPLIT_STEPS = 3,      /* split kernel: 32-position steps per wave (0 = auto, 1..64) */
+    FATTN_OPT_SPLIT_INFLIGHT = 4    /* split kernel: steps in flight per wave (0 = auto, 1..4; LDS permitting) */
 };
 int fattn_set_option(int option, int value);
 

@@ -11,7 +11,7 @@ import ctypes as C
 import os
 import sys
 
-os.environ["FATTN_LIB"] = ("libfattn_nocompute.so" if "--nocompute" in sys.argv else
+os.environ["FATTN_LIB"] = os.environ.get("FATTN_STAMPS_LIB") or ("libfattn_nocompute.so" if "--nocompute" in sys.argv else
                            "libfattn_stamps_nomem.so" if "--nomem" in sys.argv else "libfattn_stamps.so")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "ggml-cuda-experiments_amd"), ROOT]
@@ -49,10 +49,16 @@ def main():
     ap.add_argument("--kv-heads", type=int, default=0)
     ap.add_argument("--kv-len", type=int, default=4096)
     ap.add_argument("--n-q", type=int, default=1)
+    ap.add_argument("--spw", type=int, default=0)
+    ap.add_argument("--inflight", type=int, default=0)
     ap.add_argument("--nocompute", action="store_true", help="memory-only diagnostic build")
     ap.add_argument("--nomem", action="store_true", help="compute-only diagnostic build")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    if args.spw:
+        fattn.set_option(fattn.OPT_SPLIT_STEPS, args.spw)
+    if args.inflight:
+        fattn.set_option(fattn.OPT_SPLIT_INFLIGHT, args.inflight)
     D, H, N, NQ = 128, args.heads, args.kv_len, args.n_q
     Hkv = args.kv_heads or H
     typ = fattn.TYPE_NAMES[args.kv_type]
