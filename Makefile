@@ -39,7 +39,12 @@ $(LIBDIR)/libfattn_nt_stamps.so: $(CSRC) $(CHDR)
 
 ntdiag: $(LIBDIR)/libfattn_nt.so $(LIBDIR)/libfattn_nt_stamps.so
 
-mqdiag: $(LIBDIR)/libfattn_mq_nomem.so $(LIBDIR)/libfattn_mq_nodeq.so $(LIBDIR)/libfattn_mq_nocomp.so
+mqdiag: $(LIBDIR)/libfattn_mq_nomem.so $(LIBDIR)/libfattn_mq_nodeq.so $(LIBDIR)/libfattn_mq_nocomp.so \
+        $(LIBDIR)/libfattn_pf_nosm.so
+
+$(LIBDIR)/libfattn_pf_nosm.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_PF_NOSOFTMAX -shared $(CSRC) -o $@
 
 $(LIBDIR)/libfattn_mq_nomem.so: $(CSRC) $(CHDR)
 	@mkdir -p $(LIBDIR)

@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--kv-chunk", type=int, default=0)
     ap.add_argument("--spw", type=int, default=0, help="split kernel: steps per wave (0 = planner)")
     ap.add_argument("--inflight", type=int, default=0, help="split kernel: steps in flight per wave (0 = planner)")
+    ap.add_argument("--no-mask", action="store_true", help="no mask tensor (diagnostics; the metric uses a mask)")
+    ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -121,6 +123,8 @@ def main():
         fattn.set_option(fattn.OPT_SPLIT_STEPS, args.spw)
     if args.inflight:
         fattn.set_option(fattn.OPT_SPLIT_INFLIGHT, args.inflight)
+    if args.pf:
+        fattn.set_option(fattn.OPT_PF, args.pf)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -156,7 +160,8 @@ def main():
 
     att = fattn.Attention(fattn.q_view(q), fattn.kv_view(kv_sets[0][0], typ, D, N, Hkv, layout=args.layout),
                           fattn.kv_view(kv_sets[0][1], typ, D, N, Hkv, layout=args.layout),
-                          fattn.mask_view(mask), outs[0], 1.0 / D ** 0.5, kv_chunk=args.kv_chunk)
+                          None if args.no_mask else fattn.mask_view(mask), outs[0], 1.0 / D ** 0.5,
+                          kv_chunk=args.kv_chunk)
 
     def step(i, stream=None, ev=None):
         kvs = kv_sets[i % R]
@@ -232,7 +237,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_avg = float(t[0]), float(t[1])
 
-    bytes_step = (NQ * H * D * 4) * 2 + 2 * Hkv * N * rb + NQ * N * 2
+    bytes_step = (NQ * H * D * 4) * 2 + 2 * Hkv * N * rb + (0 if args.no_mask else NQ * N * 2)
     flops_step = 4 * NQ * N * D * H
     total_bytes = bytes_step * args.steps * world
     value = total_bytes / elapsed / 1e9

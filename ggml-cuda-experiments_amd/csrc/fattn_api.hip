@@ -16,6 +16,7 @@
 
 #include "fattn_quant.h"
 #include "fattn_mq.h"
+#include "fattn_pf.h"
 #include "fattn_split.h"
 
 using namespace fattn;
@@ -29,6 +30,7 @@ int g_opt_mq_rpw = 0;
 int g_opt_mq_disable = 0;
 int g_opt_split_spw = 0;
 int g_opt_split_nbuf = 0;
+int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -42,6 +44,7 @@ struct Plan {
     int lds;
     size_t ws_bytes, cnt_bytes, ml_bytes;
     bool mq;  // multi-query kernel (fattn_mq.h)
+    bool pf;  // prefill kernel (fattn_pf.h)
     int nw;   // its waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
 };
 
@@ -314,8 +317,27 @@ int make_plan(const fattn_params* p, Plan& pl) {
         a.n_hsub = 1;
         a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
     }
+    // prefill shapes: 256-row workgroups over 64-key tiles, no KV split, when
+    // the (kv head x query tile x seq) workgroups alone fill the chip
+    pl.pf = false;
+    if (pl.mq && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
+        (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= kCUs)) {
+        pl.pf = true;
+        pl.mq = false;
+        a.QPT = kPfRows / a.R;
+        a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
+    }
     const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
     if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
+    if (pl.pf) {
+        a.chunk_len = (int)N;
+        a.n_chunks = 1;
+        a.ncp = 1;
+        pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
+        pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
+        pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
+        return FATTN_OK;
+    }
     const int rc = pl.mq ? size_mq(pl, p->kv_chunk, Y, S, N) : size_split(pl, p->kv_chunk, Y, S, N, NQ);
     if (rc != FATTN_OK) return rc;
     return FATTN_OK;
@@ -394,8 +416,28 @@ int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
     return pl.a.has_mask ? launch_mq_hm<KT, D, 4, true>(pl, st, ev) : launch_mq_hm<KT, D, 4, false>(pl, st, ev);
 }
 
+template <int KT, bool HM>
+int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
+    auto kern = fattn_pf_kernel<KT, 128, HM>;
+    return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        hipLaunchKernelGGL(kern, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
+    });
+}
+
+template <int KT>
+int launch_pf(const Plan& pl, hipStream_t st, const Events& ev) {
+    return pl.a.has_mask ? launch_pf_hm<KT, true>(pl, st, ev) : launch_pf_hm<KT, false>(pl, st, ev);
+}
+
 template <int D>
 int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
+    if constexpr (D == 128) {
+        if (pl.pf) {
+            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0>(pl, st, ev);
+            return FATTN_ERR_UNSUPPORTED_TYPE;
+        }
+    }
     if (pl.mq) {
         if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_mq<FATTN_TYPE_Q8_0, D>(pl, st, ev);
         if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_mq<FATTN_TYPE_Q4_0, D>(pl, st, ev);
@@ -437,6 +479,10 @@ int fattn_set_option(int option, int value) {
             return FATTN_OK;
         case FATTN_OPT_MQ_DISABLE:
             g_opt_mq_disable = value ? 1 : 0;
+            return FATTN_OK;
+        case FATTN_OPT_PF:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_pf = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_STEPS:
             if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;

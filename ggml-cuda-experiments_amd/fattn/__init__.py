@@ -39,6 +39,7 @@ OPT_MQ_ROWS_PER_WAVE = 1
 OPT_MQ_DISABLE = 2
 OPT_SPLIT_STEPS = 3
 OPT_SPLIT_INFLIGHT = 4
+OPT_PF = 5
 
 
 class FattnError(RuntimeError):

@@ -196,6 +196,79 @@ def test_mq_fully_masked_rows_are_nan(dev):
     assert attn_rel_err(got, ref) <= RTOL
 
 
+# ------------------------------------------------------------------ prefill kernel (fattn_pf.h)
+# 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
+# workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
+
+@pytest.fixture
+def pf_force():
+    fattn.set_option(fattn.OPT_PF, 2)
+    yield
+    fattn.set_option(fattn.OPT_PF, 0)
+
+
+PF_CASES = [
+    dict(kv_type="q8_0", NQ=256, H=4, Hkv=4, N=256, mask="causal"),
+    dict(kv_type="q4_0", NQ=256, H=2, Hkv=2, N=512, mask="random"),
+    dict(kv_type="q4_0", NQ=64, H=16, Hkv=4, N=512, mask="random"),          # R=4: 64 queries x 4 heads
+    dict(kv_type="q8_0", NQ=40, H=16, Hkv=2, N=128, mask="random"),          # R=8, ragged query tile
+    dict(kv_type="q8_0", NQ=300, H=2, Hkv=2, N=256, mask="none"),            # two query tiles, ragged
+    dict(kv_type="q8_0", NQ=100, H=2, Hkv=2, N=192, mask="neginf_blocks", S=2),  # odd tile count, 2 seqs
+    dict(kv_type="q4_0", NQ=256, H=2, Hkv=2, N=64, mask="zero"),             # one tile
+    dict(kv_type="q8_0", NQ=4, H=64, Hkv=1, N=128, mask="random"),           # R=64, QPT=4
+]
+
+
+@pytest.mark.parametrize("case", PF_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_pf_sweep(dev, pf_force, case):
+    p = make_problem(D=128, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
+def test_pf_rescale(dev, pf_force, kt):
+    """Large scores and scores rising along the sequence: deferred-max rescales."""
+    for extreme, ramp, seed in ((True, 0.0, 26), (False, 12.0, 27)):
+        p = make_problem(D=128, NQ=256, H=2, N=2048, kv_type=kt, seed=seed, extreme=extreme, ramp=ramp,
+                         mask="none" if ramp else "random")
+        assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+def test_pf_fully_masked_rows_are_nan(dev, pf_force):
+    p = make_problem(D=128, NQ=256, H=2, N=256, kv_type="q8_0", mask="zero", seed=28)
+    m = orc.f16_bits_to_f32(p.mask_bits)
+    m[7, :] = -np.inf
+    p.mask_bits = orc.f32_to_f16_bits(m)
+    got, ref = run_gpu(p), p.oracle()
+    assert np.isnan(ref[:, 7]).all() and np.isnan(got[:, 7]).all()
+    assert attn_rel_err(got, ref) <= RTOL
+
+
+def test_pf_prefill_full_matches_mq(dev):
+    """The prefill shape at full size (n_q = N = 4096, 32 heads, Q8_0, random mask):
+    the prefill kernel (auto-selected) against the multi-query kernel, and one
+    head of it against the oracle."""
+    import torch
+    p = make_problem(D=128, NQ=4096, H=32, N=4096, kv_type="q8_0", seed=29)
+    a = run_gpu(p)
+    fattn.set_option(fattn.OPT_PF, 1)
+    try:
+        b = run_gpu(p)
+    finally:
+        fattn.set_option(fattn.OPT_PF, 0)
+    assert np.isfinite(a).all()
+    assert attn_rel_err(a, b) <= RTOL
+    # head 5, query rows 0..255: oracle on the sliced problem
+    sub = make_problem(D=128, NQ=256, H=1, N=4096, kv_type="q8_0", seed=29)
+    sub.q = np.ascontiguousarray(p.q[:, :256, 5:6, :])
+    kb = p.k_bytes.reshape(p.Hkv, -1)[5:6].reshape(-1)
+    vb = p.v_bytes.reshape(p.Hkv, -1)[5:6].reshape(-1)
+    sub.k_bytes, sub.v_bytes = np.ascontiguousarray(kb), np.ascontiguousarray(vb)
+    sub.mask_bits = np.ascontiguousarray(p.mask_bits[:256])
+    ref = sub.oracle()
+    assert attn_rel_err(a[:, :256, 5:6, :], ref) <= RTOL
+
+
 # ------------------------------------------------------------------ sweep
 
 CASES = []

@@ -10,10 +10,12 @@ import json
 import subprocess
 import sys
 
-libs = ["libfattn.so", "libfattn_mq_nomem.so", "libfattn_mq_nodeq.so", "libfattn_mq_nocomp.so"]
-cases = [("c5", ["--n-q", "64", "--steps", "50", "--warmup", "5"]),
-         ("c5_1ch", ["--n-q", "64", "--steps", "20", "--warmup", "2", "--kv-chunk", "4096"]),
-         ("prefill", ["--n-q", "4096", "--steps", "5", "--warmup", "1", "--rotate", "2"])]
+libs = ["libfattn.so", "libfattn_mq_nomem.so", "libfattn_mq_nodeq.so", "libfattn_mq_nocomp.so", "libfattn_pf_nosm.so"]
+import sys as _s
+cases = [("prefill", ["--n-q", "4096", "--steps", "5", "--warmup", "1", "--rotate", "2"])]
+if "--all" in _s.argv:
+    cases = [("c5", ["--n-q", "64", "--steps", "50", "--warmup", "5"]),
+             ("c5_1ch", ["--n-q", "64", "--steps", "20", "--warmup", "2", "--kv-chunk", "4096"])] + cases
 for name, args in cases:
     for lib in libs:
         env = dict(__import__("os").environ, FATTN_LIB=lib)
