@@ -17,7 +17,9 @@ Prints ONE JSON line (rank 0).  `value` = whole-job algorithmic bytes / time
 (GB/s); `roofline` prices the dominant kernel (fattn_split_kernel) from HIP
 events around that kernel alone; `cpu_baseline` times the reference's own CPU
 oracle (src/utils.h compiled from /root/reference into oracle/_ref) on a bounded
-sample of the same workload.
+sample of the same workload; `prefill` (N=1) prices fattn_pf_kernel against
+the dense f16 MFMA peak on the compute-bound prefill shape (n_q = N = 4096,
+north_star's MFMA-utilisation target), 5 graph-captured launches.
 """
 from __future__ import annotations
 
@@ -82,6 +84,59 @@ def cpu_baseline(seconds: float, threads: int):
             "ms_per_problem": round(el / reps * 1e3, 2), "host_cpu": _cpu_model()}
 
 
+def prefill_measure(dev, hip, evs, steps=5):
+    """The MFMA-bound prefill shape of SURVEY.md §8d (n_q = N = 4096, 32 heads,
+    head_dim 128, Q8_0 K/V, random f16 mask, non-causal): `steps` launches of
+    fattn_pf_kernel captured in one HIP graph, HIP events around the replay on
+    the launch stream.  Two rotated KV caches (compute-bound: the cache state
+    barely matters).  Returns the TFLOP/s roofline object."""
+    import torch
+    import fattn
+    D, H, N, NQ, R = 128, 32, 4096, 4096, 2
+    typ = fattn.TYPE_Q8_0
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321)
+    kv = [[fattn.quantize(torch.rand((H * N, D), generator=g, device=dev) * 2 - 1, typ).reshape(-1)
+           for _ in range(2)] for _ in range(R)]
+    q = torch.rand((1, NQ, H, D), generator=g, device=dev) * 2 - 1
+    mask = (torch.rand((NQ, N), generator=g, device=dev) * 2 - 1).to(torch.float16)
+    out = torch.empty((R, 1, NQ, H, D), dtype=torch.float32, device=dev)
+    att = fattn.Attention(fattn.q_view(q), fattn.kv_view(kv[0][0], typ, D, N, H), fattn.kv_view(kv[0][1], typ, D, N, H),
+                          fattn.mask_view(mask), out[0], 1.0 / D ** 0.5)
+
+    def step(i):
+        att.retarget(k=kv[i % R][0].data_ptr(), v=kv[i % R][1].data_ptr(), dst=out[i % R].data_ptr())
+        att()
+
+    gs = torch.cuda.Stream(dev)
+    gs.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(gs):
+        for i in range(2):
+            step(i)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=gs):
+        for i in range(steps):
+            step(i)
+    with torch.cuda.stream(gs):
+        graph.replay()
+    torch.cuda.synchronize()
+    f = C.c_float()
+    hip.hipEventRecord(evs[0], gs.cuda_stream)
+    with torch.cuda.stream(gs):
+        graph.replay()
+    hip.hipEventRecord(evs[1], gs.cuda_stream)
+    torch.cuda.synchronize()
+    hip.hipEventElapsedTime(C.byref(f), evs[0], evs[1])
+    ms = f.value / steps
+    flops = 4 * NQ * N * D * H
+    tf = flops / (ms * 1e-3) / 1e12
+    return {"workload": f"prefill_q8_0_h{H}_d{D}_n{N}_q{NQ}_mask", "kernel": "fattn_pf_kernel<q8_0,D128>",
+            "kernel_ms_avg": round(ms, 5), "flops_per_step": flops,
+            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None}}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -109,10 +164,12 @@ def main():
     ap.add_argument("--spw", type=int, default=0, help="split kernel: steps per wave (0 = planner)")
     ap.add_argument("--inflight", type=int, default=0, help="split kernel: steps in flight per wave (0 = planner)")
     ap.add_argument("--no-mask", action="store_true", help="no mask tensor (diagnostics; the metric uses a mask)")
+    ap.add_argument("--pf-stagger", type=int, default=0)
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prefill", action="store_true", help="skip the prefill-shape MFMA measurement")
     args = ap.parse_args()
 
     import torch
@@ -125,6 +182,7 @@ def main():
         fattn.set_option(fattn.OPT_SPLIT_INFLIGHT, args.inflight)
     if args.pf:
         fattn.set_option(fattn.OPT_PF, args.pf)
+    fattn.set_option(fattn.OPT_PF_STAGGER, args.pf_stagger)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -248,7 +306,10 @@ def main():
     rk2 = H // Hkv
     mq = (args.kv_type != "f16" and args.layout == "head" and NQ * rk2 >= 32 and rk2 <= 64
           and rk2 & (rk2 - 1) == 0 and N % 32 == 0)
-    kname = (f"fattn_mq_kernel<{args.kv_type},D{D}>" if mq
+    # the prefill kernel replaces it when the 256-row workgroups fill the chip
+    pf = (mq and args.pf != 1 and D == 128 and args.kv_chunk <= 0 and N % 64 == 0 and
+          (args.pf == 2 or Hkv * ((NQ * rk2 + 255) // 256) >= 256))
+    kname = (f"fattn_pf_kernel<{args.kv_type},D{D}>" if pf else f"fattn_mq_kernel<{args.kv_type},D{D}>" if mq
              else f"fattn_split_kernel<{args.kv_type},{args.kv_type},D{D}>")
     # compute-bound once arithmetic intensity passes the ridge (peak flops / peak bytes)
     mfma_bound = flops_step / bytes_step > MFMA_F16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
@@ -290,6 +351,9 @@ def main():
                          {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname}),
         }
+        if world == 1 and not args.no_prefill and NQ == 1:
+            # north_star's second target: MFMA utilisation on the prefill shape
+            res["prefill"] = prefill_measure(dev, hip, evs)
         if world == 1 and not args.no_cpu_baseline and NQ == 1:  # kernel_test.h's CPU path is one query row
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, min(args.cpu_threads, os.cpu_count() or 1))
         print(json.dumps(res), flush=True)

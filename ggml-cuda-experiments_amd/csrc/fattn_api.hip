@@ -31,6 +31,7 @@ int g_opt_mq_disable = 0;
 int g_opt_split_spw = 0;
 int g_opt_split_nbuf = 0;
 int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
+int g_opt_pf_stagger = 0;
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -320,7 +321,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // prefill shapes: 256-row workgroups over 64-key tiles, no KV split, when
     // the (kv head x query tile x seq) workgroups alone fill the chip
     pl.pf = false;
-    if (pl.mq && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
+    if (pl.mq && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 && p->scale > 0.0f &&
         (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= kCUs)) {
         pl.pf = true;
         pl.mq = false;
@@ -331,6 +332,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
     if (pl.pf) {
         a.chunk_len = (int)N;
+        a.pf_stagger = g_opt_pf_stagger;
         a.n_chunks = 1;
         a.ncp = 1;
         pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
@@ -483,6 +485,9 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_PF:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_pf = value;
+            return FATTN_OK;
+        case FATTN_OPT_PF_STAGGER:
+            g_opt_pf_stagger = value ? 1 : 0;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_STEPS:
             if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;

@@ -12,26 +12,30 @@
 //    head, 32 per wave; the KV sequence is walked in 64-key tiles;
 //  * HBM -> LDS: the tile's raw ggml K and V rows by buffer_load ... lds (1-KiB
 //    wave instructions dealt round-robin over the waves), three raw tiles in
-//    flight; the workgroup dequantises each tile ONCE (one half ggml block per
-//    thread for K and one for V) into f16 K and V images, h(q*d) with one f16
-//    rounding (src/utils.h:10-11);
+//    flight; the workgroup dequantises each tile ONCE -- wave w takes half
+//    block w of every row, K and V -- into f16 K and V images, h(q*d) with one
+//    f16 rounding (src/utils.h:10-11);
 //  * "swapped" products on v_mfma_f32_32x32x16_f16: S^T = K.Q^T (K rows from
 //    the image by ds_read_b128, Q^T kept in registers), so a lane holds 16
-//    keys of ONE query row -- the row max / sum are 31 in-lane ops and one
+//    keys of ONE query row -- the row max / sum are in-lane ops and one
 //    v_permlane32_swap; then O^T = V^T.P^T where P^T is the S^T accumulator
 //    itself converted to f16 (no lane movement): the 16 keys of each PV k-step
 //    are taken in the accumulator's own order and V^T is gathered in the same
 //    order with ds_read_b64_tr_b16 (4 keys x 16 dims per 16-lane group);
-//  * mask values straight from L2 into registers one tile ahead (the mask of
-//    a query row is shared by every head of the row, so it stays L2-resident);
+//  * each wave's 32 mask rows of a tile (4 KiB) arrive by four coalesced 1-KiB
+//    LDS-DMA instructions into the wave's own LDS slot, a tile ahead;
 //  * one workgroup barrier per tile: while the waves run tile s from one image
 //    pair, the workgroup dequantises tile s+1 into the other and tiles s+2,
-//    s+3 are in flight.
+//    s+3 are in flight; the two waves of each SIMD run their phases staggered
+//    (one's VALU beside the other's MFMA).
 //
-// LDS images: K [64 keys][D] f16, 16-B chunk c of row r at c ^ (r & 15) (rows
-// 0..15 of one ds_read_b128 phase hit 16 distinct chunks); V [64 keys][D] f16,
-// chunk c of row r at c ^ 2(r & 3) (the 4 rows x 32 B of one transposed-read
-// lane group hit 8 distinct chunks, chunk pairs stay adjacent).
+// LDS (D = 128), every image read address = one per-lane base + an immediate:
+//   [0, 64 KiB)   two image pairs.  K image [8 dim-slices][64 keys][32 B]
+//                 (16-B halves swapped on rows with bit 3 set); V image
+//                 [4 dim-blocks][64 keys][64 B] (16-B chunk c of row r at
+//                 c ^ ((r >> 2) & 3)).  Both read and written conflict-free.
+//   then          3 raw tiles [K rows | V rows], 8 mask slots [32 rows][8 x 16 B]
+//                 (16-B piece pc of row r at pc ^ ((r >> 1) & 7)).
 #pragma once
 
 #include "fattn_mq.h"
@@ -47,84 +51,90 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <int KT, int D>
 struct PfCfg {
+    static_assert(D == 128, "one half ggml block per wave and row");
     static constexpr int NT = kPfWaves * kWave;
     static constexpr int rowB = row_bytes<KT, D>();
     static constexpr int kvRaw = kPfKeys * rowB;                    // raw K (or V) bytes per tile
     static constexpr int rawBytes = (2 * kvRaw + 15) / 16 * 16;
     static constexpr int nRaw = 3;
     static constexpr int img = kPfKeys * D * 2;                     // one f16 image
-    static constexpr int imgOff = nRaw * rawBytes;
-    static constexpr int ldsBytes = imgOff + 2 * 2 * img;           // + (K16, V16) x 2
+    static constexpr int pairBytes = 2 * img;                       // K image + V image
+    static constexpr int rawOff = 2 * pairBytes;                    // 64 KiB
+    static constexpr int maskOff = rawOff + nRaw * rawBytes;
+    static constexpr int maskSlot = kPfRowsW * 128;                 // 32 rows x 64 keys x f16
+    static constexpr int ldsBytes = maskOff + kPfWaves * maskSlot;
     static constexpr int NI = (kvRaw + 1023) / 1024;                // 1-KiB DMA instructions per K (or V) tile
     // instructions j = 0 .. 2*NI-1 (K then V) go to wave j % 8
     static constexpr int ni_wave(int w) { return (2 * NI - w + kPfWaves - 1) / kPfWaves; }
-    static constexpr int NB = D / QK;                               // ggml blocks per row
-    static constexpr int NU = kPfKeys * NB * 2;                     // half blocks per image
-    static_assert(NU == NT, "one K and one V half block per thread");
+    static constexpr int NIM = maskSlot / 1024;                     // mask DMA instructions per wave and tile
     static_assert(ldsBytes <= 163840, "");
 };
 
 template <int KT, int D>
-__device__ __forceinline__ void pf_issue(const StepSrc& rs, int n0, uint8_t* buf, int wave, int lane) {
+__device__ __forceinline__ void pf_issue(const StepSrc& rs, int n0, uint32_t lds, int wave, int lane) {
 #ifdef FATTN_MQ_NOMEM
     return;  // diagnostic build only
 #endif
     using C = PfCfg<KT, D>;
-    const uint32_t lb = lds_addr(buf);
     for (int j = wave; j < 2 * C::NI; j += kPfWaves) {  // wave-uniform
         const bool is_v = j >= C::NI;
         const int i = is_v ? j - C::NI : j;
         const int byte = i * 1024 + lane * 16;
         if (C::kvRaw % 1024 == 0 || byte < C::kvRaw)
-            dma<16>(is_v ? rs.v : rs.k, lb + (is_v ? C::kvRaw : 0) + i * 1024, (uint32_t)n0 * C::rowB + byte);
+            dma<16>(is_v ? rs.v : rs.k, lds + (is_v ? C::kvRaw : 0) + i * 1024, (uint32_t)n0 * C::rowB + byte);
     }
 }
 
-// counted wait: all but this wave's `pending` youngest DMA tiles (pending 0/1),
-// with `extra` younger non-DMA loads allowed to stay in flight too
-template <int NI>
-__device__ __forceinline__ void pf_wait_n(int pending) {
-    if (pending <= 0) {
-        wait_vmcnt_c<0>();
-    } else {
-        wait_vmcnt_c<NI>();
+// counted wait: at most nraw (0..2) raw-tile DMA groups and nmask (0/1) mask
+// groups of this wave still in flight (vmcnt counts in issue order)
+template <int KT, int D, int W>
+__device__ __forceinline__ void pf_vm_wait_w(int nraw, int nmask) {
+    constexpr int NI = PfCfg<KT, D>::ni_wave(W);
+    constexpr int NM = PfCfg<KT, D>::NIM;
+    const int k = nraw * 4 + nmask;
+    switch (k) {
+        case 0: wait_vmcnt_c<0>(); break;
+        case 1: wait_vmcnt_c<NM>(); break;
+        case 4: wait_vmcnt_c<NI>(); break;
+        case 5: wait_vmcnt_c<NI + NM>(); break;
+        case 8: wait_vmcnt_c<2 * NI>(); break;
+        default: wait_vmcnt_c<2 * NI + NM>(); break;
     }
 }
 template <int KT, int D>
-__device__ __forceinline__ void pf_wait(int wave, int pending) {
-    using C = PfCfg<KT, D>;
+__device__ __forceinline__ void pf_vm_wait(int wave, int nraw, int nmask) {
     switch (wave) {
-        case 0: pf_wait_n<C::ni_wave(0)>(pending); break;
-        case 1: pf_wait_n<C::ni_wave(1)>(pending); break;
-        case 2: pf_wait_n<C::ni_wave(2)>(pending); break;
-        case 3: pf_wait_n<C::ni_wave(3)>(pending); break;
-        case 4: pf_wait_n<C::ni_wave(4)>(pending); break;
-        case 5: pf_wait_n<C::ni_wave(5)>(pending); break;
-        case 6: pf_wait_n<C::ni_wave(6)>(pending); break;
-        default: pf_wait_n<C::ni_wave(7)>(pending); break;
+        case 0: pf_vm_wait_w<KT, D, 0>(nraw, nmask); break;
+        case 1: pf_vm_wait_w<KT, D, 1>(nraw, nmask); break;
+        case 2: pf_vm_wait_w<KT, D, 2>(nraw, nmask); break;
+        case 3: pf_vm_wait_w<KT, D, 3>(nraw, nmask); break;
+        case 4: pf_vm_wait_w<KT, D, 4>(nraw, nmask); break;
+        case 5: pf_vm_wait_w<KT, D, 5>(nraw, nmask); break;
+        case 6: pf_vm_wait_w<KT, D, 6>(nraw, nmask); break;
+        default: pf_vm_wait_w<KT, D, 7>(nraw, nmask); break;
     }
 }
 
-// raw tile -> f16 images: thread t dequantises half block (t & 1) of block
-// (t >> 1) % NB of row t / (2 NB), for K and for V
+// raw tile -> f16 images: wave w dequantises half h = w & 1 of block b = w >> 1
+// of row `lane`, for K (into dim slice 2b + h) and V (dim block b, chunks 2h, 2h+1)
 template <int KT, int D>
-__device__ __forceinline__ void pf_dequant(const uint8_t* rb, uint8_t* k16, uint8_t* v16, int tid) {
+__device__ __forceinline__ void pf_dequant(const uint8_t* rb, uint8_t* k16, uint8_t* v16, int wave, int lane) {
 #ifdef FATTN_MQ_NODEQ
     return;  // diagnostic build only
 #endif
     using C = PfCfg<KT, D>;
-    constexpr int NB = C::NB;
-    const int row = tid / (2 * NB), b = (tid / 2) % NB, h = tid & 1;
+    const int b = wave >> 1, h = wave & 1;
     u32x4 ck[2], cv[2];
-    dequant_half<KT, D>(rb, row, b, h, ck);
-    dequant_half<KT, D>(rb + C::kvRaw, row, b, h, cv);
-    const int c0 = 4 * b + 2 * h;
-    uint8_t* kd = k16 + row * (D * 2);
-    uint8_t* vd = v16 + row * (D * 2);
-    *(u32x4*)(kd + ((c0 ^ (row & 15)) * 16)) = ck[0];
-    *(u32x4*)(kd + (((c0 + 1) ^ (row & 15)) * 16)) = ck[1];
-    *(u32x4*)(vd + ((c0 ^ (2 * (row & 3))) * 16)) = cv[0];
-    *(u32x4*)(vd + (((c0 + 1) ^ (2 * (row & 3))) * 16)) = cv[1];
+    dequant_half<KT, D>(rb, lane, b, h, ck);
+    dequant_half<KT, D>(rb + C::kvRaw, lane, b, h, cv);
+    uint8_t* kd = k16 + wave * (kPfKeys * 32) + lane * 32;
+    const int sk = (lane >> 3) & 1;
+    *(u32x4*)(kd + sk * 16) = ck[0];
+    *(u32x4*)(kd + (sk ^ 1) * 16) = ck[1];
+    uint8_t* vd = v16 + b * (kPfKeys * 64) + lane * 64;
+    const int sv = (lane >> 2) & 3;
+    *(u32x4*)(vd + ((2 * h) ^ sv) * 16) = cv[0];
+    *(u32x4*)(vd + ((2 * h + 1) ^ sv) * 16) = cv[1];
 }
 
 __device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
@@ -137,6 +147,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NK = D / 16;   // 16-dim k-steps of S^T = K.Q^T
     constexpr int NDB = D / 32;  // 32-dim blocks of O^T
+    constexpr int NM = HM ? 1 : 0;
     constexpr float kNegInf = -__builtin_inff();
     constexpr float kDeferLog2 = 8.0f;
     const int tid = threadIdx.x;
@@ -154,18 +165,24 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         ik2 = y / a.n_qt;
     }
     if (a.rk3 != 1) ik3 = iq3 / a.rk3;
-    const int p = kPfRowsW * wave + c32;  // packed row
-    const int mq = div_R(a, p);
-    const int iq1 = qt * a.QPT + mq;
-    const int iq2 = ik2 * a.rk2 + (p - mq * a.R);
-    const bool row_ok = iq1 < a.NQ;
+    auto row_of = [&](int p, int& iq1, int& iq2) {  // packed row -> (query row, q head)
+        const int mq = div_R(a, p);
+        iq1 = qt * a.QPT + mq;
+        iq2 = ik2 * a.rk2 + (p - mq * a.R);
+        return iq1 < a.NQ;
+    };
+    int iq1, iq2;
+    const bool row_ok = row_of(kPfRowsW * wave + c32, iq1, iq2);
     const int ntiles = a.N / kPfKeys;
 
     StepSrc rs;
     rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
     rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
-    auto raw = [&](int s) { return smem + (s % C::nRaw) * C::rawBytes; };
-    auto k16_of = [&](int s) { return smem + C::imgOff + (s & 1) * 2 * C::img; };
+    rs.m = make_srd(a.mask, HM ? a.m_span : 0);
+    const uint32_t lds0 = lds_addr(smem);
+    auto raw_lds = [&](int s) { return lds0 + C::rawOff + (s % C::nRaw) * C::rawBytes; };
+    auto raw_ptr = [&](int s) { return smem + C::rawOff + (s % C::nRaw) * C::rawBytes; };
+    const uint32_t mslot = lds0 + C::maskOff + wave * C::maskSlot;
 
     // ---- Q^T operands (B of S^T = K.Q^T): dims 16kk + 8h .. +8 of this lane's
     // row, rounded to f16 like src/utils.h:10; rows past n_q read zeros
@@ -186,59 +203,66 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             qop[kk] = hq;
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // ---- mask: this lane's keys of tile s are 32t + 8u + 4h + {0..3}
-    // (u = 0..3): eight 8-B loads into registers, a tile ahead.  Issued as
-    // inline asm (like the LDS-DMA): the compiler's own waits would otherwise
-    // count them without the DMA behind them and drain the prefetch; the
-    // explicit counted wait at the top of each tile covers them.
-    const i32x4 msrd = make_srd(a.mask, HM ? a.m_span : 0);
-    const uint32_t mrow = HM && row_ok ? (uint32_t)iq1 * (uint32_t)a.m_nb1 : (HM ? a.m_span : 0u);
-    auto mask_issue = [&](int s, u32x2 (&mk)[2][4]) {
+    // ---- mask DMA: instruction k of a tile fills slot units 64k .. 64k+63;
+    // lane i -> unit 64k + i = row 8k + i/8, stored piece i%8 = piece
+    // (i%8) ^ ((row >> 1) & 7) of the row's 128 B (64 keys)
+    uint32_t moff[C::NIM];
+    if constexpr (HM) {
+#pragma unroll
+        for (int k = 0; k < C::NIM; k++) {
+            const int rr = 8 * k + (lane >> 3);
+            int q1, q2;
+            const bool ok = row_of(kPfRowsW * wave + rr, q1, q2);
+            const int pc = (lane & 7) ^ ((rr >> 1) & 7);
+            moff[k] = ok ? (uint32_t)q1 * (uint32_t)a.m_nb1 + 16 * pc : a.m_span;
+        }
+    }
+    auto mask_issue = [&](int s) {
         if constexpr (HM) {
+#ifndef FATTN_MQ_NOMEM
+            const uint32_t n2 = (uint32_t)s * kPfKeys * 2;
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t off = row_ok ? mrow + (uint32_t)(s * kPfKeys + 32 * t + 8 * u + 4 * h) * 2 : mrow;
-                    asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(mk[t][u]) : "v"(off), "s"(msrd) : "memory");
-                }
+            for (int k = 0; k < C::NIM; k++) {
+                const uint32_t off = moff[k] == a.m_span ? a.m_span : moff[k] + n2;
+                dma<16>(rs.m, mslot + k * 1024, off);
             }
+#endif
         }
     };
-    // two register sets, alternating by tile parity (no copies of asm-loaded
-    // registers before their wait)
-    u32x2 mkA[2][4], mkB[2][4];
+    // this lane's mask reads: row c32, piece pc = 4t + u (keys 32t + 8u + 0..7), half h
+    uint32_t maddr[2][4];
 #pragma unroll
     for (int t = 0; t < 2; t++) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) mkA[t][u] = mkB[t][u] = u32x2{0u, 0u};
+        for (int u = 0; u < 4; u++)
+            maddr[t][u] = C::maskOff + wave * C::maskSlot + (c32 * 8 + ((4 * t + u) ^ ((c32 >> 1) & 7))) * 16 + 8 * h;
     }
 
-    // ---- prologue: mask 0, raw tiles 0..2; dequantise tile 0
-    if (ntiles > 0) mask_issue(0, mkA);
-    for (int s = 0; s < 3 && s < ntiles; s++) pf_issue<KT, D>(rs, s * kPfKeys, raw(s), wave, lane);
-    // raw 0 and mask 0 landed; raw 1, 2 may still fly
-    if (ntiles > 2) {
-        switch (wave) {  // two DMA tiles younger than raw 0
-            case 0: wait_vmcnt_c<2 * C::ni_wave(0)>(); break;
-            case 1: wait_vmcnt_c<2 * C::ni_wave(1)>(); break;
-            case 2: wait_vmcnt_c<2 * C::ni_wave(2)>(); break;
-            case 3: wait_vmcnt_c<2 * C::ni_wave(3)>(); break;
-            case 4: wait_vmcnt_c<2 * C::ni_wave(4)>(); break;
-            case 5: wait_vmcnt_c<2 * C::ni_wave(5)>(); break;
-            case 6: wait_vmcnt_c<2 * C::ni_wave(6)>(); break;
-            default: wait_vmcnt_c<2 * C::ni_wave(7)>(); break;
-        }
-    } else {
-        pf_wait<KT, D>(wave, ntiles - 1);
+    // per-lane LDS read bases (image pair 0; pair 1 is + pairBytes)
+    // K: slice kk, row 32t + c32, half h -> kk*2048 + t*1024 + kbase
+    const uint32_t kbase = c32 * 32 + ((h ^ ((c32 >> 3) & 1)) * 16);
+    // V^T gather, 16-lane group (h, dh), lane gi of it: row 32t + 16q + 8e + 4h + gi/4,
+    // chunk (2dh + (gi&3)/2) ^ ((h + 2e) & 3), half gi&1 -> db*4096 + t*2048 + q*1024 + vbase[e]
+    const int gi = lane & 15, dh = (lane >> 4) & 1;
+    uint32_t vbase[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int row = 8 * e + 4 * h + (gi >> 2);
+        const int ch = (2 * dh + ((gi & 3) >> 1)) ^ ((h + 2 * e) & 3);
+        vbase[e] = C::img + row * 64 + ch * 16 + (gi & 1) * 8;
     }
+
+    // ---- prologue: raw tiles 0..2, mask 0; dequantise tile 0
+    for (int s = 0; s < 3 && s < ntiles; s++) pf_issue<KT, D>(rs, s * kPfKeys, raw_lds(s), wave, lane);
+    if (ntiles > 0) mask_issue(0);
+    // raw 0 landed (raw 1, 2 and mask 0 may fly on)
+    pf_vm_wait<KT, D>(wave, min(2, ntiles - 1), ntiles > 0 ? NM : 0);
     __syncthreads();
-    if (ntiles > 0) pf_dequant<KT, D>(raw(0), k16_of(0), k16_of(0) + C::img, tid);
+    if (ntiles > 0) pf_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, wave, lane);
 
-    float m_run = kNegInf;  // reference max (log2 domain) of this lane's row
-    float l_run = 0.0f;     // this lane's partial row sum (its 32 of every 64 keys)
+    float m_run = kNegInf;    // reference max (log2 domain) of this lane's row
+    f32x2 l2 = {0.0f, 0.0f};  // this lane's partial row sums (its 32 of every 64 keys)
     f32x16 o[NDB];
 #pragma unroll
     for (int db = 0; db < NDB; db++) {
@@ -246,24 +270,56 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         for (int j = 0; j < 16; j++) o[db][j] = 0.0f;
     }
     const float log2e = 1.4426950408889634f;
+    const float scale = a.scale_log2 / log2e;
 
-    auto body = [&](int s, u32x2 (&mk_cur)[2][4], u32x2 (&mk_next)[2][4]) {
-        // raw s+1 and mask s landed (the youngest DMA tile, s+2, may fly on)
-        pf_wait<KT, D>(wave, s + 2 < ntiles ? 1 : 0);
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-#pragma unroll
-            for (int u = 0; u < 4; u++) reg_fence(mk_cur[t][u]);
-        }
+#ifdef FATTN_STAMPS
+    // diagnostic build only: shader-clock cycles per phase, summed over tiles
+    // (0 wait+barrier, 1 DMA issue, 2 dequant, 3 S^T, 4 softmax, 5 O^T)
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t_prev = __builtin_amdgcn_s_memtime();
+#define PF_T(k)                                              \
+    do {                                                     \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
+        ph[k] += t_ - t_prev;                                \
+        t_prev = t_;                                         \
+    } while (0)
+#else
+#define PF_T(k) do { } while (0)
+#endif
+    auto body = [&](int s, auto par) {
+        constexpr int P = decltype(par)::value;  // image pair of tile s
+        // raw s+1 landed (raw s+2 and mask s may fly on)
+        PF_T(7);
+        pf_vm_wait<KT, D>(wave, s + 2 < ntiles ? 1 : 0, NM);
         __syncthreads();
-        if (s + 1 < ntiles) mask_issue(s + 1, mk_next);
-        if (s + 3 < ntiles) pf_issue<KT, D>(rs, (s + 3) * kPfKeys, raw(s + 3), wave, lane);
-        if (s + 1 < ntiles) pf_dequant<KT, D>(raw(s + 1), k16_of(s + 1), k16_of(s + 1) + C::img, tid);
+        PF_T(0);
+        if (s + 3 < ntiles) pf_issue<KT, D>(rs, (s + 3) * kPfKeys, raw_lds(s + 3), wave, lane);
+        PF_T(1);
+        // SIMD partners (waves w and w + 4) run the tile's phases staggered:
+        // waves 0-3 dequantise first (VALU) while waves 4-7 run S^T (MFMA),
+        // then each one's softmax (VALU) meets the other's MFMA phase, and
+        // waves 4-7 dequantise last while waves 0-3 run O^T
+        // (MI355X_MICROARCH.md, two waves per SIMD)
+        const bool late = a.pf_stagger && wave >= kPfWaves / 2;
+        auto dequant_next = [&] {
+            if (s + 1 < ntiles)
+                pf_dequant<KT, D>(raw_ptr(s + 1), smem + (P ^ 1) * C::pairBytes,
+                                  smem + (P ^ 1) * C::pairBytes + C::img, wave, lane);
+        };
+        if (!late) {
+            dequant_next();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            PF_T(2);
+        }
 #ifdef FATTN_MQ_NOCOMPUTE
+        if constexpr (HM) {
+            pf_vm_wait<KT, D>(wave, s + 3 < ntiles ? 1 : 0, 0);
+            if (s + 1 < ntiles) mask_issue(s + 1);
+        }
+        if (late) dequant_next();
         return;  // diagnostic build only: copies, dequant and barriers
 #endif
-        const uint8_t* k16 = k16_of(s);
-        const uint8_t* v16 = k16 + C::img;
+        const uint8_t* img = smem + P * C::pairBytes;  // K image; vbase includes + img
 
         // -- S^T = K.Q^T: two 32-key subtiles
         f32x16 st[2];
@@ -271,30 +327,56 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         for (int t = 0; t < 2; t++) {
 #pragma unroll
             for (int j = 0; j < 16; j++) st[t][j] = 0.0f;
-            const int row = 32 * t + c32;
 #pragma unroll
             for (int kk = 0; kk < NK; kk++) {
-                const f16x8 ka = *(const f16x8*)(k16 + row * (D * 2) + (((2 * kk + h) ^ (row & 15)) * 16));
+                const f16x8 ka = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024);
                 st[t] = mfma32(ka, qop[kk], st[t]);
             }
         }
 
-        // -- online softmax (log2 domain); element j of subtile t is key
-        // 32t + 8(j/4) + 4h + (j%4) of this lane's row
-        float sv[2][16];
+#ifdef FATTN_STAMPS
+        {   // wait for the S^T results before the stamp
+            float z = 0.0f;
+            for (int t = 0; t < 2; t++) z += st[t][0] + st[t][15];
+            asm volatile("" ::"v"(z));
+        }
+#endif
+        PF_T(3);
+        // -- scores (natural units) u = scale * s + mask; element j of subtile t
+        // is key 32t + 8(j/4) + 4h + (j%4) of this lane's row
+        float u[2][16];
+        if constexpr (HM) {
+            // mask s landed (raw s+3 may fly on); read it, then refill the slot
+            pf_vm_wait<KT, D>(wave, s + 3 < ntiles ? 1 : 0, 0);
+            u32x2 mk[2][4];
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
+            for (int t = 0; t < 2; t++) {
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                float mk[4] = {0.f, 0.f, 0.f, 0.f};
-                if constexpr (HM) {
-                    const f16x2 m01 = as_h2(mk_cur[t][u].x), m23 = as_h2(mk_cur[t][u].y);
-                    mk[0] = (float)m01.x; mk[1] = (float)m01.y; mk[2] = (float)m23.x; mk[3] = (float)m23.y;
+                for (int uu = 0; uu < 4; uu++) mk[t][uu] = *(const u32x2*)(smem + maddr[t][uu]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (s + 1 < ntiles) mask_issue(s + 1);
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+#pragma unroll
+                for (int uu = 0; uu < 4; uu++) {
+                    const f16x2 m01 = as_h2(mk[t][uu].x), m23 = as_h2(mk[t][uu].y);
+                    u[t][4 * uu + 0] = fmaf(st[t][4 * uu + 0], scale, (float)m01.x);
+                    u[t][4 * uu + 1] = fmaf(st[t][4 * uu + 1], scale, (float)m01.y);
+                    u[t][4 * uu + 2] = fmaf(st[t][4 * uu + 2], scale, (float)m23.x);
+                    u[t][4 * uu + 3] = fmaf(st[t][4 * uu + 3], scale, (float)m23.y);
                 }
+            }
+        } else {
 #pragma unroll
-                for (int r = 0; r < 4; r++) sv[t][4 * u + r] = st[t][4 * u + r] * a.scale_log2 + mk[r] * log2e;
+            for (int t = 0; t < 2; t++) {
+#pragma unroll
+                for (int j = 0; j < 16; j++) u[t][j] = st[t][j];
             }
         }
+        // exponent argument: x * c - m (log2 domain); c = log2e with a mask,
+        // scale * log2e without (scale > 0: the planner's condition)
+        const float c = HM ? log2e : a.scale_log2;
 #ifdef FATTN_PF_NOSOFTMAX
         // diagnostic build only: P = raw scores (MFMA + LDS reads, no softmax)
         f16x8 pb[2][2];
@@ -304,39 +386,37 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             for (int q = 0; q < 2; q++) {
                 f16x8 x;
 #pragma unroll
-                for (int i = 0; i < 8; i++) x[i] = (f16)sv[t][8 * q + i];
+                for (int i = 0; i < 8; i++) x[i] = (f16)u[t][8 * q + i];
                 pb[t][q] = x;
             }
         }
-        l_run += 1.0f;
+        l2.x += 1.0f;
 #else
         float tmax = kNegInf;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
 #pragma unroll
-            for (int j = 0; j < 16; j++) tmax = fmaxf(tmax, sv[t][j]);
+            for (int j = 0; j < 16; j++) tmax = fmaxf(tmax, u[t][j]);
         }
-        tmax = xor32_pair(tmax, true);
+        tmax = xor32_pair(tmax, true) * c;
         // deferred max (cdna_hip_programming.md T13), as in the multi-query kernel
         if (__builtin_amdgcn_ballot_w64(tmax > m_run + kDeferLog2)) {
             const float m_new = fmaxf(m_run, tmax);
             const float alpha = (m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run - m_new);
-            l_run *= alpha;
+            l2 *= alpha;
 #pragma unroll
             for (int db = 0; db < NDB; db++) o[db] *= alpha;
             m_run = m_new;
         }
-        const float m_use = (m_run == kNegInf) ? 0.0f : m_run;
+        const float nm = (m_run == kNegInf) ? 0.0f : -m_run;
         f16x8 pb[2][2];
-        float lsum = 0.0f;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
             float pv[16];
 #pragma unroll
-            for (int j = 0; j < 16; j++) {
-                pv[j] = __builtin_amdgcn_exp2f(sv[t][j] - m_use);
-                lsum += pv[j];
-            }
+            for (int j = 0; j < 16; j++) pv[j] = __builtin_amdgcn_exp2f(fmaf(u[t][j], c, nm));
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) l2 += f32x2{pv[j], pv[j + 1]};
 #pragma unroll
             for (int q = 0; q < 2; q++) {
                 f16x8 x;
@@ -345,45 +425,65 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
                 pb[t][q] = x;
             }
         }
-        l_run += lsum;
 #endif
 
+#ifdef FATTN_STAMPS
+        {
+            uint32_t z = 0;
+            for (int t = 0; t < 2; t++) z += __builtin_bit_cast(u32x4, pb[t][0]).x + __builtin_bit_cast(u32x4, pb[t][1]).w;
+            asm volatile("" ::"v"(z));
+        }
+#endif
+        PF_T(4);
         // -- O^T += V^T.P^T: k-step (t, q) covers keys 32t + 16q + 8(i/4) + 4h + (i%4)
-        // of k-group h (i = 0..7), V^T gathered in that order: 16-lane group
-        // (h, dh) reads rows r0 + {0..3} (r0 = 32t + 16q + 4h, then + 8) x dims
-        // 32db + 16dh + {0..15}; lane i of the group supplies row r0 + i/4, dims
-        // + 4(i%4) .. + 3, and receives dim 32db + 16dh + i of the 4 rows
-        const int gi = lane & 15, dh = (lane >> 4) & 1;
+        // of k-group h (i = 0..7); V^T gathered in that order (rows + 0 / + 8)
 #pragma unroll
         for (int t = 0; t < 2; t++) {
 #pragma unroll
             for (int q = 0; q < 2; q++) {
-                const int r0 = 32 * t + 16 * q + 4 * h + (gi >> 2);
-                const int r1 = r0 + 8;
 #pragma unroll
                 for (int db = 0; db < NDB; db++) {
-                    const int ch = 4 * db + 2 * dh + ((gi & 3) >> 1);
-                    const int a0 = r0 * (D * 2) + ((ch ^ (2 * (r0 & 3))) * 16) + (gi & 1) * 8;
-                    const int a1 = r1 * (D * 2) + ((ch ^ (2 * (r1 & 3))) * 16) + (gi & 1) * 8;
                     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v16 + a0));
-                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v16 + a1));
-                    const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
-                    const u32x4 r = {l2.x, l2.y, h2.x, h2.y};
+                    const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[0] + off));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[1] + off));
+                    const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                    const u32x4 r = {a2.x, a2.y, b2.x, b2.y};
                     o[db] = mfma32(__builtin_bit_cast(f16x8, r), pb[t][q], o[db]);
                 }
             }
         }
+#ifdef FATTN_STAMPS
+        {
+            float z = 0.0f;
+            for (int db = 0; db < NDB; db++) z += o[db][0];
+            asm volatile("" ::"v"(z));
+        }
+#endif
+        PF_T(5);
+        if (late) {
+            dequant_next();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            PF_T(2);
+        }
     };
     for (int s = 0; s < ntiles; s += 2) {
-        body(s, mkA, mkB);
-        if (s + 1 < ntiles) body(s + 1, mkB, mkA);
+        body(s, std::integral_constant<int, 0>());
+        if (s + 1 < ntiles) body(s + 1, std::integral_constant<int, 1>());
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#ifdef FATTN_STAMPS
+    if (lane == 0 && g_stamps) {
+        const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        for (int k = 0; k < 8; k++) g_stamps[(blk * kPfWaves + wave) * 16 + k] = ph[k];
+        g_stamps[(blk * kPfWaves + wave) * 16 + 8] = (unsigned long long)ntiles;
+    }
+#endif
+#undef PF_T
 
     // ---- normalise and store: O^T element j of block db is dim
     // 32db + 8(j/4) + 4h + (j%4) of this lane's row
-    const float l_tot = xor32_pair(l_run, false);
+    const float l_tot = xor32_pair(l2.x + l2.y, false);
     if (row_ok) {
         float* out = a.dst + (((int64_t)iq3 * a.NQ + iq1) * a.H + iq2) * D + 4 * h;
         const float inv = 1.0f / l_tot;  // fully masked row -> NaN like the reference

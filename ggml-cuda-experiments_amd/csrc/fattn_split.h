@@ -68,6 +68,7 @@ struct SplitArgs {
     int has_mask;
     int nbuf;           // steps in flight per wave (1..4); LDS per wave = wave_bytes
     int wave_bytes;
+    int pf_stagger;     // prefill kernel: SIMD partner waves run their phases staggered
 };
 
 template <int KT, int VT, int D>

@@ -40,6 +40,7 @@ OPT_MQ_DISABLE = 2
 OPT_SPLIT_STEPS = 3
 OPT_SPLIT_INFLIGHT = 4
 OPT_PF = 5
+OPT_PF_STAGGER = 6
 
 
 class FattnError(RuntimeError):

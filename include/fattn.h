@@ -120,8 +120,9 @@ enum {
     FATTN_OPT_MQ_DISABLE = 2,       /* 1 = never pick the multi-query kernel (split-KV kernel only) */
     FATTN_OPT_SPLIT_STEPS = 3,      /* split kernel: 32-position steps per wave (0 = auto, 1..64) */
     FATTN_OPT_SPLIT_INFLIGHT = 4,   /* split kernel: steps in flight per wave (0 = auto, 1..4; LDS permitting) */
-    FATTN_OPT_PF = 5                /* prefill kernel: 0 = auto, 1 = never, 2 = whenever eligible (even if the
+    FATTN_OPT_PF = 5,               /* prefill kernel: 0 = auto, 1 = never, 2 = whenever eligible (even if the
                                        workgroups do not fill the chip) */
+    FATTN_OPT_PF_STAGGER = 6        /* prefill kernel: 1 = SIMD partner waves staggered, 0 (default) = lockstep */
 };
 int fattn_set_option(int option, int value);
 
