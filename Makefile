@@ -31,11 +31,11 @@ stamps: $(LIBDIR)/libfattn_stamps.so $(LIBDIR)/libfattn_nocompute.so $(LIBDIR)/l
 
 $(LIBDIR)/libfattn_nt.so: $(CSRC) $(CHDR)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -DFATTN_DMA_NT -shared $(CSRC) -o $@
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DMA_NO_NT -shared $(CSRC) -o $@
 
 $(LIBDIR)/libfattn_nt_stamps.so: $(CSRC) $(CHDR)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -DFATTN_DMA_NT -DFATTN_STAMPS -shared $(CSRC) -o $@
+	$(HIPCC) $(HIPFLAGS) -DFATTN_DMA_NO_NT -DFATTN_STAMPS -shared $(CSRC) -o $@
 
 ntdiag: $(LIBDIR)/libfattn_nt.so $(LIBDIR)/libfattn_nt_stamps.so
 

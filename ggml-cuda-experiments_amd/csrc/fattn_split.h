@@ -38,7 +38,12 @@ constexpr int kSplitWaves = 4;
 constexpr int kStep = 32;   // KV positions per wave step (= one PV k-step)
 constexpr int kRows = 16;   // packed query rows per workgroup (MFMA N)
 constexpr int VT_F16T = 100;  // V f16 stored transposed ([D][N], flash_row_float.h:177)
-constexpr int kCntStride = 64;  // uint32 words between arrival counters (256 B: atomics to one line serialise)
+constexpr int kCntStride = 64;
+#ifdef FATTN_DMA_NO_NT
+constexpr bool kDecodeNT = false;  // diagnostic build only
+#else
+constexpr bool kDecodeNT = true;   // decode K/V: read once per launch
+#endif  // uint32 words between arrival counters (256 B: atomics to one line serialise)
 
 struct SplitArgs {
     const uint8_t* q;
@@ -150,6 +155,15 @@ __device__ __forceinline__ i32x4 make_srd(const void* base, uint32_t bytes) {
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(const lds_void*)p; }
 
+// L1-bypassing (sc1) 16-B load through a buffer descriptor; offsets at or past
+// num_records return zeros without memory traffic.  Inline asm like ld_sc1
+// (fattn_common.h): explicit wait + reg_fence before use.
+__device__ __forceinline__ u32x4 ld_sc1_buf(const i32x4& srd, uint32_t off) {
+    u32x4 v;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(srd) : "memory");
+    return v;
+}
+
 // HBM -> LDS, one piece per lane at lds + lane*BYTES.  Inline asm: through the
 // builtin, hipcc treats the LDS base as a per-lane value, and around an
 // exec-masked (partial) instruction it built per-lane phis of (LDS base,
@@ -158,17 +172,29 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(
 // (saved and restored: M0 is compiler-reserved; s_nop 0 = M0 -> LDS-DMA
 // hazard).  Not tracked by the compiler's s_waitcnt bookkeeping: every
 // consumer waits with an explicit vmcnt.
-#ifdef FATTN_DMA_NT
-#define FATTN_DMA_MOD " nt"
-#else
-#define FATTN_DMA_MOD ""
-#endif
-template <int BYTES>
+// NT: non-temporal policy for bytes one CU reads once (the decode KV stream,
+// MI355X_MICROARCH.md 'nt-weights'); never for tiles other workgroups re-read.
+template <int BYTES, bool NT = false>
 __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds, uint32_t off) {
     uint32_t keep;
-    if constexpr (BYTES == 16) {
+    if constexpr (BYTES == 16 && NT) {
         asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" FATTN_DMA_MOD " lds\n\t"
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(off), "s"(srd), "s"(lds)
+            : "memory");
+    } else if constexpr (BYTES == 16) {
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(off), "s"(srd), "s"(lds)
+            : "memory");
+    } else if constexpr (NT) {
+        static_assert(BYTES == 4, "");
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen nt lds\n\t"
             "s_mov_b32 m0, %0"
             : "=&s"(keep)
             : "v"(off), "s"(srd), "s"(lds)
@@ -176,7 +202,7 @@ __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds, uint32_t off
     } else {
         static_assert(BYTES == 4, "");
         asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen" FATTN_DMA_MOD " lds\n\t"
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
             "s_mov_b32 m0, %0"
             : "=&s"(keep)
             : "v"(off), "s"(srd), "s"(lds)
@@ -217,7 +243,7 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs
             const int row = byte / C::rowK;
             off = (uint32_t)(n0 + row) * kn1 + (byte % C::rowK);
         }
-        if (P::PK % kWave == 0 || p < P::PK) dma<GRAN>(rs.k, lds_addr(buf + i * kWave * GRAN), off);
+        if (P::PK % kWave == 0 || p < P::PK) dma<GRAN, kDecodeNT>(rs.k, lds_addr(buf + i * kWave * GRAN), off);
     }
     uint8_t* vbuf = buf + C::kBytes;
 #pragma unroll
@@ -240,7 +266,7 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs
             const int row = byte / C::rowV;
             off = (uint32_t)(n0 + row) * vn1 + (byte % C::rowV);
         }
-        if (P::PV % kWave == 0 || p < P::PV) dma<GRAN>(rs.v, lds_addr(vbuf + i * kWave * GRAN), off);
+        if (P::PV % kWave == 0 || p < P::PV) dma<GRAN, kDecodeNT>(rs.v, lds_addr(vbuf + i * kWave * GRAN), off);
     }
     if constexpr (HM) {
         uint8_t* mbuf = buf + C::kBytes + C::vBytes;
@@ -250,7 +276,10 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs
             const int mr = q / P::MPR;
             const int off = (q % P::MPR) * P::MG;
             const uint32_t moff = (uint32_t)(mrow0 + mr) * (uint32_t)a.m_nb1 + (uint32_t)n0 * 2 + off;
-            dma<P::MG>(rs.m, lds_addr(mbuf + i * kWave * P::MG), moff);
+            // 16-B path (one instruction, rows 0..15): lanes of rows past the
+            // tile's query rows stay idle -- row 0's lanes always issue it, so
+            // the per-step instruction count (vmcnt budget) is unchanged
+            if (GRAN != 16 || mr < a.QPT) dma<P::MG>(rs.m, lds_addr(mbuf + i * kWave * P::MG), moff);
         }
     }
 }
@@ -410,7 +439,7 @@ __device__ unsigned long long* g_stamps;
 
 // ---------------------------------------------------------------- kernel
 
-template <int D>
+template <int D, int CB = 2>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
                                              int rv, int row_base, uint8_t* smem);
 
@@ -825,7 +854,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     __syncthreads();
     FATTN_STAMP(12);
     if (!*last_flag) return;
-    combine_tile<D>(a, tile, qt, hs, ik2, iq3, rv, 0, smem);
+    combine_tile<D, (D == 128 && KT != FATTN_TYPE_F16) ? 8 : 2>(a, tile, qt, hs, ik2, iq3, rv, 0, smem);
     FATTN_STAMP(13);
 }
 
@@ -841,12 +870,15 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
 // (row_base != 0: the multi-query kernel's 16-row subtiles).  Written for
 // 256 threads; in a 512-thread workgroup the upper half only joins the
 // barriers (its groups, rows and chunks are all out of range).
-template <int D>
+template <int D, int CB>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
                                              int rv, int row_base, uint8_t* smem) {
     constexpr float kNegInf = -__builtin_inff();
     constexpr int EPT = D / 16;
-    constexpr int CB = 2;  // chunks per load batch (register budget of the split kernel)
+    // CB = chunks per load batch: with 8 (the split kernel at D = 128) every
+    // thread's partials come in ONE memory round trip up to 8 chunks per thread
+    // (config 4: 32 chunks x 4 rows); batch slots past the thread's chunks
+    // issue no load
     float(*red)[D] = (float(*)[D])smem;                                // [16][D]
     float(*wts)[64] = (float(*)[64])(smem + kRows * D * 4);            // [16][64]
     float* rowL = (float*)(smem + kRows * D * 4 + kRows * 64 * 4);     // [16]
@@ -858,14 +890,21 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
     const bool active = grp < rv * G;
     const int kmax = active ? (NCH - cg + G - 1) / G : 0;
     auto fl = [](uint32_t x) { return __builtin_bit_cast(float, x); };
-    // partial loads of chunks cg + (k0 + kk) * G (clamped index, zero weight past kmax)
+    // partial loads of chunks cg + (k0 + kk) * G through a buffer descriptor
+    // over this tile's partials: slots past kmax use an out-of-range offset
+    // (zeros, no memory traffic; zero weight too).  Every lane executes every
+    // load -- an asm load under a branch would leave a register copy (phi)
+    // reading the destination before its wait.
+    const uint32_t obytes = (uint32_t)(NCH * kRows * D * 4);
+    const i32x4 osrd = make_srd(a.ws_o + sb * kRows * D, obytes);
     auto issue = [&](u32x4 (&v)[CB][EPT / 4], int k0) {
 #pragma unroll
         for (int kk = 0; kk < CB; kk++) {
-            const int c = min(cg + (k0 + kk) * G, NCH - 1);
-            const float* wo = a.ws_o + ((sb + c) * kRows + (active ? r : 0)) * D + d0;
+            const int c = cg + (k0 + kk) * G;
+            const uint32_t off =
+                (k0 + kk < kmax) ? (uint32_t)(((c * kRows + (active ? r : 0)) * D + d0) * 4) : obytes;
 #pragma unroll
-            for (int e = 0; e < EPT / 4; e++) v[kk][e] = ld_sc1(wo + 4 * e);
+            for (int e = 0; e < EPT / 4; e++) v[kk][e] = ld_sc1_buf(osrd, off + 16 * e);
         }
     };
     auto fence_all = [&](u32x4 (&v)[CB][EPT / 4]) {
