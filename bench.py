@@ -164,7 +164,7 @@ def main():
     ap.add_argument("--spw", type=int, default=0, help="split kernel: steps per wave (0 = planner)")
     ap.add_argument("--inflight", type=int, default=0, help="split kernel: steps in flight per wave (0 = planner)")
     ap.add_argument("--no-mask", action="store_true", help="no mask tensor (diagnostics; the metric uses a mask)")
-    ap.add_argument("--pf-stagger", type=int, default=0)
+    ap.add_argument("--pf-stagger", type=int, default=2)
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)

@@ -31,7 +31,7 @@ int g_opt_mq_disable = 0;
 int g_opt_split_spw = 0;
 int g_opt_split_nbuf = 0;
 int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
-int g_opt_pf_stagger = 0;
+int g_opt_pf_stagger = 2;
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -487,7 +487,8 @@ int fattn_set_option(int option, int value) {
             g_opt_pf = value;
             return FATTN_OK;
         case FATTN_OPT_PF_STAGGER:
-            g_opt_pf_stagger = value ? 1 : 0;
+            if (value < 0 || value > 3) return FATTN_ERR_INVALID_ARG;
+            g_opt_pf_stagger = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_STEPS:
             if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;
