@@ -37,6 +37,10 @@ $(LIBDIR)/libfattn_nt_stamps.so: $(CSRC) $(CHDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DFATTN_DMA_NO_NT -DFATTN_STAMPS -shared $(CSRC) -o $@
 
+$(LIBDIR)/libfattn_pf4nosgb.so: $(CSRC) $(CHDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_PF4_NO_SGB -shared $(CSRC) -o $@
+
 ntdiag: $(LIBDIR)/libfattn_nt.so $(LIBDIR)/libfattn_nt_stamps.so
 
 mqdiag: $(LIBDIR)/libfattn_mq_nomem.so $(LIBDIR)/libfattn_mq_nodeq.so $(LIBDIR)/libfattn_mq_nocomp.so \

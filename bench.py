@@ -165,6 +165,7 @@ def main():
     ap.add_argument("--inflight", type=int, default=0, help="split kernel: steps in flight per wave (0 = planner)")
     ap.add_argument("--no-mask", action="store_true", help="no mask tensor (diagnostics; the metric uses a mask)")
     ap.add_argument("--pf-stagger", type=int, default=2)
+    ap.add_argument("--pf-waves", type=int, default=0, help="prefill kernel waves (4 or 8; 0 = library default)")
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -183,6 +184,8 @@ def main():
     if args.pf:
         fattn.set_option(fattn.OPT_PF, args.pf)
     fattn.set_option(fattn.OPT_PF_STAGGER, args.pf_stagger)
+    if args.pf_waves:
+        fattn.set_option(fattn.OPT_PF_WAVES, args.pf_waves)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

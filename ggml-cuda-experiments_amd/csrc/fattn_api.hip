@@ -17,6 +17,7 @@
 #include "fattn_quant.h"
 #include "fattn_mq.h"
 #include "fattn_pf.h"
+#include "fattn_pf4.h"
 #include "fattn_split.h"
 
 using namespace fattn;
@@ -32,6 +33,7 @@ int g_opt_split_spw = 0;
 int g_opt_split_nbuf = 0;
 int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
 int g_opt_pf_stagger = 2;
+int g_opt_pf_waves = 8;
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -45,7 +47,8 @@ struct Plan {
     int lds;
     size_t ws_bytes, cnt_bytes, ml_bytes;
     bool mq;  // multi-query kernel (fattn_mq.h)
-    bool pf;  // prefill kernel (fattn_pf.h)
+    bool pf;  // prefill kernel (fattn_pf.h, or fattn_pf4.h when pf_waves == 4)
+    int pf_waves;
     int nw;   // its waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
 };
 
@@ -335,7 +338,11 @@ int make_plan(const fattn_params* p, Plan& pl) {
         a.pf_stagger = g_opt_pf_stagger;
         a.n_chunks = 1;
         a.ncp = 1;
-        pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
+        pl.pf_waves = g_opt_pf_waves;
+        if (pl.pf_waves == 4)
+            pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? Pf4Cfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : Pf4Cfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
+        else
+            pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
         return FATTN_OK;
@@ -420,6 +427,12 @@ int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
 
 template <int KT, bool HM>
 int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
+    if (pl.pf_waves == 4) {
+        auto kern4 = fattn_pf4_kernel<KT, 128, HM>;
+        return launch_kernel((const void*)kern4, pl, st, ev, [&] {
+            hipLaunchKernelGGL(kern4, pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
+        });
+    }
     auto kern = fattn_pf_kernel<KT, 128, HM>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         hipLaunchKernelGGL(kern, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
@@ -489,6 +502,10 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_PF_STAGGER:
             if (value < 0 || value > 3) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_stagger = value;
+            return FATTN_OK;
+        case FATTN_OPT_PF_WAVES:
+            if (value != 4 && value != 8) return FATTN_ERR_INVALID_ARG;
+            g_opt_pf_waves = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_STEPS:
             if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;

@@ -41,6 +41,7 @@ OPT_SPLIT_STEPS = 3
 OPT_SPLIT_INFLIGHT = 4
 OPT_PF = 5
 OPT_PF_STAGGER = 6
+OPT_PF_WAVES = 7
 
 
 class FattnError(RuntimeError):

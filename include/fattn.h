@@ -122,8 +122,9 @@ enum {
     FATTN_OPT_SPLIT_INFLIGHT = 4,   /* split kernel: steps in flight per wave (0 = auto, 1..4; LDS permitting) */
     FATTN_OPT_PF = 5,               /* prefill kernel: 0 = auto, 1 = never, 2 = whenever eligible (even if the
                                        workgroups do not fill the chip) */
-    FATTN_OPT_PF_STAGGER = 6        /* prefill kernel, bit 0: SIMD partner waves staggered (default lockstep);
+    FATTN_OPT_PF_STAGGER = 6,       /* prefill kernel, bit 0: SIMD partner waves staggered (default lockstep);
                                        bit 1 (default on): waves 4-7 at s_setprio 1 */
+    FATTN_OPT_PF_WAVES = 7          /* prefill kernel: 8 = 8 waves x 32 rows, 4 = 4 waves x 64 rows (one per SIMD) */
 };
 int fattn_set_option(int option, int value);
 

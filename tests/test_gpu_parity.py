@@ -200,11 +200,15 @@ def test_mq_fully_masked_rows_are_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture
-def pf_force():
+@pytest.fixture(params=[8, 4], ids=["8waves", "4waves"])
+def pf_force(request):
+    """Prefill kernel on every eligible problem, in both forms: 8 waves x 32
+    rows (fattn_pf.h) and 4 waves x 64 rows (fattn_pf4.h)."""
     fattn.set_option(fattn.OPT_PF, 2)
+    fattn.set_option(fattn.OPT_PF_WAVES, request.param)
     yield
     fattn.set_option(fattn.OPT_PF, 0)
+    fattn.set_option(fattn.OPT_PF_WAVES, 8)
 
 
 PF_CASES = [
@@ -244,13 +248,18 @@ def test_pf_fully_masked_rows_are_nan(dev, pf_force):
     assert attn_rel_err(got, ref) <= RTOL
 
 
-def test_pf_prefill_full_matches_mq(dev):
+@pytest.mark.parametrize("waves", [8, 4])
+def test_pf_prefill_full_matches_mq(dev, waves):
     """The prefill shape at full size (n_q = N = 4096, 32 heads, Q8_0, random mask):
     the prefill kernel (auto-selected) against the multi-query kernel, and one
     head of it against the oracle."""
     import torch
     p = make_problem(D=128, NQ=4096, H=32, N=4096, kv_type="q8_0", seed=29)
-    a = run_gpu(p)
+    fattn.set_option(fattn.OPT_PF_WAVES, waves)
+    try:
+        a = run_gpu(p)
+    finally:
+        fattn.set_option(fattn.OPT_PF_WAVES, 8)
     fattn.set_option(fattn.OPT_PF, 1)
     try:
         b = run_gpu(p)
