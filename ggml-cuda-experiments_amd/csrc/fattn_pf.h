@@ -327,17 +327,19 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
 #endif
         const uint8_t* img = smem + P * C::pairBytes;  // K image; vbase includes + img
 
-        // -- S^T = K.Q^T: two 32-key subtiles
+        // -- S^T = K.Q^T: two 32-key subtiles; each subtile's 8 K operands are
+        // read before its MFMA chain (one LDS wait per chain, not per MFMA)
         f32x16 st[2];
 #pragma unroll
         for (int t = 0; t < 2; t++) {
+            f16x8 ka[NK];
+#pragma unroll
+            for (int kk = 0; kk < NK; kk++) ka[kk] = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024);
+            __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the chain
 #pragma unroll
             for (int j = 0; j < 16; j++) st[t][j] = 0.0f;
 #pragma unroll
-            for (int kk = 0; kk < NK; kk++) {
-                const f16x8 ka = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024);
-                st[t] = mfma32(ka, qop[kk], st[t]);
-            }
+            for (int kk = 0; kk < NK; kk++) st[t] = mfma32(ka[kk], qop[kk], st[t]);
         }
 
 #ifdef FATTN_STAMPS
@@ -443,20 +445,24 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         PF_T(4);
         // -- O^T += V^T.P^T: k-step (t, q) covers keys 32t + 16q + 8(i/4) + 4h + (i%4)
         // of k-group h (i = 0..7); V^T gathered in that order (rows + 0 / + 8)
+        // (per k-step: the 8 transposed reads of its 4 dim blocks, then 4 MFMAs)
 #pragma unroll
         for (int t = 0; t < 2; t++) {
 #pragma unroll
             for (int q = 0; q < 2; q++) {
+                typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+                u32x4 va[NDB];
 #pragma unroll
                 for (int db = 0; db < NDB; db++) {
-                    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
                     const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
                     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[0] + off));
                     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[1] + off));
                     const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
-                    const u32x4 r = {a2.x, a2.y, b2.x, b2.y};
-                    o[db] = mfma32(__builtin_bit_cast(f16x8, r), pb[t][q], o[db]);
+                    va[db] = u32x4{a2.x, a2.y, b2.x, b2.y};
                 }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[t][q], o[db]);
             }
         }
 #ifdef FATTN_STAMPS
