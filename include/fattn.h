@@ -108,9 +108,9 @@ int fattn_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 int fattn_ext(const fattn_params* p, void* stream);
 
 /* Same as fattn_ext, additionally recording the hipEvent_t `ev_begin` / `ev_end`
- * on `stream` immediately before / after the main attention kernel (excluding
- * the split-KV combine), so a caller can time the dominant kernel alone with
- * hipEventElapsedTime.  Either event may be NULL. */
+ * on `stream` immediately before / after the attention kernel (one launch: the
+ * split-KV chunk merge is fused into it), so a caller can time that kernel alone
+ * with hipEventElapsedTime.  Either event may be NULL. */
 int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* ev_end);
 
 /* Process-wide planner overrides (tests, benchmarks).  Not thread-safe against
