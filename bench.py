@@ -84,7 +84,7 @@ def cpu_baseline(seconds: float, threads: int):
             "ms_per_problem": round(el / reps * 1e3, 2), "host_cpu": _cpu_model()}
 
 
-def prefill_measure(dev, hip, evs, steps=5):
+def prefill_measure(dev, hip, evs, kvn="q8_0", pf_dequant=0, pf_pipe=0, steps=5):
     """The MFMA-bound prefill shape of SURVEY.md §8d (n_q = N = 4096, 32 heads,
     head_dim 128, Q8_0 K/V, random f16 mask, non-causal): `steps` launches of
     fattn_pf_kernel captured in one HIP graph, HIP events around the replay on
@@ -93,11 +93,16 @@ def prefill_measure(dev, hip, evs, steps=5):
     import torch
     import fattn
     D, H, N, NQ, R = 128, 32, 4096, 4096, 2
-    typ = fattn.TYPE_Q8_0
+
+    typ = fattn.TYPE_NAMES[kvn]
     g = torch.Generator(device=dev)
     g.manual_seed(4321)
-    kv = [[fattn.quantize(torch.rand((H * N, D), generator=g, device=dev) * 2 - 1, typ).reshape(-1)
-           for _ in range(2)] for _ in range(R)]
+    if kvn == "f16":
+        kv = [[(torch.rand((H * N, D), generator=g, device=dev) * 2 - 1).to(torch.float16).reshape(-1)
+               for _ in range(2)] for _ in range(R)]
+    else:
+        kv = [[fattn.quantize(torch.rand((H * N, D), generator=g, device=dev) * 2 - 1, typ).reshape(-1)
+               for _ in range(2)] for _ in range(R)]
     q = torch.rand((1, NQ, H, D), generator=g, device=dev) * 2 - 1
     mask = (torch.rand((NQ, N), generator=g, device=dev) * 2 - 1).to(torch.float16)
     out = torch.empty((R, 1, NQ, H, D), dtype=torch.float32, device=dev)
@@ -131,7 +136,11 @@ def prefill_measure(dev, hip, evs, steps=5):
     ms = f.value / steps
     flops = 4 * NQ * N * D * H
     tf = flops / (ms * 1e-3) / 1e12
-    return {"workload": f"prefill_q8_0_h{H}_d{D}_n{N}_q{NQ}_mask", "kernel": "fattn_pf_kernel<q8_0,D128>",
+    pre = kvn != "f16" and pf_dequant == 2
+    f16k = "fattn_pfp_kernel<f16,D128>" if pf_pipe == 2 else "fattn_pf_kernel<f16,D128>"
+    kname = (f"pf_dequant_rows_kernel<{kvn}> x2 + {f16k}" if pre
+             else f16k if kvn == "f16" else f"fattn_pf_kernel<{kvn},D128>")
+    return {"workload": f"prefill_{kvn}_h{H}_d{D}_n{N}_q{NQ}_mask", "kernel": kname,
             "kernel_ms_avg": round(ms, 5), "flops_per_step": flops,
             "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None}}
@@ -167,6 +176,12 @@ def main():
     ap.add_argument("--pf-stagger", type=int, default=2)
     ap.add_argument("--pf-waves", type=int, default=0, help="prefill kernel waves (4 or 8; 0 = library default)")
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
+    ap.add_argument("--pf-dequant", type=int, default=0,
+                    help="quantised prefill: 0 auto, 1 in-kernel dequantisation, 2 f16 pre-pass")
+    ap.add_argument("--pf-pipe", type=int, default=0,
+                    help="prefill over f16 images: 0 auto, 1 fattn_pf_kernel, 2 software-pipelined fattn_pfp_kernel")
+    ap.add_argument("--prefill-kv", default="q8_0", choices=["q8_0", "q4_0", "f16"],
+                    help="K/V type of the prefill measurement (the metric's is q8_0)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -186,6 +201,10 @@ def main():
     fattn.set_option(fattn.OPT_PF_STAGGER, args.pf_stagger)
     if args.pf_waves:
         fattn.set_option(fattn.OPT_PF_WAVES, args.pf_waves)
+    if args.pf_dequant:
+        fattn.set_option(fattn.OPT_PF_DEQUANT, args.pf_dequant)
+    if args.pf_pipe:
+        fattn.set_option(fattn.OPT_PF_PIPE, args.pf_pipe)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -356,7 +375,7 @@ def main():
         }
         if world == 1 and not args.no_prefill and NQ == 1:
             # north_star's second target: MFMA utilisation on the prefill shape
-            res["prefill"] = prefill_measure(dev, hip, evs)
+            res["prefill"] = prefill_measure(dev, hip, evs, args.prefill_kv, args.pf_dequant, args.pf_pipe)
         if world == 1 and not args.no_cpu_baseline and NQ == 1:  # kernel_test.h's CPU path is one query row
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, min(args.cpu_threads, os.cpu_count() or 1))
         print(json.dumps(res), flush=True)

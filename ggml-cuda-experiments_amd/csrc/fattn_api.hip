@@ -18,6 +18,7 @@
 #include "fattn_mq.h"
 #include "fattn_pf.h"
 #include "fattn_pf4.h"
+#include "fattn_pfp.h"
 #include "fattn_split.h"
 
 using namespace fattn;
@@ -34,6 +35,8 @@ int g_opt_split_nbuf = 0;
 int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
 int g_opt_pf_stagger = 2;
 int g_opt_pf_waves = 8;
+int g_opt_pf_dequant = 0;  // 0 auto, 1 in the prefill kernel, 2 pre-pass to f16 rows
+int g_opt_pf_pipe = 0;     // f16 images: 0 auto, 1 fattn_pf_kernel, 2 fattn_pfp_kernel
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -49,6 +52,10 @@ struct Plan {
     bool mq;  // multi-query kernel (fattn_mq.h)
     bool pf;  // prefill kernel (fattn_pf.h, or fattn_pf4.h when pf_waves == 4)
     int pf_waves;
+    bool pf_pre;            // quantised K/V converted to f16 rows in the workspace first
+    bool pf_pipe;           // f16 images: the software-pipelined kernel (fattn_pfp.h)
+    int64_t pf_rows;        // rows per converted tensor (Skv * Hkv * N)
+    int64_t hkv;            // kv heads
     int nw;   // its waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
 };
 
@@ -323,13 +330,21 @@ int make_plan(const fattn_params* p, Plan& pl) {
     }
     // prefill shapes: 256-row workgroups over 64-key tiles, no KV split, when
     // the (kv head x query tile x seq) workgroups alone fill the chip
+    // (f16 K/V rows, not transposed V: the same kernel, images filled by DMA)
     pl.pf = false;
-    if (pl.mq && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 && p->scale > 0.0f &&
-        (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= kCUs)) {
+    pl.pf_pre = false;
+    const bool heads_ok = NQ * a.rk2 >= 32 && a.rk2 <= 64 && (a.rk2 & (a.rk2 - 1)) == 0;
+    const bool pf_f16 = !g_opt_mq_disable && k.type == FATTN_TYPE_F16 && !v_trans && g16 && heads_ok;
+    if ((pl.mq || pf_f16) && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
+        p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= kCUs)) {
         pl.pf = true;
         pl.mq = false;
+        a.R = a.rk2;
+        a.R_inv = 1.0f / (float)a.R;
+        a.n_hsub = 1;
         a.QPT = kPfRows / a.R;
         a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
+        pl.pf_pre = is_quant(k.type) && g_opt_pf_dequant == 2 && g_opt_pf_waves == 8;
     }
     const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
     if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
@@ -338,13 +353,24 @@ int make_plan(const fattn_params* p, Plan& pl) {
         a.pf_stagger = g_opt_pf_stagger;
         a.n_chunks = 1;
         a.ncp = 1;
-        pl.pf_waves = g_opt_pf_waves;
-        if (pl.pf_waves == 4)
+        pl.pf_waves = pl.kt == FATTN_TYPE_F16 ? 8 : g_opt_pf_waves;
+        pl.hkv = Hkv;
+        pl.pf_rows = Skv * Hkv * N;
+        pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
+        // auto = fattn_pf_kernel: the pipelined kernel measures slower so far
+        // (DESIGN.md §9); kept behind the option while its schedule is worked on
+        pl.pf_pipe = (pl.kt == FATTN_TYPE_F16 || pl.pf_pre) && g_opt_pf_pipe == 2;
+        if (pl.pf_pipe)
+            pl.lds = PfpCfg::ldsBytes;
+        else if (pl.kt == FATTN_TYPE_F16 || pl.pf_pre)
+            pl.lds = PfCfg<FATTN_TYPE_F16, 128>::ldsBytes;
+        else if (pl.pf_waves == 4)
             pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? Pf4Cfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : Pf4Cfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
         else
             pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
-        pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
+        // pre-pass: [K rows | V rows], f16 [Skv][Hkv][N][D] each
+        if (pl.pf_pre) pl.ws_bytes = 2 * (size_t)pl.pf_rows * D * 2;
         return FATTN_OK;
     }
     const int rc = pl.mq ? size_mq(pl, p->kv_chunk, Y, S, N) : size_split(pl, p->kv_chunk, Y, S, N, NQ);
@@ -427,11 +453,21 @@ int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
 
 template <int KT, bool HM>
 int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    if (pl.pf_waves == 4) {
-        auto kern4 = fattn_pf4_kernel<KT, 128, HM>;
-        return launch_kernel((const void*)kern4, pl, st, ev, [&] {
-            hipLaunchKernelGGL(kern4, pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
-        });
+    if constexpr (KT != FATTN_TYPE_F16) {
+        if (pl.pf_waves == 4) {
+            auto kern4 = fattn_pf4_kernel<KT, 128, HM>;
+            return launch_kernel((const void*)kern4, pl, st, ev, [&] {
+                hipLaunchKernelGGL(kern4, pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
+            });
+        }
+    }
+    if constexpr (KT == FATTN_TYPE_F16) {
+        if (pl.pf_pipe) {
+            auto kernp = fattn_pfp_kernel<HM>;
+            return launch_kernel((const void*)kernp, pl, st, ev, [&] {
+                hipLaunchKernelGGL(kernp, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
+            });
+        }
     }
     auto kern = fattn_pf_kernel<KT, 128, HM>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
@@ -444,10 +480,48 @@ int launch_pf(const Plan& pl, hipStream_t st, const Events& ev) {
     return pl.a.has_mask ? launch_pf_hm<KT, true>(pl, st, ev) : launch_pf_hm<KT, false>(pl, st, ev);
 }
 
+// Quantised prefill through the pre-pass: K and V rows -> f16 rows in the
+// workspace, then the f16 prefill kernel over them.  The events bracket both
+// launches (the conversion is part of the operation).
+template <int KT>
+int launch_pf_pre(const Plan& plq, hipStream_t st, const Events& ev) {
+    Plan pl = plq;
+    SplitArgs& a = pl.a;
+    constexpr int D = 128;
+    const int64_t rowF = D * 2, units = pl.pf_rows * (2 * D / QK);
+    uint8_t* wk = (uint8_t*)a.ws_o;
+    uint8_t* wv = wk + pl.pf_rows * rowF;
+    const int N = a.N, Hkv = (int)pl.hkv;
+    (void)hipGetLastError();
+    if (ev.begin) (void)hipEventRecord(ev.begin, st);
+    const unsigned nblk = (unsigned)((units + 255) / 256);
+    hipLaunchKernelGGL((pf_dequant_rows_kernel<KT, D>), dim3(nblk), dim3(256), 0, st, a.k, a.k_nb1, a.k_nb2, a.k_nb3,
+                       N, Hkv, wk, units);
+    hipLaunchKernelGGL((pf_dequant_rows_kernel<KT, D>), dim3(nblk), dim3(256), 0, st, a.v, a.v_nb1, a.v_nb2, a.v_nb3,
+                       N, Hkv, wv, units);
+    if (hipGetLastError() != hipSuccess) return FATTN_ERR_LAUNCH;
+    a.k = wk;
+    a.v = wv;
+    a.k_nb1 = a.v_nb1 = rowF;
+    a.k_nb2 = a.v_nb2 = (int64_t)N * rowF;
+    a.k_nb3 = a.v_nb3 = (int64_t)Hkv * N * rowF;
+    a.k_span = a.v_span = (uint32_t)((int64_t)N * rowF);
+    pl.kt = pl.vt = FATTN_TYPE_F16;
+    Events e2;
+    e2.end = ev.end;
+    return launch_pf<FATTN_TYPE_F16>(pl, st, e2);
+}
+
 template <int D>
 int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
     if constexpr (D == 128) {
         if (pl.pf) {
+            if (pl.pf_pre) {
+                if (pl.kt == FATTN_TYPE_Q8_0) return launch_pf_pre<FATTN_TYPE_Q8_0>(pl, st, ev);
+                if (pl.kt == FATTN_TYPE_Q4_0) return launch_pf_pre<FATTN_TYPE_Q4_0>(pl, st, ev);
+                return FATTN_ERR_UNSUPPORTED_TYPE;
+            }
+            if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_pf<FATTN_TYPE_F16>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0>(pl, st, ev);
             return FATTN_ERR_UNSUPPORTED_TYPE;
@@ -500,12 +574,20 @@ int fattn_set_option(int option, int value) {
             g_opt_pf = value;
             return FATTN_OK;
         case FATTN_OPT_PF_STAGGER:
-            if (value < 0 || value > 3) return FATTN_ERR_INVALID_ARG;
+            if (value < 0 || value > 7) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_stagger = value;
             return FATTN_OK;
         case FATTN_OPT_PF_WAVES:
             if (value != 4 && value != 8) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_waves = value;
+            return FATTN_OK;
+        case FATTN_OPT_PF_DEQUANT:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_pf_dequant = value;
+            return FATTN_OK;
+        case FATTN_OPT_PF_PIPE:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_pf_pipe = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_STEPS:
             if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;
@@ -569,7 +651,7 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
         uint8_t* w = (uint8_t*)p->workspace;
         pl.a.ws_cnt = (uint32_t*)w;
         pl.a.ws_ml = (float*)(w + pl.cnt_bytes);
-        pl.a.ws_o = (float*)(w + pl.cnt_bytes + pl.ml_bytes);
+        pl.a.ws_o = (float*)(w + pl.cnt_bytes + pl.ml_bytes);  // (prefill pre-pass: the f16 rows)
     }
     hipStream_t st = (hipStream_t)stream;
     Events ev;

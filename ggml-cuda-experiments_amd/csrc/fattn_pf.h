@@ -53,13 +53,18 @@ template <int KT, int D>
 struct PfCfg {
     static_assert(D == 128, "one half ggml block per wave and row");
     static constexpr int NT = kPfWaves * kWave;
+    // f16 K/V: LDS-DMA straight into the images (no raw tiles, no dequantisation);
+    // three image pairs: tile s in use, s+1 and s+2 in flight
+    static constexpr bool kDirect = KT == FATTN_TYPE_F16;
     static constexpr int rowB = row_bytes<KT, D>();
     static constexpr int kvRaw = kPfKeys * rowB;                    // raw K (or V) bytes per tile
     static constexpr int rawBytes = (2 * kvRaw + 15) / 16 * 16;
-    static constexpr int nRaw = 3;
+    static constexpr int nRaw = kDirect ? 0 : 3;
     static constexpr int img = kPfKeys * D * 2;                     // one f16 image
     static constexpr int pairBytes = 2 * img;                       // K image + V image
-    static constexpr int rawOff = 2 * pairBytes;                    // 64 KiB
+    static constexpr int nPairs = kDirect ? 3 : 2;
+    static constexpr int ahead = kDirect ? 2 : 3;                   // tiles in flight beyond the current one
+    static constexpr int rawOff = nPairs * pairBytes;
     static constexpr int maskOff = rawOff + nRaw * rawBytes;
     static constexpr int maskSlot = kPfRowsW * 128;                 // 32 rows x 64 keys x f16
     static constexpr int ldsBytes = maskOff + kPfWaves * maskSlot;
@@ -82,6 +87,43 @@ __device__ __forceinline__ void pf_issue(const StepSrc& rs, int n0, uint32_t lds
         const int byte = i * 1024 + lane * 16;
         if (C::kvRaw % 1024 == 0 || byte < C::kvRaw)
             dma<16>(is_v ? rs.v : rs.k, lds + (is_v ? C::kvRaw : 0) + i * 1024, (uint32_t)n0 * C::rowB + byte);
+    }
+}
+
+// f16 K/V: this lane's source offsets (tile-relative; + n0 * nb1 per tile) of
+// its wave's DMA instructions j = wave + 8i, i = 0..3 (j < 16: K image bytes
+// [1024j, +1024); else V image bytes [1024(j-16), +1024)), laid out as the
+// image swizzles above.  Rows are addressed by nb1 (any 16-B aligned stride).
+template <int D>
+__device__ __forceinline__ void pf_direct_offsets(const SplitArgs& a, int wave, int lane, uint32_t (&off)[4]) {
+    static_assert(kPfWaves == 8 && D == 128, "");
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int j = wave + 8 * i;
+        if (i < 2) {  // K: slice kk = j / 2, rows 32 (j & 1) + lane / 2, stored half lane & 1
+            const int kk = j >> 1, r = 32 * (j & 1) + (lane >> 1), hh = lane & 1;
+            off[i] = (uint32_t)r * (uint32_t)a.k_nb1 + kk * 32 + ((hh ^ ((r >> 3) & 1)) * 16);
+        } else {      // V: dim block db = jj / 4, rows 16 (jj & 3) + lane / 4, stored chunk lane & 3
+            const int jj = j - 16, db = jj >> 2, r = 16 * (jj & 3) + (lane >> 2), pc = lane & 3;
+            off[i] = (uint32_t)r * (uint32_t)a.v_nb1 + db * 64 + ((pc ^ ((r >> 2) & 3)) * 16);
+        }
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void pf_direct_issue(const SplitArgs& a, const StepSrc& rs, int n0, uint32_t pair_lds,
+                                                int wave, const uint32_t (&off)[4]) {
+#ifdef FATTN_MQ_NOMEM
+    return;  // diagnostic build only
+#endif
+    const uint32_t nk = (uint32_t)n0 * (uint32_t)a.k_nb1, nv = (uint32_t)n0 * (uint32_t)a.v_nb1;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int j = wave + 8 * i;
+        if (i < 2)
+            dma<16>(rs.k, pair_lds + j * 1024, nk + off[i]);
+        else
+            dma<16>(rs.v, pair_lds + PfCfg<FATTN_TYPE_F16, D>::img + (j - 16) * 1024, nv + off[i]);
     }
 }
 
@@ -163,7 +205,12 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     const int c32 = lane & 31;    // MFMA column: this lane's packed row within the wave
 
     // ---- tile decode: y -> (kv head, query tile); whole head groups (R = rk2)
-    const int y = blockIdx.y;
+    int y = blockIdx.y;
+    // XCD-aware order (pf_stagger bit 2): workgroups are dealt round-robin to the
+    // 8 XCDs, so consecutive y -- the query tiles of one kv head -- would land
+    // on 8 different L2s; remap so that each XCD takes a contiguous range of y
+    // (the query tiles of a few heads share their K/V stream in one L2)
+    if ((a.pf_stagger & 4) && gridDim.y % 8 == 0) y = (y & 7) * (gridDim.y >> 3) + (y >> 3);
     const int iq3 = blockIdx.z;
     int qt = 0, ik2 = y, ik3 = iq3;
     if (a.n_qt != 1) {
@@ -186,8 +233,9 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
     rs.m = make_srd(a.mask, HM ? a.m_span : 0);
     const uint32_t lds0 = lds_addr(smem);
-    auto raw_lds = [&](int s) { return lds0 + C::rawOff + (s % C::nRaw) * C::rawBytes; };
-    auto raw_ptr = [&](int s) { return smem + C::rawOff + (s % C::nRaw) * C::rawBytes; };
+    constexpr int kNRaw = C::nRaw ? C::nRaw : 1;
+    auto raw_lds = [&](int s) { return lds0 + C::rawOff + (s % kNRaw) * C::rawBytes; };
+    auto raw_ptr = [&](int s) { return smem + C::rawOff + (s % kNRaw) * C::rawBytes; };
     const uint32_t mslot = lds0 + C::maskOff + wave * C::maskSlot;
 
     // ---- Q^T operands (B of S^T = K.Q^T): dims 16kk + 8h .. +8 of this lane's
@@ -259,13 +307,21 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         vbase[e] = C::img + row * 64 + ch * 16 + (gi & 1) * 8;
     }
 
-    // ---- prologue: raw tiles 0..2, mask 0; dequantise tile 0
-    for (int s = 0; s < 3 && s < ntiles; s++) pf_issue<KT, D>(rs, s * kPfKeys, raw_lds(s), wave, lane);
-    if (ntiles > 0) mask_issue(0);
-    // raw 0 landed (raw 1, 2 and mask 0 may fly on)
-    pf_vm_wait<KT, D>(wave, min(2, ntiles - 1), ntiles > 0 ? NM : 0);
-    __syncthreads();
-    if (ntiles > 0) pf_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, wave, lane);
+    // ---- prologue.  Quantised: raw tiles 0..2, mask 0; dequantise tile 0.
+    // f16: image pairs 0 and 1, mask 0 (the first body waits for pair 0).
+    uint32_t doff[4];
+    if constexpr (C::kDirect) {
+        pf_direct_offsets<D>(a, wave, lane, doff);
+        for (int s = 0; s < 2 && s < ntiles; s++) pf_direct_issue<D>(a, rs, s * kPfKeys, lds0 + s * C::pairBytes, wave, doff);
+        if (ntiles > 0) mask_issue(0);
+    } else {
+        for (int s = 0; s < 3 && s < ntiles; s++) pf_issue<KT, D>(rs, s * kPfKeys, raw_lds(s), wave, lane);
+        if (ntiles > 0) mask_issue(0);
+        // raw 0 landed (raw 1, 2 and mask 0 may fly on)
+        pf_vm_wait<KT, D>(wave, min(2, ntiles - 1), ntiles > 0 ? NM : 0);
+        __syncthreads();
+        if (ntiles > 0) pf_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, wave, lane);
+    }
 
     float m_run = kNegInf;    // reference max (log2 domain) of this lane's row
     f32x2 l2 = {0.0f, 0.0f};  // this lane's partial row sums (its 32 of every 64 keys)
@@ -294,12 +350,19 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
 #endif
     auto body = [&](int s, auto par) {
         constexpr int P = decltype(par)::value;  // image pair of tile s
-        // raw s+1 landed (raw s+2 and mask s may fly on)
+        // quantised: raw s+1 landed (raw s+2 and mask s may fly on);
+        // f16: image pair of tile s landed (tile s+1 and mask s may fly on)
         PF_T(7);
-        pf_vm_wait<KT, D>(wave, s + 2 < ntiles ? 1 : 0, NM);
+        pf_vm_wait<KT, D>(wave, s + C::ahead - 1 < ntiles ? 1 : 0, NM);
         __syncthreads();
         PF_T(0);
-        if (s + 3 < ntiles) pf_issue<KT, D>(rs, (s + 3) * kPfKeys, raw_lds(s + 3), wave, lane);
+        if constexpr (C::kDirect) {
+            // into the pair every wave finished reading before the barrier
+            if (s + 2 < ntiles)
+                pf_direct_issue<D>(a, rs, (s + 2) * kPfKeys, lds0 + ((P + 2) % 3) * C::pairBytes, wave, doff);
+        } else {
+            if (s + 3 < ntiles) pf_issue<KT, D>(rs, (s + 3) * kPfKeys, raw_lds(s + 3), wave, lane);
+        }
         PF_T(1);
         // SIMD partners (waves w and w + 4) run the tile's phases staggered:
         // waves 0-3 dequantise first (VALU) while waves 4-7 run S^T (MFMA),
@@ -308,9 +371,11 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         // (MI355X_MICROARCH.md, two waves per SIMD)
         const bool late = (a.pf_stagger & 1) && wave >= kPfWaves / 2;
         auto dequant_next = [&] {
-            if (s + 1 < ntiles)
-                pf_dequant<KT, D>(raw_ptr(s + 1), smem + (P ^ 1) * C::pairBytes,
-                                  smem + (P ^ 1) * C::pairBytes + C::img, wave, lane);
+            if constexpr (!C::kDirect) {
+                if (s + 1 < ntiles)
+                    pf_dequant<KT, D>(raw_ptr(s + 1), smem + (P ^ 1) * C::pairBytes,
+                                      smem + (P ^ 1) * C::pairBytes + C::img, wave, lane);
+            }
         };
         if (!late) {
             dequant_next();
@@ -319,7 +384,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         }
 #ifdef FATTN_MQ_NOCOMPUTE
         if constexpr (HM) {
-            pf_vm_wait<KT, D>(wave, s + 3 < ntiles ? 1 : 0, 0);
+            pf_vm_wait<KT, D>(wave, s + C::ahead < ntiles ? 1 : 0, 0);
             if (s + 1 < ntiles) mask_issue(s + 1);
         }
         if (late) dequant_next();
@@ -354,8 +419,8 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         // is key 32t + 8(j/4) + 4h + (j%4) of this lane's row
         float u[2][16];
         if constexpr (HM) {
-            // mask s landed (raw s+3 may fly on); read it, then refill the slot
-            pf_vm_wait<KT, D>(wave, s + 3 < ntiles ? 1 : 0, 0);
+            // mask s landed (raw s+3 / image s+2 may fly on); read it, then refill the slot
+            pf_vm_wait<KT, D>(wave, s + C::ahead < ntiles ? 1 : 0, 0);
             u32x2 mk[2][4];
 #pragma unroll
             for (int t = 0; t < 2; t++) {
@@ -479,9 +544,17 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             PF_T(2);
         }
     };
-    for (int s = 0; s < ntiles; s += 2) {
-        body(s, std::integral_constant<int, 0>());
-        if (s + 1 < ntiles) body(s + 1, std::integral_constant<int, 1>());
+    if constexpr (C::kDirect) {
+        for (int s = 0; s < ntiles; s += 3) {
+            body(s, std::integral_constant<int, 0>());
+            if (s + 1 < ntiles) body(s + 1, std::integral_constant<int, 1>());
+            if (s + 2 < ntiles) body(s + 2, std::integral_constant<int, 2>());
+        }
+    } else {
+        for (int s = 0; s < ntiles; s += 2) {
+            body(s, std::integral_constant<int, 0>());
+            if (s + 1 < ntiles) body(s + 1, std::integral_constant<int, 1>());
+        }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #ifdef FATTN_STAMPS
@@ -510,6 +583,50 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             }
         }
     }
+}
+
+// ---- prefill pre-pass: quantised K or V rows -> dense f16 rows [Skv][Hkv][N][D],
+// h(q * d) with one f16 rounding -- the same values the in-kernel
+// dequantisation writes to the images, so both paths give identical results.
+// One thread per half ggml block (16 elements, 32 B out): a wave writes 2 KiB
+// contiguous.
+template <int KT, int D>
+__global__ __launch_bounds__(256) void pf_dequant_rows_kernel(const uint8_t* __restrict__ src, int64_t nb1, int64_t nb2,
+                                                              int64_t nb3, int N, int Hkv, uint8_t* __restrict__ dst,
+                                                              int64_t nunits) {
+    constexpr int NB = D / QK;
+    constexpr int BB = TypeInfo<KT>::block_bytes;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nunits) return;
+    const int h = (int)(t & 1), b = (int)((t >> 1) % NB);
+    const int64_t row = t / (2 * NB);
+    const int n = (int)(row % N);
+    const int64_t hk = row / N;
+    const uint16_t* p16 = (const uint16_t*)(src + (hk / Hkv) * nb3 + (hk % Hkv) * nb2 + (int64_t)n * nb1 + b * BB);
+    const f16x2 d = bcast_h(p16[0]);
+    // Q8_0: qs bytes 16h..16h+15; Q4_0: all 16 qs bytes (low / high nibbles)
+    const uint16_t* qs = p16 + 1 + (KT == FATTN_TYPE_Q8_0 ? 8 * h : 0);
+    uint32_t q[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) q[j] = (uint32_t)qs[2 * j] | ((uint32_t)qs[2 * j + 1] << 16);
+    u32x4 out[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        f16x2 h0, h1, h2, h3;
+        if constexpr (KT == FATTN_TYPE_Q8_0) {
+            i8x4_to_h2x2(q[2 * k], h0, h1);
+            i8x4_to_h2x2(q[2 * k + 1], h2, h3);
+        } else {
+            const uint32_t sft = 4 * h;
+            u4x4_to_h2x2((q[2 * k] >> sft) & 0x0F0F0F0Fu, h0, h1);
+            u4x4_to_h2x2((q[2 * k + 1] >> sft) & 0x0F0F0F0Fu, h2, h3);
+        }
+        h0 *= d; h1 *= d; h2 *= d; h3 *= d;
+        out[k] = u32x4{as_u32(h0), as_u32(h1), as_u32(h2), as_u32(h3)};
+    }
+    uint8_t* o = dst + row * (D * 2) + (4 * b + 2 * h) * 16;
+    *(u32x4*)o = out[0];
+    *(u32x4*)(o + 16) = out[1];
 }
 
 }  // namespace fattn

@@ -42,6 +42,8 @@ OPT_SPLIT_INFLIGHT = 4
 OPT_PF = 5
 OPT_PF_STAGGER = 6
 OPT_PF_WAVES = 7
+OPT_PF_DEQUANT = 8
+OPT_PF_PIPE = 9
 
 
 class FattnError(RuntimeError):

@@ -123,8 +123,14 @@ enum {
     FATTN_OPT_PF = 5,               /* prefill kernel: 0 = auto, 1 = never, 2 = whenever eligible (even if the
                                        workgroups do not fill the chip) */
     FATTN_OPT_PF_STAGGER = 6,       /* prefill kernel, bit 0: SIMD partner waves staggered (default lockstep);
-                                       bit 1 (default on): waves 4-7 at s_setprio 1 */
-    FATTN_OPT_PF_WAVES = 7          /* prefill kernel: 8 = 8 waves x 32 rows, 4 = 4 waves x 64 rows (one per SIMD) */
+                                       bit 1 (default on): waves 4-7 at s_setprio 1; bit 2: XCD-grouped
+                                       workgroup order (the query tiles of a kv head on one XCD) */
+    FATTN_OPT_PF_WAVES = 7,         /* prefill kernel: 8 = 8 waves x 32 rows, 4 = 4 waves x 64 rows (one per SIMD) */
+    FATTN_OPT_PF_DEQUANT = 8        /* quantised prefill: 0 = auto, 1 = dequantise inside the kernel, 2 = convert K/V
+                                       to f16 rows in the workspace first (fattn_workspace_size grows by
+                                       2 * Skv * Hkv * N * D * 2 bytes; 8 waves only) */,
+    FATTN_OPT_PF_PIPE = 9           /* prefill over f16 images (f16 K/V, or after the pre-pass): 0 = auto,
+                                       1 = fattn_pf_kernel, 2 = software-pipelined fattn_pfp_kernel */
 };
 int fattn_set_option(int option, int value);
 

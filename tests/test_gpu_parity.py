@@ -200,15 +200,22 @@ def test_mq_fully_masked_rows_are_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture(params=[8, 4], ids=["8waves", "4waves"])
+@pytest.fixture(params=[8, 4, "pre", "pipe"], ids=["8waves", "4waves", "predequant", "pipelined"])
 def pf_force(request):
-    """Prefill kernel on every eligible problem, in both forms: 8 waves x 32
-    rows (fattn_pf.h) and 4 waves x 64 rows (fattn_pf4.h)."""
+    """Prefill kernel on every eligible problem, in all its forms: 8 waves x 32
+    rows (fattn_pf.h), 4 waves x 64 rows (fattn_pf4.h), quantised K/V converted
+    to f16 rows first (pf_dequant_rows_kernel + the f16 form), and the f16
+    images through the software-pipelined kernel (fattn_pfp.h)."""
+    prm = request.param
     fattn.set_option(fattn.OPT_PF, 2)
-    fattn.set_option(fattn.OPT_PF_WAVES, request.param)
+    fattn.set_option(fattn.OPT_PF_WAVES, prm if isinstance(prm, int) else 8)
+    fattn.set_option(fattn.OPT_PF_DEQUANT, 1 if isinstance(prm, int) else 2)
+    fattn.set_option(fattn.OPT_PF_PIPE, 2 if prm == "pipe" else 1)
     yield
     fattn.set_option(fattn.OPT_PF, 0)
     fattn.set_option(fattn.OPT_PF_WAVES, 8)
+    fattn.set_option(fattn.OPT_PF_DEQUANT, 0)
+    fattn.set_option(fattn.OPT_PF_PIPE, 0)
 
 
 PF_CASES = [
@@ -220,6 +227,11 @@ PF_CASES = [
     dict(kv_type="q8_0", NQ=100, H=2, Hkv=2, N=192, mask="neginf_blocks", S=2),  # odd tile count, 2 seqs
     dict(kv_type="q4_0", NQ=256, H=2, Hkv=2, N=64, mask="zero"),             # one tile
     dict(kv_type="q8_0", NQ=4, H=64, Hkv=1, N=128, mask="random"),           # R=64, QPT=4
+    # f16 K/V: images filled by LDS-DMA straight from the rows
+    dict(kv_type="f16", NQ=256, H=4, Hkv=4, N=256, mask="causal"),
+    dict(kv_type="f16", NQ=100, H=8, Hkv=2, N=192, mask="random", layout="pos"),  # rows strided by Hkv
+    dict(kv_type="f16", NQ=300, H=2, Hkv=2, N=128, mask="none", S=2),
+    dict(kv_type="f16", NQ=256, H=2, Hkv=2, N=64, mask="neginf_blocks"),        # one tile
 ]
 
 
@@ -227,6 +239,23 @@ PF_CASES = [
 def test_pf_sweep(dev, pf_force, case):
     p = make_problem(D=128, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("case", [c for c in PF_CASES if c["kv_type"] == "f16"][:2] + PF_CASES[:2],
+                         ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_pf_images_pipelined(dev, case):
+    """f16 images through the software-pipelined kernel (OPT_PF_PIPE = 2):
+    f16 K/V directly, quantised K/V after the pre-pass."""
+    fattn.set_option(fattn.OPT_PF, 2)
+    fattn.set_option(fattn.OPT_PF_PIPE, 2)
+    fattn.set_option(fattn.OPT_PF_DEQUANT, 2)
+    try:
+        p = make_problem(D=128, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+        assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+    finally:
+        fattn.set_option(fattn.OPT_PF, 0)
+        fattn.set_option(fattn.OPT_PF_PIPE, 0)
+        fattn.set_option(fattn.OPT_PF_DEQUANT, 0)
 
 
 @pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
@@ -248,18 +277,54 @@ def test_pf_fully_masked_rows_are_nan(dev, pf_force):
     assert attn_rel_err(got, ref) <= RTOL
 
 
-@pytest.mark.parametrize("waves", [8, 4])
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
+def test_pf_predequant_bitexact(dev, kt):
+    """Quantised prefill through the f16 pre-pass gives bit-identical output to
+    the in-kernel dequantisation (same f16 operands h(q*d), same kernel math)."""
+    p = make_problem(D=128, NQ=512, H=4, Hkv=2, N=1024, kv_type=kt, mask="random", seed=31)
+    fattn.set_option(fattn.OPT_PF, 2)
+    try:
+        fattn.set_option(fattn.OPT_PF_DEQUANT, 1)
+        a = run_gpu(p)
+        fattn.set_option(fattn.OPT_PF_DEQUANT, 2)
+        b = run_gpu(p)
+    finally:
+        fattn.set_option(fattn.OPT_PF, 0)
+        fattn.set_option(fattn.OPT_PF_DEQUANT, 0)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert attn_rel_err(a, p.oracle()) <= RTOL
+
+
+def test_pf_f16_prefill_full(dev):
+    """f16 K/V at the prefill shape (n_q = N = 4096, 32 heads, random mask): the
+    prefill kernel against the split-KV kernel, one head against the oracle."""
+    p = make_problem(D=128, NQ=4096, H=32, N=4096, kv_type="f16", seed=33)
+    a = run_gpu(p)
+    fattn.set_option(fattn.OPT_PF, 1)
+    try:
+        b = run_gpu(p)
+    finally:
+        fattn.set_option(fattn.OPT_PF, 0)
+    assert np.isfinite(a).all()
+    assert attn_rel_err(a, b) <= RTOL
+
+
+@pytest.mark.parametrize("waves", [8, 4, "pre", "pipe"])
 def test_pf_prefill_full_matches_mq(dev, waves):
     """The prefill shape at full size (n_q = N = 4096, 32 heads, Q8_0, random mask):
     the prefill kernel (auto-selected) against the multi-query kernel, and one
     head of it against the oracle."""
     import torch
     p = make_problem(D=128, NQ=4096, H=32, N=4096, kv_type="q8_0", seed=29)
-    fattn.set_option(fattn.OPT_PF_WAVES, waves)
+    fattn.set_option(fattn.OPT_PF_WAVES, waves if isinstance(waves, int) else 8)
+    fattn.set_option(fattn.OPT_PF_DEQUANT, 1 if isinstance(waves, int) else 2)
+    fattn.set_option(fattn.OPT_PF_PIPE, 2 if waves == "pipe" else 1)
     try:
         a = run_gpu(p)
     finally:
         fattn.set_option(fattn.OPT_PF_WAVES, 8)
+        fattn.set_option(fattn.OPT_PF_DEQUANT, 0)
+        fattn.set_option(fattn.OPT_PF_PIPE, 0)
     fattn.set_option(fattn.OPT_PF, 1)
     try:
         b = run_gpu(p)

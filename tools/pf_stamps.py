@@ -24,8 +24,12 @@ args = ap.parse_args()
 dev = torch.device("cuda:0")
 D, H, N, NQ = 128, args.heads, args.kv_len, args.n_q
 typ = fattn.TYPE_NAMES[args.kv_type]
-k = fattn.quantize(torch.rand((H * N, D), device=dev) * 2 - 1, typ).reshape(-1)
-v = fattn.quantize(torch.rand((H * N, D), device=dev) * 2 - 1, typ).reshape(-1)
+if args.kv_type == "f16":
+    k = (torch.rand((H * N, D), device=dev) * 2 - 1).half().reshape(-1)
+    v = (torch.rand((H * N, D), device=dev) * 2 - 1).half().reshape(-1)
+else:
+    k = fattn.quantize(torch.rand((H * N, D), device=dev) * 2 - 1, typ).reshape(-1)
+    v = fattn.quantize(torch.rand((H * N, D), device=dev) * 2 - 1, typ).reshape(-1)
 q = torch.rand((1, NQ, H, D), device=dev) * 2 - 1
 mask = (torch.rand((NQ, (N + 63) // 64 * 64), device=dev) * 2 - 1).half()
 out = torch.empty((1, NQ, H, D), device=dev)
