@@ -131,3 +131,22 @@ tests-hip: tests/_build/libprims.so
 tests/_build/libprims.so: tests/hip/prims.hip $(CHDR)
 	@mkdir -p tests/_build
 	$(HIPCC) $(HIPFLAGS) -shared tests/hip/prims.hip -o $@
+
+# pipelined prefill schedule variants (tools/gpu_pfp.sh); diagnostic only
+pfpvar: $(LIBDIR)/libfattn_pfp_nosgb.so $(LIBDIR)/libfattn_pfp_a4b3.so $(LIBDIR)/libfattn_pfp_a9b6.so \
+        $(LIBDIR)/libfattn_pfp_r4r8.so $(LIBDIR)/libfattn_pfp_r8r16.so
+
+$(LIBDIR)/libfattn_pfp_nosgb.so: $(CSRC) $(CHDR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_PFP_NO_SGB -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_pfp_a4b3.so: $(CSRC) $(CHDR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_PFP_FILL_A=4 -DFATTN_PFP_FILL_B=3 -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_pfp_a9b6.so: $(CSRC) $(CHDR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_PFP_FILL_A=9 -DFATTN_PFP_FILL_B=6 -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_pfp_r4r8.so: $(CSRC) $(CHDR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_PFP_AHEAD_A=4 -DFATTN_PFP_AHEAD_B=8 -shared $(CSRC) -o $@
+
+$(LIBDIR)/libfattn_pfp_r8r16.so: $(CSRC) $(CHDR)
+	$(HIPCC) $(HIPFLAGS) -DFATTN_PFP_AHEAD_A=8 -DFATTN_PFP_AHEAD_B=16 -shared $(CSRC) -o $@

@@ -39,6 +39,12 @@ struct PfpCfg {
 #ifndef FATTN_PFP_FILL_A
 #define FATTN_PFP_FILL_A 6   // VALU fillers placed per S^T MFMA (phase A)
 #endif
+#ifndef FATTN_PFP_AHEAD_A
+#define FATTN_PFP_AHEAD_A 2  // K reads placed before the first S^T MFMA (then 1 per MFMA)
+#endif
+#ifndef FATTN_PFP_AHEAD_B
+#define FATTN_PFP_AHEAD_B 4  // V^T reads placed before the first O^T MFMA (then 2 per MFMA)
+#endif
 #ifndef FATTN_PFP_FILL_B
 #define FATTN_PFP_FILL_B 4   // VALU fillers placed per O^T MFMA (phase B)
 #endif
@@ -130,13 +136,9 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pfp_kernel(const Spl
             }
         }
     };
-    uint32_t maddr[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; t++) {
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            maddr[t][u] = PC::maskOff + wave * C::maskSlot + (c32 * 8 + ((4 * t + u) ^ ((c32 >> 1) & 7))) * 16 + 8 * h;
-    }
+    // this lane's mask piece pc = 4t + u of row c32 sits at mrow + ((pc ^ msw) * 16)
+    const uint32_t mrow = PC::maskOff + wave * C::maskSlot + c32 * 128 + 8 * h;
+    const uint32_t msw = ((c32 >> 1) & 7) * 16;
     const uint32_t kbase = c32 * 32 + ((h ^ ((c32 >> 3) & 1)) * 16);
     const int gi = lane & 15, dh = (lane >> 4) & 1;
     uint32_t vbase[2];
@@ -162,57 +164,52 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pfp_kernel(const Spl
 #pragma unroll
         for (int j = 0; j < 16; j++) o[db][j] = 0.0f;
     }
-    float u[2][16];  // scores of the tile whose softmax is half done
+    // The pipeline runs over 32-key subtiles j = 2s + t of the 64-key tiles s
+    // (half the live score / P state of whole tiles: no spills).
+    float u[16];     // scores of the subtile whose softmax is half done
+    u32x2 mk1[4];    // mask pieces of the odd subtile of the current tile
 
-    // -- S^T of one tile from image `img` (K operands of a subtile read ahead of its chain)
-    auto s_tile = [&](const uint8_t* img, f32x16 (&st)[2]) {
+    // -- S^T of subtile t of the tile in image `img`
+    auto s_sub = [&](const uint8_t* img, int t, f32x16& st) {
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
-            f16x8 ka[NK];
+        for (int j = 0; j < 16; j++) st[j] = 0.0f;
 #pragma unroll
-            for (int kk = 0; kk < NK; kk++) ka[kk] = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024);
-#pragma unroll
-            for (int j = 0; j < 16; j++) st[t][j] = 0.0f;
-#pragma unroll
-            for (int kk = 0; kk < NK; kk++) st[t] = mfma32(ka[kk], qop[kk], st[t]);
-        }
+        for (int kk = 0; kk < NK; kk++)
+            st = mfma32(*(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024), qop[kk], st);
     };
-    // -- start softmax of a tile: mask, scores, row max, deferred rescale
-    //    (mask slot: this wave's; `s` = the tile, its mask landed)
-    auto sm_start = [&](int s, const f32x16 (&st)[2]) {
+    // -- read both subtiles' mask pieces of a tile (landed), then refill the
+    //    slot with the next tile's mask
+    auto sm_mask = [&](int s, u32x2 (&mk0)[4]) {
         if constexpr (HM) {
-            u32x2 mk[2][4];
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
+            for (int uu = 0; uu < 4; uu++) mk0[uu] = *(const u32x2*)(smem + mrow + ((uu * 16) ^ msw));
 #pragma unroll
-                for (int uu = 0; uu < 4; uu++) mk[t][uu] = *(const u32x2*)(smem + maddr[t][uu]);
-            }
+            for (int uu = 0; uu < 4; uu++) mk1[uu] = *(const u32x2*)(smem + mrow + (((4 + uu) * 16) ^ msw));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (s + 1 < ntiles) mask_issue(s + 1);
+        }
+    };
+    // -- scores u = scale s + mask and their max (element j: key 8(j/4) + 4h + j%4)
+    auto sm_scores = [&](const f32x16& st, const u32x2 (&mk)[4]) {
+        if constexpr (HM) {
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
-#pragma unroll
-                for (int uu = 0; uu < 4; uu++) {
-                    const f16x2 m01 = as_h2(mk[t][uu].x), m23 = as_h2(mk[t][uu].y);
-                    u[t][4 * uu + 0] = fmaf(st[t][4 * uu + 0], scale, (float)m01.x);
-                    u[t][4 * uu + 1] = fmaf(st[t][4 * uu + 1], scale, (float)m01.y);
-                    u[t][4 * uu + 2] = fmaf(st[t][4 * uu + 2], scale, (float)m23.x);
-                    u[t][4 * uu + 3] = fmaf(st[t][4 * uu + 3], scale, (float)m23.y);
-                }
+            for (int uu = 0; uu < 4; uu++) {
+                const f16x2 m01 = as_h2(mk[uu].x), m23 = as_h2(mk[uu].y);
+                u[4 * uu + 0] = fmaf(st[4 * uu + 0], scale, (float)m01.x);
+                u[4 * uu + 1] = fmaf(st[4 * uu + 1], scale, (float)m01.y);
+                u[4 * uu + 2] = fmaf(st[4 * uu + 2], scale, (float)m23.x);
+                u[4 * uu + 3] = fmaf(st[4 * uu + 3], scale, (float)m23.y);
             }
         } else {
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
-#pragma unroll
-                for (int j = 0; j < 16; j++) u[t][j] = st[t][j];
-            }
+            for (int j = 0; j < 16; j++) u[j] = st[j];
         }
         float tmax = kNegInf;
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) tmax = fmaxf(tmax, u[t][j]);
-        }
+        for (int j = 0; j < 16; j++) tmax = fmaxf(tmax, u[j]);
+        return tmax;
+    };
+    auto sm_rescale = [&](float tmax) {
         tmax = xor32_pair(tmax, true) * c;
         if (__builtin_amdgcn_ballot_w64(tmax > m_run + kDeferLog2)) {
             const float m_new = fmaxf(m_run, tmax);
@@ -224,102 +221,128 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pfp_kernel(const Spl
         }
         nm = (m_run == kNegInf) ? 0.0f : -m_run;
     };
-    // -- finish softmax of the started tile: P (f16, MFMA B layout) and row sums
-    auto sm_finish = [&](f16x8 (&pb)[2][2]) {
+    // -- finish softmax of the started subtile: P (f16, two 16-key k-steps) and row sums
+    auto sm_finish = [&](f16x8 (&pb)[2]) {
+        float pv[16];
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
-            float pv[16];
+        for (int j = 0; j < 16; j++) pv[j] = __builtin_amdgcn_exp2f(fmaf(u[j], c, nm));
 #pragma unroll
-            for (int j = 0; j < 16; j++) pv[j] = __builtin_amdgcn_exp2f(fmaf(u[t][j], c, nm));
+        for (int j = 0; j < 16; j += 2) l2 += f32x2{pv[j], pv[j + 1]};
 #pragma unroll
-            for (int j = 0; j < 16; j += 2) l2 += f32x2{pv[j], pv[j + 1]};
-#pragma unroll
-            for (int q = 0; q < 2; q++) {
-                f16x8 x;
-                x.s0 = (f16)pv[8 * q]; x.s1 = (f16)pv[8 * q + 1]; x.s2 = (f16)pv[8 * q + 2]; x.s3 = (f16)pv[8 * q + 3];
-                x.s4 = (f16)pv[8 * q + 4]; x.s5 = (f16)pv[8 * q + 5]; x.s6 = (f16)pv[8 * q + 6]; x.s7 = (f16)pv[8 * q + 7];
-                pb[t][q] = x;
-            }
+        for (int q = 0; q < 2; q++) {
+            f16x8 x;
+            x.s0 = (f16)pv[8 * q]; x.s1 = (f16)pv[8 * q + 1]; x.s2 = (f16)pv[8 * q + 2]; x.s3 = (f16)pv[8 * q + 3];
+            x.s4 = (f16)pv[8 * q + 4]; x.s5 = (f16)pv[8 * q + 5]; x.s6 = (f16)pv[8 * q + 6]; x.s7 = (f16)pv[8 * q + 7];
+            pb[q] = x;
         }
     };
-    // -- O^T += V^T.P^T from image `img`
-    auto o_tile = [&](const uint8_t* img, const f16x8 (&pb)[2][2]) {
+    // -- O^T += V^T.P^T for subtile t of the tile in image `img`
+    auto o_sub = [&](const uint8_t* img, int t, const f16x8 (&pb)[2]) {
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
+        for (int q = 0; q < 2; q++) {
+            typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+            u32x4 va[NDB];
 #pragma unroll
-            for (int q = 0; q < 2; q++) {
-                typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-                u32x4 va[NDB];
-#pragma unroll
-                for (int db = 0; db < NDB; db++) {
-                    const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
-                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[0] + off));
-                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[1] + off));
-                    const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
-                    va[db] = u32x4{a2.x, a2.y, b2.x, b2.y};
-                }
-#pragma unroll
-                for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[t][q], o[db]);
+            for (int db = 0; db < NDB; db++) {
+                const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[0] + off));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[1] + off));
+                const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                va[db] = u32x4{a2.x, a2.y, b2.x, b2.y};
             }
+#pragma unroll
+            for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[q], o[db]);
         }
     };
-    auto interleave = [](auto nfill) {
-        constexpr int F = decltype(nfill)::value;
+    // per phase: `ahead` LDS reads first, then 8 x {MFMA, `per` LDS reads, F VALU}
+    [[maybe_unused]] auto interleave = [](auto nfill, auto ahead, auto per, auto id) {
+        constexpr int F = decltype(nfill)::value, A = decltype(ahead)::value, R = decltype(per)::value;
+        constexpr int I = decltype(id)::value;
+        __builtin_amdgcn_sched_group_barrier(0x100, A, I);
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, F, 0);  // then F VALU
+        for (int i = 0; i < 8; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, I);
+            __builtin_amdgcn_sched_group_barrier(0x100, R, I);
+            __builtin_amdgcn_sched_group_barrier(0x002, F, I);
         }
     };
 
-    // ---- prologue: image 0 and mask 0 (waited), images 1, 2 in flight; S^T(0), start softmax(0)
+    // ---- prologue: image 0 and mask 0 (waited), images 1, 2 in flight;
+    // S^T(subtile 0), start softmax(subtile 0)
     if (ntiles > 0) pf_direct_issue<D>(a, rs, 0, lds0, wave, doff);
     if (ntiles > 0) mask_issue(0);
     for (int s = 1; s < 3 && s < ntiles; s++) pf_direct_issue<D>(a, rs, s * kPfKeys, lds0 + s * C::pairBytes, wave, doff);
     pf_vm_wait<FATTN_TYPE_F16, D>(wave, min(2, max(0, ntiles - 1)), 0);
     __syncthreads();
+    const int nsub = 2 * ntiles;
     if (ntiles > 0) {
-        f32x16 st[2];
-        s_tile(smem, st);
-        sm_start(0, st);
+        f32x16 st;
+        s_sub(smem, 0, st);
+        u32x2 mk0[4];
+        sm_mask(0, mk0);
+        sm_rescale(sm_scores(st, mk0));
     }
 
-    auto body = [&](int s, auto par) {
-        constexpr int P = decltype(par)::value;  // ring slot of tile s
-        // image s+1 landed (image s+2 and mask s+1 may fly on); every wave is
-        // past tile s-1, so its slot (P + 3) % 4 takes image s+3
-        pf_vm_wait<FATTN_TYPE_F16, D>(wave, s + 2 < ntiles ? 1 : 0, s + 1 < ntiles ? NM : 0);
-        __syncthreads();
-        if (s + 3 < ntiles)
-            pf_direct_issue<D>(a, rs, (s + 3) * kPfKeys, lds0 + ((P + 3) % 4) * C::pairBytes, wave, doff);
+    auto body = [&](int j, auto par) {
+        constexpr int J = decltype(par)::value;  // j mod 8
+        constexpr int T = J & 1, P = (J >> 1) & 3;  // subtile of tile s = j / 2, its ring slot
+        constexpr int PN = ((J + 1) >> 1) & 3;      // ring slot of subtile j + 1
+        const int s = j >> 1;
+        if constexpr (T == 1) {
+            // image s+1 landed (image s+2 and mask s+1 may fly on); every wave is
+            // past tile s-1, so its slot (P + 3) % 4 takes image s+3
+            pf_vm_wait<FATTN_TYPE_F16, D>(wave, s + 2 < ntiles ? 1 : 0, s + 1 < ntiles ? NM : 0);
+            __syncthreads();
+            if (s + 3 < ntiles)
+                pf_direct_issue<D>(a, rs, (s + 3) * kPfKeys, lds0 + ((P + 3) % 4) * C::pairBytes, wave, doff);
+        }
         const uint8_t* img_s = smem + P * C::pairBytes;
-        const uint8_t* img_n = smem + ((P + 1) % 4) * C::pairBytes;
-        f16x8 pb[2][2];
-        f32x16 st[2];
-        // phase A: S^T(s+1) || finish softmax(s)
-        if (s + 1 < ntiles) {
-            s_tile(img_n, st);
+        const uint8_t* img_n = smem + PN * C::pairBytes;
+        f16x8 pb[2];
+        f32x16 st;
+        const bool more = j + 1 < nsub;
+        // phase A: S^T(j+1) || finish softmax(j)
+        if (more) {
+            s_sub(img_n, T ^ 1, st);
             sm_finish(pb);
 #ifndef FATTN_PFP_NO_SGB
-            interleave(std::integral_constant<int, FATTN_PFP_FILL_A>());
+            interleave(std::integral_constant<int, FATTN_PFP_FILL_A>(), std::integral_constant<int, FATTN_PFP_AHEAD_A>(),
+                       std::integral_constant<int, 1>(), std::integral_constant<int, 0>());
 #endif
         } else {
             sm_finish(pb);
         }
-        // phase B: O^T(s) || start softmax(s+1)
-        if (s + 1 < ntiles) {
-            if constexpr (HM) pf_vm_wait<FATTN_TYPE_F16, D>(wave, s + 3 < ntiles ? 1 : 0, 0);  // mask s+1 landed
-            o_tile(img_s, pb);
-            sm_start(s + 1, st);
+        // phase B: O^T(j) || start softmax(j+1)
+        if (more) {
+            u32x2 mk[4];
+            if constexpr (T == 1) {
+                // subtile j+1 opens tile s+1: its mask landed (image s+3 may fly on)
+                if constexpr (HM) pf_vm_wait<FATTN_TYPE_F16, D>(wave, s + 3 < ntiles ? 1 : 0, 0);
+                sm_mask(s + 1, mk);
+            } else {
+#pragma unroll
+                for (int uu = 0; uu < 4; uu++) mk[uu] = mk1[uu];
+            }
+            o_sub(img_s, T, pb);
+            const float tmax = sm_scores(st, mk);
+#ifndef FATTN_PFP_NO_SGB
+            interleave(std::integral_constant<int, FATTN_PFP_FILL_B>(), std::integral_constant<int, FATTN_PFP_AHEAD_B>(),
+                       std::integral_constant<int, 2>(), std::integral_constant<int, 1>());
+#endif
+            sm_rescale(tmax);
         } else {
-            o_tile(img_s, pb);
+            o_sub(img_s, T, pb);
         }
     };
-    for (int s = 0; s < ntiles; s += 4) {
-        body(s, std::integral_constant<int, 0>());
-        if (s + 1 < ntiles) body(s + 1, std::integral_constant<int, 1>());
-        if (s + 2 < ntiles) body(s + 2, std::integral_constant<int, 2>());
-        if (s + 3 < ntiles) body(s + 3, std::integral_constant<int, 3>());
+    for (int j = 0; j < nsub; j += 8) {
+        body(j, std::integral_constant<int, 0>());
+        if (j + 1 < nsub) body(j + 1, std::integral_constant<int, 1>());
+        if (j + 2 < nsub) body(j + 2, std::integral_constant<int, 2>());
+        if (j + 3 < nsub) body(j + 3, std::integral_constant<int, 3>());
+        if (j + 4 < nsub) body(j + 4, std::integral_constant<int, 4>());
+        if (j + 5 < nsub) body(j + 5, std::integral_constant<int, 5>());
+        if (j + 6 < nsub) body(j + 6, std::integral_constant<int, 6>());
+        if (j + 7 < nsub) body(j + 7, std::integral_constant<int, 7>());
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 

@@ -115,6 +115,18 @@ __device__ __forceinline__ void wait_steps(int outstanding) {
     }
 }
 
+// wait until at most `outstanding` whole steps plus EXTRA instructions remain
+// (EXTRA = the V part of the oldest pending step: its K and mask have landed)
+template <int NI, int EXTRA>
+__device__ __forceinline__ void wait_steps_plus(int outstanding) {
+    switch (__builtin_amdgcn_readfirstlane(outstanding)) {
+        case 0: wait_vmcnt_c<EXTRA>(); break;
+        case 1: wait_vmcnt_c<NI + EXTRA>(); break;
+        case 2: wait_vmcnt_c<2 * NI + EXTRA>(); break;
+        default: wait_vmcnt_c<3 * NI + EXTRA>(); break;
+    }
+}
+
 // ---------------------------------------------------------------- HBM -> LDS
 template <int KT, int VT, int D, int GRAN>
 struct StepPlan {
@@ -174,6 +186,14 @@ __device__ __forceinline__ u32x4 ld_sc1_buf(const i32x4& srd, uint32_t off) {
 // consumer waits with an explicit vmcnt.
 // NT: non-temporal policy for bytes one CU reads once (the decode KV stream,
 // MI355X_MICROARCH.md 'nt-weights'); never for tiles other workgroups re-read.
+// 16-B load through a buffer descriptor, as asm: the compiler inserts no wait
+// for it; the caller retires it with a counted wait and reg_fence
+__device__ __forceinline__ u32x4 ld_buf(const i32x4& srd, uint32_t off) {
+    u32x4 v;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(srd) : "memory");
+    return v;
+}
+
 template <int BYTES, bool NT = false>
 __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds, uint32_t off) {
     uint32_t keep;
@@ -245,6 +265,22 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs
         }
         if (P::PK % kWave == 0 || p < P::PK) dma<GRAN, kDecodeNT>(rs.k, lds_addr(buf + i * kWave * GRAN), off);
     }
+    // K, then the mask, then V: a step's S^T and softmax start once K and the
+    // mask have landed, while V is still in flight
+    if constexpr (HM) {
+        uint8_t* mbuf = buf + C::kBytes + C::vBytes;
+#pragma unroll
+        for (int i = 0; i < P::NIM; i++) {
+            const int q = i * kWave + lane;
+            const int mr = q / P::MPR;
+            const int off = (q % P::MPR) * P::MG;
+            const uint32_t moff = (uint32_t)(mrow0 + mr) * (uint32_t)a.m_nb1 + (uint32_t)n0 * 2 + off;
+            // 16-B path (one instruction, rows 0..15): lanes of rows past the
+            // tile's query rows stay idle -- row 0's lanes always issue it, so
+            // the per-step instruction count (vmcnt budget) is unchanged
+            if (GRAN != 16 || mr < a.QPT) dma<P::MG>(rs.m, lds_addr(mbuf + i * kWave * P::MG), moff);
+        }
+    }
     uint8_t* vbuf = buf + C::kBytes;
 #pragma unroll
     for (int i = 0; i < P::NIV; i++) {
@@ -267,20 +303,6 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs
             off = (uint32_t)(n0 + row) * vn1 + (byte % C::rowV);
         }
         if (P::PV % kWave == 0 || p < P::PV) dma<GRAN, kDecodeNT>(rs.v, lds_addr(vbuf + i * kWave * GRAN), off);
-    }
-    if constexpr (HM) {
-        uint8_t* mbuf = buf + C::kBytes + C::vBytes;
-#pragma unroll
-        for (int i = 0; i < P::NIM; i++) {
-            const int q = i * kWave + lane;
-            const int mr = q / P::MPR;
-            const int off = (q % P::MPR) * P::MG;
-            const uint32_t moff = (uint32_t)(mrow0 + mr) * (uint32_t)a.m_nb1 + (uint32_t)n0 * 2 + off;
-            // 16-B path (one instruction, rows 0..15): lanes of rows past the
-            // tile's query rows stay idle -- row 0's lanes always issue it, so
-            // the per-step instruction count (vmcnt budget) is unchanged
-            if (GRAN != 16 || mr < a.QPT) dma<P::MG>(rs.m, lds_addr(mbuf + i * kWave * P::MG), moff);
-        }
     }
 }
 
@@ -514,33 +536,39 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
         default: break;
     }
 
+    // ---- Q^T operand (B of S^T = K.Q^T), rounded to f16 like src/utils.h:10
+    // (lanes of unused columns point past the descriptor: zeros, no traffic).
+    // Loaded first, as asm (no compiler wait), so that waiting for Q leaves the
+    // steps' LDS-DMA behind it in flight: compute starts as soon as step 0's K
+    // and mask land.
+    u32x4 qraw[NB][2];
+    {
+        const i32x4 qs = make_srd(a.q + (int64_t)iq3 * a.q_nb3, a.q_span);
+        const uint32_t qoff = row_ok ? (uint32_t)iq1 * (uint32_t)a.q_nb1 + (uint32_t)iq2 * (uint32_t)a.q_nb2 + 32 * g
+                                     : a.q_span;
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            qraw[b][0] = ld_buf(qs, qoff + 128 * b);
+            qraw[b][1] = ld_buf(qs, qoff + 128 * b + 16);
+        }
+    }
     for (int s = 0; s < nbuf && s < nsteps; s++) {
         issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + s * kStep, mrow0, wbuf + s * C::stepBytes, lane);
     }
 
     FATTN_STAMP(1);
-    // ---- Q^T operand (B of S^T = K.Q^T), rounded to f16 like src/utils.h:10
-    // (lanes of unused columns point past the descriptor: zeros, no traffic)
+    wait_steps<NI>(min(nbuf, nsteps));  // Q landed (the steps issued after it may fly on)
     f16x8 qop[NB];
-    {
-        const auto qs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.q + (int64_t)iq3 * a.q_nb3), 0,
-                                                          a.q_span, 0x00020000);
-        const uint32_t qoff = row_ok ? (uint32_t)iq1 * (uint32_t)a.q_nb1 + (uint32_t)iq2 * (uint32_t)a.q_nb2 + 32 * g
-                                     : a.q_span;
 #pragma unroll
-        for (int b = 0; b < NB; b++) {
-            const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qoff + 128 * b, 0, 0));
-            const f32x4 x1 =
-                __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qoff + 128 * b + 16, 0, 0));
-            f16x8 h;
-            h.s0 = (f16)x0.x; h.s1 = (f16)x0.y; h.s2 = (f16)x0.z; h.s3 = (f16)x0.w;
-            h.s4 = (f16)x1.x; h.s5 = (f16)x1.y; h.s6 = (f16)x1.z; h.s7 = (f16)x1.w;
-            qop[b] = h;
-        }
+    for (int b = 0; b < NB; b++) {
+        reg_fence(qraw[b][0]);
+        reg_fence(qraw[b][1]);
+        const f32x4 x0 = __builtin_bit_cast(f32x4, qraw[b][0]), x1 = __builtin_bit_cast(f32x4, qraw[b][1]);
+        f16x8 h;
+        h.s0 = (f16)x0.x; h.s1 = (f16)x0.y; h.s2 = (f16)x0.z; h.s3 = (f16)x0.w;
+        h.s4 = (f16)x1.x; h.s5 = (f16)x1.y; h.s6 = (f16)x1.z; h.s7 = (f16)x1.w;
+        qop[b] = h;
     }
-    // Q is loaded after the first steps' LDS-DMA is in flight, so the HBM stream
-    // starts at once; waiting for Q (the youngest loads) retires those steps too
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     float m_run = kNegInf;  // running max (log2 domain) of column m
     float l_run = 0.0f;     // this lane's partial row sum
@@ -554,10 +582,13 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     const float log2e = 1.4426950408889634f;
     int cur = 0;  // buffer of step s
     for (int s = 0; s < nsteps; s++) {
-        wait_steps<NI>(min(nbuf - 1, nsteps - 1 - s));
+        const int ahead = min(nbuf - 1, nsteps - 1 - s);  // steps issued after step s
+        // K and mask of step s landed (its V and the later steps may fly on)
+        wait_steps_plus<NI, P::NIV>(ahead);
         if (s < 8) FATTN_STAMP(2 + s);
 #ifdef FATTN_DIAG_NOCOMPUTE
         // diagnostic build only: memory-side ceiling of this access pattern
+        wait_steps<NI>(ahead);
         if (s + nbuf < nsteps) {
             issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf) * kStep, mrow0,
                                             wbuf + cur * C::stepBytes, lane);
@@ -635,7 +666,8 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
         pb.s0 = (f16)pv[0]; pb.s1 = (f16)pv[1]; pb.s2 = (f16)pv[2]; pb.s3 = (f16)pv[3];
         pb.s4 = (f16)pv[4]; pb.s5 = (f16)pv[5]; pb.s6 = (f16)pv[6]; pb.s7 = (f16)pv[7];
 
-        // -- O^T += V^T.P^T
+        // -- O^T += V^T.P^T (V of step s landed)
+        wait_steps<NI>(ahead);
         if constexpr (C::VTT == FATTN_TYPE_F16) {
 #pragma unroll
             for (int c = 0; c < NC; c++) o[c] = mfma16(v_operand_f16<VT, D>(vb, c, g, i16), pb, o[c]);
