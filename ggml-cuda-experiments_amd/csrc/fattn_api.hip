@@ -36,6 +36,7 @@ int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
 int g_opt_pf_stagger = 2;
 int g_opt_pf_waves = 8;
 int g_opt_pf_dequant = 0;  // 0 auto, 1 in the prefill kernel, 2 pre-pass to f16 rows
+int g_opt_no_wave_merge = 0;  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
 int g_opt_pf_pipe = 0;     // f16 images: 0 auto, 1 fattn_pf_kernel, 2 fattn_pfp_kernel
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
@@ -155,9 +156,18 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     a.ncp = 1;
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     if (a.n_chunks > 1 && !combine_ok(a.n_chunks, rv_max, pl.D)) return FATTN_ERR_INVALID_ARG;
+    // one-row tiles with few parts: per-wave partials, merged by the last wave
+    a.wave_merge = a.n_chunks > 1 && rv_max == 1 && pl.D == 128 && !g_opt_no_wave_merge &&
+                   a.n_chunks * kSplitWaves <= kWaveMergeParts;
     pl.lds = G.lds_bytes(nbuf);
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
-    if (a.n_chunks > 1) {
+    if (a.n_chunks > 1 && a.wave_merge) {
+        // [arrival counters][(m, l) per part][row-0 O per part], parts = waves
+        const size_t parts = (size_t)S * Y * a.n_chunks * kSplitWaves;
+        pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
+        pl.ml_bytes = (parts * 2 * sizeof(float) + 255) / 256 * 256;
+        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + parts * pl.D * 4;
+    } else if (a.n_chunks > 1) {
         // [arrival counters, one 256-B line per tile][(m, l) pairs][O partials];
         // zero-filled once per allocation: each launch re-arms the counters
         pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
@@ -584,6 +594,10 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_PF_DEQUANT:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_dequant = value;
+            return FATTN_OK;
+        case FATTN_OPT_SPLIT_WAVE_MERGE:
+            if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
+            g_opt_no_wave_merge = value;
             return FATTN_OK;
         case FATTN_OPT_PF_PIPE:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;

@@ -74,6 +74,8 @@ struct SplitArgs {
     int nbuf;           // steps in flight per wave (1..4); LDS per wave = wave_bytes
     int wave_bytes;
     int pf_stagger;     // prefill kernel: SIMD partner waves run their phases staggered
+    int wave_merge;     // split kernel, one-row tiles: every wave publishes its own partial and
+                        // the last-arriving WAVE merges them (no LDS merge, no barriers)
 };
 
 template <int KT, int VT, int D>
@@ -186,6 +188,14 @@ __device__ __forceinline__ u32x4 ld_sc1_buf(const i32x4& srd, uint32_t off) {
 // consumer waits with an explicit vmcnt.
 // NT: non-temporal policy for bytes one CU reads once (the decode KV stream,
 // MI355X_MICROARCH.md 'nt-weights'); never for tiles other workgroups re-read.
+// (one dword: hipcc mis-tracked the .y half of a u32x2 asm output here --
+// it reused that register as a temporary before the value's last use)
+__device__ __forceinline__ uint32_t ld_sc1_buf_b32(const i32x4& srd, uint32_t off) {
+    uint32_t v;
+    asm volatile("buffer_load_dword %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(srd) : "memory");
+    return v;
+}
+
 // 16-B load through a buffer descriptor, as asm: the compiler inserts no wait
 // for it; the caller retires it with a counted wait and reg_fence
 __device__ __forceinline__ u32x4 ld_buf(const i32x4& srd, uint32_t off) {
@@ -464,6 +474,90 @@ __device__ unsigned long long* g_stamps;
 template <int D, int CB = 2>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
                                              int rv, int row_base, uint8_t* smem);
+
+// One-row tiles (decode with n_q * H / Hkv == 1 per tile), up to 32 parts per
+// tile: each WAVE is a part.  It stores its (O, m, l) write-through (sc1),
+// drains, and counts itself on the tile's arrival word; the wave that counts
+// last merges all parts alone -- lane i owns dims 2i, 2i+1, every part's
+// values come in one round trip, weights by wave reductions -- and writes dst.
+// No LDS merge and no workgroup barrier: waves leave as they finish.  Same
+// fa_reduce math as combine_tile (src/flash_row_float.h:415-472), fixed order.
+constexpr int kWaveMergeParts = 32;
+template <int D, bool VQ8>
+__device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f32x4 (&o)[D / 16], float m_run,
+                                                    float l_tot, int chunk, int wave, int lane, int qt, int hs,
+                                                    int ik2, int iq3) {
+    static_assert(D == 128, "lane i <-> dims 2i, 2i+1");
+    constexpr int NB = D / QK;
+    constexpr int NC = D / 16;
+    constexpr float kNegInf = -__builtin_inff();
+    const int g = lane >> 4, m = lane & 15;
+    const int NP = a.n_chunks * kSplitWaves;
+    const int64_t tile = (int64_t)iq3 * gridDim.y + blockIdx.y;
+    const int part = chunk * kSplitWaves + wave;
+    float* po = a.ws_o + (tile * NP + part) * D;  // row 0 of the part: [NP][D] per tile
+    auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
+    if (m == 0) {  // column 0 = the tile's row; its dims sit on lanes 0, 16, 32, 48
+        if constexpr (VQ8) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                const f32x4 e = o[2 * b], od = o[2 * b + 1];
+                st_sc1(po + 32 * b + 8 * g, u32x4{bits(e.x), bits(od.x), bits(e.y), bits(od.y)});
+                st_sc1(po + 32 * b + 8 * g + 4, u32x4{bits(e.z), bits(od.z), bits(e.w), bits(od.w)});
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < NC; c++)
+                st_sc1(po + 16 * c + 4 * g, u32x4{bits(o[c].x), bits(o[c].y), bits(o[c].z), bits(o[c].w)});
+        }
+        if (g == 0) st_sc1_x2(a.ws_ml + 2 * (tile * NP + part), u32x2{bits(m_run), bits(l_tot)});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t* cnt = a.ws_cnt + tile * kCntStride;
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != (uint32_t)(NP - 1)) return;
+    if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- merge: every load issued before one wait (parts past NP: out of range, zeros)
+    const uint32_t obytes = (uint32_t)(NP * D * 4);
+    const i32x4 osrd = make_srd(a.ws_o + tile * NP * D, obytes);
+    const i32x4 msrd = make_srd(a.ws_ml + 2 * tile * NP, (uint32_t)(NP * 8));
+    uint32_t v0[kWaveMergeParts], v1[kWaveMergeParts];
+#pragma unroll
+    for (int p = 0; p < kWaveMergeParts; p++) {
+        const uint32_t off = p < NP ? (uint32_t)((p * D + 2 * lane) * 4) : obytes;
+        v0[p] = ld_sc1_buf_b32(osrd, off);
+        v1[p] = ld_sc1_buf_b32(osrd, off + 4);
+    }
+    uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
+    uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8 + 4));  //          l of part p
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    reg_fence(mlm);
+    reg_fence(mll);
+#pragma unroll
+    for (int p = 0; p < kWaveMergeParts; p++) {
+        reg_fence(v0[p]);
+        reg_fence(v1[p]);
+    }
+    const float mp = lane < NP ? __builtin_bit_cast(float, mlm) : kNegInf;
+    const float M = seg_reduce<true>(mp, 64);
+    const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M);
+    const float L = seg_reduce<false>(lane < NP ? w * __builtin_bit_cast(float, mll) : 0.0f, 64);
+    float acc0 = 0.0f, acc1 = 0.0f;
+#pragma unroll
+    for (int p = 0; p < kWaveMergeParts; p++) {
+        const float wp = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w), p));
+        acc0 += wp * __builtin_bit_cast(float, v0[p]);
+        acc1 += wp * __builtin_bit_cast(float, v1[p]);
+    }
+    const int rq = div_R(a, 0);
+    const int riq1 = qt * a.QPT + rq;
+    const int riq2 = ik2 * a.rk2 + hs * a.R;
+    float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + 2 * lane;
+    const float inv = 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
+    *(f32x2*)out = f32x2{L == 0.0f ? __builtin_nanf("") : acc0 * inv, L == 0.0f ? __builtin_nanf("") : acc1 * inv};
+}
 
 template <int KT, int VT, int D, int GRAN, bool HM>
 __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4) ? 2 : 4) void fattn_split_kernel(
@@ -768,6 +862,12 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
             const float cb = kVOff * grp4_sum(corr[b]);
             o[2 * b] -= cb;
             o[2 * b + 1] -= cb;
+        }
+    }
+    if constexpr (D == 128) {
+        if (a.wave_merge) {
+            wave_merge_epilogue<D, kVQ8>(a, o, m_run, l_tot, chunk, wave, lane, qt, hs, ik2, iq3);
+            return;
         }
     }
     constexpr int MS = C::kMergeStride;

@@ -44,6 +44,7 @@ OPT_PF_STAGGER = 6
 OPT_PF_WAVES = 7
 OPT_PF_DEQUANT = 8
 OPT_PF_PIPE = 9
+OPT_SPLIT_WAVE_MERGE = 10
 
 
 class FattnError(RuntimeError):

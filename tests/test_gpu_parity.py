@@ -196,6 +196,32 @@ def test_mq_fully_masked_rows_are_nan(dev):
     assert attn_rel_err(got, ref) <= RTOL
 
 
+@pytest.mark.parametrize("kt,N,chunk", [("q8_0", 4096, 0), ("q4_0", 2048, 256), ("f16", 1024, 128), ("q8_0", 96, 32)])
+def test_wave_merge(dev, kt, N, chunk):
+    """One-row split tiles (n_q = 1, H == Hkv): per-wave partials merged by the
+    last-arriving wave, against the oracle and against the workgroup-level merge
+    (FATTN_OPT_SPLIT_WAVE_MERGE = 1)."""
+    p = make_problem(D=128, NQ=1, H=8, N=N, kv_type=kt, mask="random", seed=41)
+    a = run_gpu(p, kv_chunk=chunk)
+    fattn.set_option(fattn.OPT_SPLIT_WAVE_MERGE, 1)
+    try:
+        b = run_gpu(p, kv_chunk=chunk)
+    finally:
+        fattn.set_option(fattn.OPT_SPLIT_WAVE_MERGE, 0)
+    ref = p.oracle()
+    assert attn_rel_err(a, ref) <= RTOL
+    assert attn_rel_err(b, ref) <= RTOL
+
+
+def test_wave_merge_fully_masked_is_nan(dev):
+    p = make_problem(D=128, NQ=1, H=4, N=2048, kv_type="q8_0", mask="zero", seed=42)
+    m = orc.f16_bits_to_f32(p.mask_bits)
+    m[0, :] = -np.inf
+    p.mask_bits = orc.f32_to_f16_bits(m)
+    got = run_gpu(p)
+    assert np.isnan(got).all()
+
+
 # ------------------------------------------------------------------ prefill kernel (fattn_pf.h)
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
@@ -460,7 +486,8 @@ def test_graph_capture(dev):
     assert attn_rel_err(t["dst"].cpu().numpy(), p.oracle()) <= RTOL
 
 
-def test_chunk_merge_handoff_stress(dev):
+@pytest.mark.parametrize("hkv", [8, 32], ids=["gqa4-workgroup-merge", "mha-wave-merge"])
+def test_chunk_merge_handoff_stress(dev, hkv):
     """The last-arriving workgroup of a tile merges the chunk partials of the
     others (sc1 stores -> drain -> agent atomic add -> sc1 loads).  Stress the
     hand-off the way MI355X_MICROARCH.md asks: one workspace reused across
@@ -468,7 +495,7 @@ def test_chunk_merge_handoff_stress(dev):
     zero), a competing copy stream for uneven load, and every output word
     checked on every launch."""
     import torch
-    p = make_problem(D=128, NQ=1, H=32, Hkv=8, N=4096, kv_type="q8_0", seed=21)
+    p = make_problem(D=128, NQ=1, H=32, Hkv=hkv, N=4096, kv_type="q8_0", seed=21)
     ref = p.oracle()
     t = upload(p, dev)
     qv, kv, vv, mv = views(p, t)
@@ -499,5 +526,5 @@ def test_chunk_merge_handoff_stress(dev):
         got = t["dst"].cpu().numpy()
         assert attn_rel_err(got, ref) <= RTOL, f"iteration {it} (plan {it % len(atts)})"
     assert multi > 0
-    # counters re-armed: the 8 tiles' counters (one 256-B line each) are zero again
-    assert int(shared[: 8 * 256].view(torch.int32).abs().sum()) == 0
+    # counters re-armed: the tiles' counters (one 256-B line each) are zero again
+    assert int(shared[: hkv * 256].view(torch.int32).abs().sum()) == 0
