@@ -482,7 +482,8 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
 // values come in one round trip, weights by wave reductions -- and writes dst.
 // No LDS merge and no workgroup barrier: waves leave as they finish.  Same
 // fa_reduce math as combine_tile (src/flash_row_float.h:415-472), fixed order.
-constexpr int kWaveMergeParts = 32;
+constexpr int kWaveMergeParts = 64;  // parts per tile (one (m, l) pair per lane)
+constexpr int kWaveMergeBatch = 32;  // parts loaded per round trip
 template <int D, bool VQ8>
 __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f32x4 (&o)[D / 16], float m_run,
                                                     float l_tot, int chunk, int wave, int lane, int qt, int hs,
@@ -523,33 +524,46 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     const uint32_t obytes = (uint32_t)(NP * D * 4);
     const i32x4 osrd = make_srd(a.ws_o + tile * NP * D, obytes);
     const i32x4 msrd = make_srd(a.ws_ml + 2 * tile * NP, (uint32_t)(NP * 8));
-    uint32_t v0[kWaveMergeParts], v1[kWaveMergeParts];
+    uint32_t v0[kWaveMergeBatch], v1[kWaveMergeBatch];
+    auto issue = [&](int p0) {
 #pragma unroll
-    for (int p = 0; p < kWaveMergeParts; p++) {
-        const uint32_t off = p < NP ? (uint32_t)((p * D + 2 * lane) * 4) : obytes;
-        v0[p] = ld_sc1_buf_b32(osrd, off);
-        v1[p] = ld_sc1_buf_b32(osrd, off + 4);
-    }
+        for (int p = 0; p < kWaveMergeBatch; p++) {
+            const uint32_t off = p0 + p < NP ? (uint32_t)(((p0 + p) * D + 2 * lane) * 4) : obytes;
+            v0[p] = ld_sc1_buf_b32(osrd, off);
+            v1[p] = ld_sc1_buf_b32(osrd, off + 4);
+        }
+    };
+    auto fence = [&] {
+#pragma unroll
+        for (int p = 0; p < kWaveMergeBatch; p++) {
+            reg_fence(v0[p]);
+            reg_fence(v1[p]);
+        }
+    };
+    issue(0);
     uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
     uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8 + 4));  //          l of part p
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     reg_fence(mlm);
     reg_fence(mll);
-#pragma unroll
-    for (int p = 0; p < kWaveMergeParts; p++) {
-        reg_fence(v0[p]);
-        reg_fence(v1[p]);
-    }
+    fence();
     const float mp = lane < NP ? __builtin_bit_cast(float, mlm) : kNegInf;
     const float M = seg_reduce<true>(mp, 64);
     const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M);
     const float L = seg_reduce<false>(lane < NP ? w * __builtin_bit_cast(float, mll) : 0.0f, 64);
     float acc0 = 0.0f, acc1 = 0.0f;
+    for (int p0 = 0; p0 < NP; p0 += kWaveMergeBatch) {  // wave-uniform
+        if (p0 > 0) {
+            issue(p0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            fence();
+        }
 #pragma unroll
-    for (int p = 0; p < kWaveMergeParts; p++) {
-        const float wp = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w), p));
-        acc0 += wp * __builtin_bit_cast(float, v0[p]);
-        acc1 += wp * __builtin_bit_cast(float, v1[p]);
+        for (int p = 0; p < kWaveMergeBatch; p++) {
+            const float wp = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w), p0 + p));
+            acc0 += wp * __builtin_bit_cast(float, v0[p]);
+            acc1 += wp * __builtin_bit_cast(float, v1[p]);
+        }
     }
     const int rq = div_R(a, 0);
     const int riq1 = qt * a.QPT + rq;

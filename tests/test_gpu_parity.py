@@ -196,7 +196,9 @@ def test_mq_fully_masked_rows_are_nan(dev):
     assert attn_rel_err(got, ref) <= RTOL
 
 
-@pytest.mark.parametrize("kt,N,chunk", [("q8_0", 4096, 0), ("q4_0", 2048, 256), ("f16", 1024, 128), ("q8_0", 96, 32)])
+@pytest.mark.parametrize("kt,N,chunk", [("q8_0", 4096, 0), ("q4_0", 2048, 256), ("f16", 1024, 128), ("q8_0", 96, 32),
+                                        ("q8_0", 4096, 256),    # 64 parts: two load batches
+                                        ("q8_0", 4096, 128)])   # 128 parts: workgroup-level merge
 def test_wave_merge(dev, kt, N, chunk):
     """One-row split tiles (n_q = 1, H == Hkv): per-wave partials merged by the
     last-arriving wave, against the oracle and against the workgroup-level merge
