@@ -178,6 +178,8 @@ def main():
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--pf-dequant", type=int, default=0,
                     help="quantised prefill: 0 auto, 1 in-kernel dequantisation, 2 f16 pre-pass")
+    ap.add_argument("--split-prio", type=int, default=0,
+                    help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
     ap.add_argument("--pf-pipe", type=int, default=0,
                     help="prefill over f16 images: 0 auto, 1 fattn_pf_kernel, 2 software-pipelined fattn_pfp_kernel")
     ap.add_argument("--prefill-kv", default="q8_0", choices=["q8_0", "q4_0", "f16"],
@@ -203,6 +205,8 @@ def main():
         fattn.set_option(fattn.OPT_PF_WAVES, args.pf_waves)
     if args.pf_dequant:
         fattn.set_option(fattn.OPT_PF_DEQUANT, args.pf_dequant)
+    if args.split_prio:
+        fattn.set_option(fattn.OPT_SPLIT_PRIO, args.split_prio)
     if args.pf_pipe:
         fattn.set_option(fattn.OPT_PF_PIPE, args.pf_pipe)
     world = int(os.environ.get("WORLD_SIZE", "1"))

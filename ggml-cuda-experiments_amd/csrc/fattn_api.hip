@@ -36,6 +36,7 @@ int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
 int g_opt_pf_stagger = 2;
 int g_opt_pf_waves = 8;
 int g_opt_pf_dequant = 0;  // 0 auto, 1 in the prefill kernel, 2 pre-pass to f16 rows
+int g_opt_split_prio = 0;     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
 int g_opt_no_wave_merge = 0;  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
 int g_opt_pf_pipe = 0;     // f16 images: 0 auto, 1 fattn_pf_kernel, 2 fattn_pfp_kernel
 
@@ -150,6 +151,7 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
         while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
     }
     a.nbuf = nbuf;
+    a.split_prio = g_opt_split_prio;
     a.wave_bytes = G.wave_bytes(nbuf);
     a.chunk_len = spw * quantum;
     a.n_chunks = (int)((N + a.chunk_len - 1) / a.chunk_len);
@@ -594,6 +596,10 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_PF_DEQUANT:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_dequant = value;
+            return FATTN_OK;
+        case FATTN_OPT_SPLIT_PRIO:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_prio = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_WAVE_MERGE:
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;

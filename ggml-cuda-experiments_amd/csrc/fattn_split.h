@@ -74,6 +74,7 @@ struct SplitArgs {
     int nbuf;           // steps in flight per wave (1..4); LDS per wave = wave_bytes
     int wave_bytes;
     int pf_stagger;     // prefill kernel: SIMD partner waves run their phases staggered
+    int split_prio;     // split kernel wave priorities: 0 staggered 3/2/1/0, 1 none, 2 staggered while issuing
     int wave_merge;     // split kernel, one-row tiles: every wave publishes its own partial and
                         // the last-arriving WAVE merges them (no LDS merge, no barriers)
 };
@@ -637,11 +638,14 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     // issue, so every wave's last piece lands near the end of the burst and
     // all compute starts late; by priority the first waves' steps land first
     // and their compute overlaps the rest of the stream.
-    switch (__builtin_amdgcn_readfirstlane(wave)) {
-        case 0: __builtin_amdgcn_s_setprio(3); break;
-        case 1: __builtin_amdgcn_s_setprio(2); break;
-        case 2: __builtin_amdgcn_s_setprio(1); break;
-        default: break;
+    // (split_prio 1: no priorities; 2: staggered only while the first steps issue)
+    if (a.split_prio != 1) {
+        switch (__builtin_amdgcn_readfirstlane(wave)) {
+            case 0: __builtin_amdgcn_s_setprio(3); break;
+            case 1: __builtin_amdgcn_s_setprio(2); break;
+            case 2: __builtin_amdgcn_s_setprio(1); break;
+            default: break;
+        }
     }
 
     // ---- Q^T operand (B of S^T = K.Q^T), rounded to f16 like src/utils.h:10
@@ -665,6 +669,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     }
 
     FATTN_STAMP(1);
+    if (a.split_prio == 2) __builtin_amdgcn_s_setprio(0);
     wait_steps<NI>(min(nbuf, nsteps));  // Q landed (the steps issued after it may fly on)
     f16x8 qop[NB];
 #pragma unroll

@@ -45,6 +45,7 @@ OPT_PF_WAVES = 7
 OPT_PF_DEQUANT = 8
 OPT_PF_PIPE = 9
 OPT_SPLIT_WAVE_MERGE = 10
+OPT_SPLIT_PRIO = 11
 
 
 class FattnError(RuntimeError):

@@ -133,7 +133,9 @@ enum {
                                        1 = fattn_pf_kernel, 2 = software-pipelined fattn_pfp_kernel */,
     FATTN_OPT_SPLIT_WAVE_MERGE = 10 /* split kernel, one-row tiles with <= 32 wave partials: 0 = every wave
                                        publishes and the last-arriving wave merges (default), 1 = the
-                                       workgroup-level merge used for all other tiles */
+                                       workgroup-level merge used for all other tiles */,
+    FATTN_OPT_SPLIT_PRIO = 11       /* split kernel wave priorities: 0 = staggered 3/2/1/0 (default), 1 = none,
+                                       2 = staggered only while the first steps are issued */
 };
 int fattn_set_option(int option, int value);
 
