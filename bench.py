@@ -84,7 +84,7 @@ def cpu_baseline(seconds: float, threads: int):
             "ms_per_problem": round(el / reps * 1e3, 2), "host_cpu": _cpu_model()}
 
 
-def prefill_measure(dev, hip, evs, kvn="q8_0", pf_dequant=0, pf_pipe=0, steps=5):
+def prefill_measure(dev, hip, evs, kvn="q8_0", pf_dequant=0, pf_pipe=0, causal=False, steps=5):
     """The MFMA-bound prefill shape of SURVEY.md §8d (n_q = N = 4096, 32 heads,
     head_dim 128, Q8_0 K/V, random f16 mask, non-causal): `steps` launches of
     fattn_pf_kernel captured in one HIP graph, HIP events around the replay on
@@ -105,6 +105,9 @@ def prefill_measure(dev, hip, evs, kvn="q8_0", pf_dequant=0, pf_pipe=0, steps=5)
                for _ in range(2)] for _ in range(R)]
     q = torch.rand((1, NQ, H, D), generator=g, device=dev) * 2 - 1
     mask = (torch.rand((NQ, N), generator=g, device=dev) * 2 - 1).to(torch.float16)
+    if causal:  # query i sees keys <= i (N == NQ): the upper triangle is -inf
+        tri = torch.triu(torch.ones((NQ, N), dtype=torch.bool, device=dev), diagonal=1)
+        mask = mask.masked_fill(tri, float("-inf"))
     out = torch.empty((R, 1, NQ, H, D), dtype=torch.float32, device=dev)
     att = fattn.Attention(fattn.q_view(q), fattn.kv_view(kv[0][0], typ, D, N, H), fattn.kv_view(kv[0][1], typ, D, N, H),
                           fattn.mask_view(mask), out[0], 1.0 / D ** 0.5)
@@ -134,13 +137,15 @@ def prefill_measure(dev, hip, evs, kvn="q8_0", pf_dequant=0, pf_pipe=0, steps=5)
     torch.cuda.synchronize()
     hip.hipEventElapsedTime(C.byref(f), evs[0], evs[1])
     ms = f.value / steps
-    flops = 4 * NQ * N * D * H
+    # algorithmic flops: the unmasked (query, key) pairs (all of them without causality)
+    pairs = NQ * (NQ + 1) // 2 if causal else NQ * N
+    flops = 4 * pairs * D * H
     tf = flops / (ms * 1e-3) / 1e12
     pre = kvn != "f16" and pf_dequant == 2
     f16k = "fattn_pfp_kernel<f16,D128>" if pf_pipe == 2 else "fattn_pf_kernel<f16,D128>"
     kname = (f"pf_dequant_rows_kernel<{kvn}> x2 + {f16k}" if pre
              else f16k if kvn == "f16" else f"fattn_pf_kernel<{kvn},D128>")
-    return {"workload": f"prefill_{kvn}_h{H}_d{D}_n{N}_q{NQ}_mask", "kernel": kname,
+    return {"workload": f"prefill_{kvn}_h{H}_d{D}_n{N}_q{NQ}_{'causal' if causal else 'mask'}", "kernel": kname,
             "kernel_ms_avg": round(ms, 5), "flops_per_step": flops,
             "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None}}
@@ -182,6 +187,8 @@ def main():
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
     ap.add_argument("--pf-pipe", type=int, default=0,
                     help="prefill over f16 images: 0 auto, 1 fattn_pf_kernel, 2 software-pipelined fattn_pfp_kernel")
+    ap.add_argument("--prefill-causal", action="store_true",
+                    help="causal mask on the prefill measurement (fully masked blocks are skipped)")
     ap.add_argument("--prefill-kv", default="q8_0", choices=["q8_0", "q4_0", "f16"],
                     help="K/V type of the prefill measurement (the metric's is q8_0)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -379,7 +386,8 @@ def main():
         }
         if world == 1 and not args.no_prefill and NQ == 1:
             # north_star's second target: MFMA utilisation on the prefill shape
-            res["prefill"] = prefill_measure(dev, hip, evs, args.prefill_kv, args.pf_dequant, args.pf_pipe)
+            res["prefill"] = prefill_measure(dev, hip, evs, args.prefill_kv, args.pf_dequant, args.pf_pipe,
+                                             args.prefill_causal)
         if world == 1 and not args.no_cpu_baseline and NQ == 1:  # kernel_test.h's CPU path is one query row
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, min(args.cpu_threads, os.cpu_count() or 1))
         print(json.dumps(res), flush=True)

@@ -56,6 +56,7 @@ struct Plan {
     int pf_waves;
     bool pf_pre;            // quantised K/V converted to f16 rows in the workspace first
     bool pf_pipe;           // f16 images: the software-pipelined kernel (fattn_pfp.h)
+    bool pf_flags;          // masked prefill: live-block flags pre-pass (tile-range skipping)
     int64_t pf_rows;        // rows per converted tensor (Skv * Hkv * N)
     int64_t hkv;            // kv heads
     int nw;   // its waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
@@ -381,8 +382,11 @@ int make_plan(const fattn_params* p, Plan& pl) {
         else
             pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
-        // pre-pass: [K rows | V rows], f16 [Skv][Hkv][N][D] each
-        if (pl.pf_pre) pl.ws_bytes = 2 * (size_t)pl.pf_rows * D * 2;
+        // workspace: [live-block flags, n_qt x N/64 bytes (masked fattn_pf_kernel)]
+        //            [pre-pass: K rows | V rows, f16 [Skv][Hkv][N][D] each]
+        pl.pf_flags = has_mask && pl.pf_waves == 8 && !pl.pf_pipe;
+        if (pl.pf_flags) pl.cnt_bytes = ((size_t)a.n_qt * (N / kPfKeys) + 255) / 256 * 256;
+        pl.ws_bytes = pl.cnt_bytes + (pl.pf_pre ? 2 * (size_t)pl.pf_rows * D * 2 : 0);
         return FATTN_OK;
     }
     const int rc = pl.mq ? size_mq(pl, p->kv_chunk, Y, S, N) : size_split(pl, p->kv_chunk, Y, S, N, NQ);
@@ -483,6 +487,9 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     }
     auto kern = fattn_pf_kernel<KT, 128, HM>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        if (HM && pl.a.pf_flags)
+            hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,
+                               pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
         hipLaunchKernelGGL(kern, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
     });
 }
@@ -672,6 +679,7 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
         pl.a.ws_cnt = (uint32_t*)w;
         pl.a.ws_ml = (float*)(w + pl.cnt_bytes);
         pl.a.ws_o = (float*)(w + pl.cnt_bytes + pl.ml_bytes);  // (prefill pre-pass: the f16 rows)
+        if (pl.pf && pl.pf_flags) pl.a.pf_flags = w;
     }
     hipStream_t st = (hipStream_t)stream;
     Events ev;

@@ -213,7 +213,14 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     if ((a.pf_stagger & 4) && gridDim.y % 8 == 0) y = (y & 7) * (gridDim.y >> 3) + (y >> 3);
     const int iq3 = blockIdx.z;
     int qt = 0, ik2 = y, ik3 = iq3;
-    if (a.n_qt != 1) {
+    if (a.pf_flags) {
+        // masked: query tiles may see different KV ranges (causal: tile qt sees
+        // 4 qt + 4 of them), so the longest go first -- the last query tile of
+        // every head, then the one before, ... (longest-first dispatch)
+        const int nh = gridDim.y / a.n_qt;
+        qt = a.n_qt - 1 - y / nh;
+        ik2 = y % nh;
+    } else if (a.n_qt != 1) {
         qt = y % a.n_qt;
         ik2 = y / a.n_qt;
     }
@@ -226,7 +233,26 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     };
     int iq1, iq2;
     const bool row_ok = row_of(kPfRowsW * wave + c32, iq1, iq2);
-    const int ntiles = a.N / kPfKeys;
+    // live KV tile range of this query tile: [t0, t0 + ntiles).  With a mask,
+    // pf_mask_flags_kernel marked each (query tile, KV tile) block that has any
+    // key above -inf; tiles outside the first..last marked one are never
+    // fetched (causal prefill: about half of them).  Blocks inside the range
+    // that are -inf for a whole wave are skipped below.
+    int t0 = 0, ntiles = a.N / kPfKeys;
+    if (a.pf_flags) {
+        const uint8_t* fl = a.pf_flags + (int64_t)qt * ntiles;
+        int lo = ntiles, hi = -1;
+        for (int b = 0; b < ntiles; b += kWave) {  // wave-uniform; every wave computes the same range
+            const bool f = b + lane < ntiles && fl[b + lane] != 0;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(f);
+            if (m) {
+                lo = min(lo, b + (int)__builtin_ctzll(m));
+                hi = b + 63 - (int)__builtin_clzll(m);
+            }
+        }
+        t0 = lo;
+        ntiles = hi >= lo ? hi - lo + 1 : 0;
+    }
 
     StepSrc rs;
     rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
@@ -275,7 +301,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     auto mask_issue = [&](int s) {
         if constexpr (HM) {
 #ifndef FATTN_MQ_NOMEM
-            const uint32_t n2 = (uint32_t)s * kPfKeys * 2;
+            const uint32_t n2 = (uint32_t)(t0 + s) * kPfKeys * 2;
 #pragma unroll
             for (int k = 0; k < C::NIM; k++) {
                 const uint32_t off = moff[k] == a.m_span ? a.m_span : moff[k] + n2;
@@ -312,10 +338,11 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     uint32_t doff[4];
     if constexpr (C::kDirect) {
         pf_direct_offsets<D>(a, wave, lane, doff);
-        for (int s = 0; s < 2 && s < ntiles; s++) pf_direct_issue<D>(a, rs, s * kPfKeys, lds0 + s * C::pairBytes, wave, doff);
+        for (int s = 0; s < 2 && s < ntiles; s++)
+            pf_direct_issue<D>(a, rs, (t0 + s) * kPfKeys, lds0 + s * C::pairBytes, wave, doff);
         if (ntiles > 0) mask_issue(0);
     } else {
-        for (int s = 0; s < 3 && s < ntiles; s++) pf_issue<KT, D>(rs, s * kPfKeys, raw_lds(s), wave, lane);
+        for (int s = 0; s < 3 && s < ntiles; s++) pf_issue<KT, D>(rs, (t0 + s) * kPfKeys, raw_lds(s), wave, lane);
         if (ntiles > 0) mask_issue(0);
         // raw 0 landed (raw 1, 2 and mask 0 may fly on)
         pf_vm_wait<KT, D>(wave, min(2, ntiles - 1), ntiles > 0 ? NM : 0);
@@ -359,9 +386,9 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         if constexpr (C::kDirect) {
             // into the pair every wave finished reading before the barrier
             if (s + 2 < ntiles)
-                pf_direct_issue<D>(a, rs, (s + 2) * kPfKeys, lds0 + ((P + 2) % 3) * C::pairBytes, wave, doff);
+                pf_direct_issue<D>(a, rs, (t0 + s + 2) * kPfKeys, lds0 + ((P + 2) % 3) * C::pairBytes, wave, doff);
         } else {
-            if (s + 3 < ntiles) pf_issue<KT, D>(rs, (s + 3) * kPfKeys, raw_lds(s + 3), wave, lane);
+            if (s + 3 < ntiles) pf_issue<KT, D>(rs, (t0 + s + 3) * kPfKeys, raw_lds(s + 3), wave, lane);
         }
         PF_T(1);
         // SIMD partners (waves w and w + 4) run the tile's phases staggered:
@@ -392,6 +419,30 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
 #endif
         const uint8_t* img = smem + P * C::pairBytes;  // K image; vbase includes + img
 
+        // -- this wave's mask block of tile s (landed; raw s+3 / image s+2 may fly
+        // on): read it, refill the slot, and skip the tile when the whole 32 x 64
+        // block is -inf (causal prefill: a fully masked block adds nothing to m,
+        // l or O, so skipping it is exact -- the rows' state is left untouched)
+        u32x2 mk[2][4];
+        bool live = true;
+        if constexpr (HM) {
+            pf_vm_wait<KT, D>(wave, s + C::ahead < ntiles ? 1 : 0, 0);
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+#pragma unroll
+                for (int uu = 0; uu < 4; uu++) mk[t][uu] = *(const u32x2*)(smem + maddr[t][uu]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (s + 1 < ntiles) mask_issue(s + 1);
+            uint32_t open = 0;  // any key not at -inf (f16 0xFC00)
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+#pragma unroll
+                for (int uu = 0; uu < 4; uu++) open |= (mk[t][uu].x ^ 0xFC00FC00u) | (mk[t][uu].y ^ 0xFC00FC00u);
+            }
+            live = __builtin_amdgcn_ballot_w64(open != 0) != 0;
+        }
+        if (live) {
         // -- S^T = K.Q^T: two 32-key subtiles; each subtile's 8 K operands are
         // read before its MFMA chain (one LDS wait per chain, not per MFMA)
         f32x16 st[2];
@@ -419,16 +470,6 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         // is key 32t + 8(j/4) + 4h + (j%4) of this lane's row
         float u[2][16];
         if constexpr (HM) {
-            // mask s landed (raw s+3 / image s+2 may fly on); read it, then refill the slot
-            pf_vm_wait<KT, D>(wave, s + C::ahead < ntiles ? 1 : 0, 0);
-            u32x2 mk[2][4];
-#pragma unroll
-            for (int t = 0; t < 2; t++) {
-#pragma unroll
-                for (int uu = 0; uu < 4; uu++) mk[t][uu] = *(const u32x2*)(smem + maddr[t][uu]);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (s + 1 < ntiles) mask_issue(s + 1);
 #pragma unroll
             for (int t = 0; t < 2; t++) {
 #pragma unroll
@@ -537,6 +578,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             asm volatile("" ::"v"(z));
         }
 #endif
+        }  // live
         PF_T(5);
         if (late) {
             dequant_next();
@@ -583,6 +625,27 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             }
         }
     }
+}
+
+// ---- prefill mask pre-pass: flags[qt][s] = 1 when any of the query tile's
+// QPT mask rows has a key above -inf (f16 0xFC00) in KV tile s.  One workgroup
+// per (query tile, KV tile) block; every flag is written on every launch, so
+// the array needs no initialisation.  Reads the mask once (f16 [NQ][N]).
+__global__ __launch_bounds__(256) void pf_mask_flags_kernel(const uint8_t* __restrict__ mask, int64_t m_nb1, int NQ,
+                                                            int QPT, int ntiles, uint8_t* __restrict__ flags) {
+    const int s = blockIdx.x, qt = blockIdx.y;
+    // thread -> (row qt*QPT + r, 16-B piece pc of the tile's 128 B): 8 pieces per row
+    uint32_t open = 0;
+    for (int i = threadIdx.x; i < QPT * 8; i += 256) {
+        const int r = i >> 3, pc = i & 7;
+        const int q = qt * QPT + r;
+        if (q < NQ) {
+            const u32x4 w = *(const u32x4*)(mask + (int64_t)q * m_nb1 + (int64_t)s * kPfKeys * 2 + pc * 16);
+            open |= (w.x ^ 0xFC00FC00u) | (w.y ^ 0xFC00FC00u) | (w.z ^ 0xFC00FC00u) | (w.w ^ 0xFC00FC00u);
+        }
+    }
+    const int any = __syncthreads_or(open != 0);
+    if (threadIdx.x == 0) flags[(int64_t)qt * ntiles + s] = any ? 1 : 0;
 }
 
 // ---- prefill pre-pass: quantised K or V rows -> dense f16 rows [Skv][Hkv][N][D],

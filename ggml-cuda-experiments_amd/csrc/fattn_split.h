@@ -74,6 +74,7 @@ struct SplitArgs {
     int nbuf;           // steps in flight per wave (1..4); LDS per wave = wave_bytes
     int wave_bytes;
     int pf_stagger;     // prefill kernel: SIMD partner waves run their phases staggered
+    const uint8_t* pf_flags;  // prefill: [n_qt][N/64] live-block flags (pf_mask_flags_kernel), or null
     int split_prio;     // split kernel wave priorities: 0 staggered 3/2/1/0, 1 none, 2 staggered while issuing
     int wave_merge;     // split kernel, one-row tiles: every wave publishes its own partial and
                         // the last-arriving WAVE merges them (no LDS merge, no barriers)

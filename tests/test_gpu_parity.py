@@ -323,6 +323,32 @@ def test_pf_predequant_bitexact(dev, kt):
     assert attn_rel_err(a, p.oracle()) <= RTOL
 
 
+@pytest.mark.parametrize("kt", ["q8_0", "f16"])
+def test_pf_causal_block_skip(dev, kt):
+    """Causal prefill (n_q = N = 1024, 8 heads): the prefill kernel skips every
+    wave's fully masked 32 x 64 blocks; against the multi-query / split kernel
+    (no skipping) and one head against the oracle."""
+    p = make_problem(D=128, NQ=1024, H=8, N=1024, kv_type=kt, mask="causal", seed=43)
+    fattn.set_option(fattn.OPT_PF, 2)
+    try:
+        a = run_gpu(p)
+    finally:
+        fattn.set_option(fattn.OPT_PF, 0)
+    fattn.set_option(fattn.OPT_PF, 1)
+    try:
+        b = run_gpu(p)
+    finally:
+        fattn.set_option(fattn.OPT_PF, 0)
+    assert np.isfinite(a).all()
+    assert attn_rel_err(a, b) <= RTOL
+    sub = make_problem(D=128, NQ=1024, H=1, N=1024, kv_type=kt, mask="causal", seed=43)
+    sub.q = np.ascontiguousarray(p.q[:, :, 3:4, :])
+    sub.k_bytes = np.ascontiguousarray(p.k_bytes.reshape(p.Hkv, -1)[3:4].reshape(-1))
+    sub.v_bytes = np.ascontiguousarray(p.v_bytes.reshape(p.Hkv, -1)[3:4].reshape(-1))
+    sub.mask_bits = p.mask_bits
+    assert attn_rel_err(a[:, :, 3:4, :], sub.oracle()) <= RTOL
+
+
 def test_pf_f16_prefill_full(dev):
     """f16 K/V at the prefill shape (n_q = N = 4096, 32 heads, random mask): the
     prefill kernel against the split-KV kernel, one head against the oracle."""
