@@ -36,6 +36,7 @@ int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
 int g_opt_pf_stagger = 2;
 int g_opt_pf_waves = 8;
 int g_opt_pf_dequant = 0;  // 0 auto, 1 in the prefill kernel, 2 pre-pass to f16 rows
+int g_opt_pf_no_skip = 0;     // 1: masked prefill without the live-block pre-pass (FATTN_OPT_PF_SKIP)
 int g_opt_split_prio = 0;     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
 int g_opt_no_wave_merge = 0;  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
 int g_opt_pf_pipe = 0;     // f16 images: 0 auto, 1 fattn_pf_kernel, 2 fattn_pfp_kernel
@@ -384,7 +385,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: [live-block flags, n_qt x N/64 bytes (masked fattn_pf_kernel)]
         //            [pre-pass: K rows | V rows, f16 [Skv][Hkv][N][D] each]
-        pl.pf_flags = has_mask && pl.pf_waves == 8 && !pl.pf_pipe;
+        pl.pf_flags = has_mask && pl.pf_waves == 8 && !pl.pf_pipe && !g_opt_pf_no_skip;
         if (pl.pf_flags) pl.cnt_bytes = ((size_t)a.n_qt * (N / kPfKeys) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes + (pl.pf_pre ? 2 * (size_t)pl.pf_rows * D * 2 : 0);
         return FATTN_OK;
@@ -603,6 +604,10 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_PF_DEQUANT:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_dequant = value;
+            return FATTN_OK;
+        case FATTN_OPT_PF_SKIP:
+            if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
+            g_opt_pf_no_skip = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_PRIO:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;

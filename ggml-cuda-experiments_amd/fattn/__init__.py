@@ -46,6 +46,7 @@ OPT_PF_DEQUANT = 8
 OPT_PF_PIPE = 9
 OPT_SPLIT_WAVE_MERGE = 10
 OPT_SPLIT_PRIO = 11
+OPT_PF_SKIP = 12
 
 
 class FattnError(RuntimeError):

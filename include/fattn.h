@@ -135,7 +135,11 @@ enum {
                                        publishes and the last-arriving wave merges (default), 1 = the
                                        workgroup-level merge used for all other tiles */,
     FATTN_OPT_SPLIT_PRIO = 11       /* split kernel wave priorities: 0 = staggered 3/2/1/0 (default), 1 = none,
-                                       2 = staggered only while the first steps are issued */
+                                       2 = staggered only while the first steps are issued */,
+    FATTN_OPT_PF_SKIP = 12          /* masked prefill: 0 = a pre-pass flags the blocks with any key above -inf
+                                       and the kernel walks only the live KV range, longest query tiles
+                                       first (default; the workspace holds n_qt * N/64 flag bytes),
+                                       1 = no pre-pass (every tile fetched; all -inf wave blocks still skipped) */
 };
 int fattn_set_option(int option, int value);
 

@@ -323,17 +323,20 @@ def test_pf_predequant_bitexact(dev, kt):
     assert attn_rel_err(a, p.oracle()) <= RTOL
 
 
+@pytest.mark.parametrize("skip", [0, 1], ids=["range", "noprepass"])
 @pytest.mark.parametrize("kt", ["q8_0", "f16"])
-def test_pf_causal_block_skip(dev, kt):
+def test_pf_causal_block_skip(dev, kt, skip):
     """Causal prefill (n_q = N = 1024, 8 heads): the prefill kernel skips every
     wave's fully masked 32 x 64 blocks; against the multi-query / split kernel
     (no skipping) and one head against the oracle."""
     p = make_problem(D=128, NQ=1024, H=8, N=1024, kv_type=kt, mask="causal", seed=43)
     fattn.set_option(fattn.OPT_PF, 2)
+    fattn.set_option(fattn.OPT_PF_SKIP, skip)
     try:
         a = run_gpu(p)
     finally:
         fattn.set_option(fattn.OPT_PF, 0)
+        fattn.set_option(fattn.OPT_PF_SKIP, 0)
     fattn.set_option(fattn.OPT_PF, 1)
     try:
         b = run_gpu(p)
