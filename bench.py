@@ -183,6 +183,7 @@ def main():
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--pf-dequant", type=int, default=0,
                     help="quantised prefill: 0 auto, 1 in-kernel dequantisation, 2 f16 pre-pass")
+    ap.add_argument("--no-mq", action="store_true", help="never pick the multi-query kernel (split-KV kernel only)")
     ap.add_argument("--split-prio", type=int, default=0,
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
     ap.add_argument("--pf-pipe", type=int, default=0,
@@ -212,6 +213,8 @@ def main():
         fattn.set_option(fattn.OPT_PF_WAVES, args.pf_waves)
     if args.pf_dequant:
         fattn.set_option(fattn.OPT_PF_DEQUANT, args.pf_dequant)
+    if args.no_mq:
+        fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
     if args.split_prio:
         fattn.set_option(fattn.OPT_SPLIT_PRIO, args.split_prio)
     if args.pf_pipe:
@@ -335,13 +338,15 @@ def main():
     achieved = bytes_step / (kern_ms_avg * 1e-3) / 1e9
     achieved_tf = flops_step / (kern_ms_avg * 1e-3) / 1e12
     # which kernel the planner picks (fattn_api.hip make_plan): the multi-query
-    # kernel for quantised K/V with >= 32 query rows per kv head (16-B layout)
+    # kernel for quantised K/V with >= 256 packed rows per kv head (16-B layout)
     rk2 = H // Hkv
-    mq = (args.kv_type != "f16" and args.layout == "head" and NQ * rk2 >= 32 and rk2 <= 64
-          and rk2 & (rk2 - 1) == 0 and N % 32 == 0)
-    # the prefill kernel replaces it when the 256-row workgroups fill the chip
-    pf = (mq and args.pf != 1 and D == 128 and args.kv_chunk <= 0 and N % 64 == 0 and
+    heads_ok = NQ * rk2 >= 32 and rk2 <= 64 and rk2 & (rk2 - 1) == 0
+    mq_ok = (not args.no_mq and args.kv_type != "f16" and args.layout == "head" and heads_ok and N % 32 == 0)
+    pf_ok = mq_ok or (not args.no_mq and args.kv_type == "f16" and args.layout == "head" and heads_ok)
+    # the prefill kernel takes it when the 256-row workgroups fill the chip
+    pf = (pf_ok and args.pf != 1 and D == 128 and args.kv_chunk <= 0 and N % 64 == 0 and
           (args.pf == 2 or Hkv * ((NQ * rk2 + 255) // 256) >= 256))
+    mq = mq_ok and NQ * rk2 >= 256 and not pf
     kname = (f"fattn_pf_kernel<{args.kv_type},D{D}>" if pf else f"fattn_mq_kernel<{args.kv_type},D{D}>" if mq
              else f"fattn_split_kernel<{args.kv_type},{args.kv_type},D{D}>")
     # compute-bound once arithmetic intensity passes the ridge (peak flops / peak bytes)

@@ -36,6 +36,7 @@ int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
 int g_opt_pf_stagger = 2;
 int g_opt_pf_waves = 8;
 int g_opt_pf_dequant = 0;  // 0 auto, 1 in the prefill kernel, 2 pre-pass to f16 rows
+int g_opt_mq_min_rows = 256;  // multi-query kernel from this many packed rows per kv head (>= 32)
 int g_opt_pf_no_skip = 0;     // 1: masked prefill without the live-block pre-pass (FATTN_OPT_PF_SKIP)
 int g_opt_split_prio = 0;     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
 int g_opt_no_wave_merge = 0;  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
@@ -330,8 +331,11 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // many query rows per kv head (batched decode, prefill): the multi-query
     // kernel dequantises each K/V tile once for 64 rows.  Whole head groups
     // are packed (R = rk2, a power of two <= 64).
-    pl.mq = !g_opt_mq_disable && is_quant(k.type) && g16 && NQ * a.rk2 >= 32 && a.rk2 <= 64 &&
-            (a.rk2 & (a.rk2 - 1)) == 0;
+    // (below 256 packed rows per kv head the split kernel measures faster:
+    // config 5, 64 rows, 15.5 vs 37.6 us at 4 heads; FATTN_OPT_MQ_MIN_ROWS)
+    const bool mq_ok = !g_opt_mq_disable && is_quant(k.type) && g16 && NQ * a.rk2 >= 32 && a.rk2 <= 64 &&
+                       (a.rk2 & (a.rk2 - 1)) == 0;
+    pl.mq = mq_ok && NQ * a.rk2 >= g_opt_mq_min_rows;
     if (pl.mq) {
         // 256 rows per workgroup once that still gives one workgroup per CU
         const int64_t wg256 = Hkv * S * ((NQ * a.rk2 + 255) / 256);
@@ -349,7 +353,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     pl.pf_pre = false;
     const bool heads_ok = NQ * a.rk2 >= 32 && a.rk2 <= 64 && (a.rk2 & (a.rk2 - 1)) == 0;
     const bool pf_f16 = !g_opt_mq_disable && k.type == FATTN_TYPE_F16 && !v_trans && g16 && heads_ok;
-    if ((pl.mq || pf_f16) && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
+    if ((mq_ok || pf_f16) && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
         p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= kCUs)) {
         pl.pf = true;
         pl.mq = false;
@@ -604,6 +608,10 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_PF_DEQUANT:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_dequant = value;
+            return FATTN_OK;
+        case FATTN_OPT_MQ_MIN_ROWS:
+            if (value < 32) return FATTN_ERR_INVALID_ARG;
+            g_opt_mq_min_rows = value;
             return FATTN_OK;
         case FATTN_OPT_PF_SKIP:
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;

@@ -47,6 +47,7 @@ OPT_PF_PIPE = 9
 OPT_SPLIT_WAVE_MERGE = 10
 OPT_SPLIT_PRIO = 11
 OPT_PF_SKIP = 12
+OPT_MQ_MIN_ROWS = 13
 
 
 class FattnError(RuntimeError):

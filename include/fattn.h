@@ -139,7 +139,9 @@ enum {
     FATTN_OPT_PF_SKIP = 12          /* masked prefill: 0 = a pre-pass flags the blocks with any key above -inf
                                        and the kernel walks only the live KV range, longest query tiles
                                        first (default; the workspace holds n_qt * N/64 flag bytes),
-                                       1 = no pre-pass (every tile fetched; all -inf wave blocks still skipped) */
+                                       1 = no pre-pass (every tile fetched; all -inf wave blocks still skipped) */,
+    FATTN_OPT_MQ_MIN_ROWS = 13      /* multi-query kernel only from this many packed (query x head) rows per kv
+                                       head (default 256, minimum 32); fewer rows take the split-KV kernel */
 };
 int fattn_set_option(int option, int value);
 

@@ -99,6 +99,15 @@ def test_config5_full_batch64(dev):
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
+@pytest.fixture
+def mq_on():
+    """The multi-query kernel from 32 packed rows per kv head (the planner's
+    default threshold is 256; below it the split kernel is faster)."""
+    fattn.set_option(fattn.OPT_MQ_MIN_ROWS, 32)
+    yield
+    fattn.set_option(fattn.OPT_MQ_MIN_ROWS, 256)
+
+
 MQ_CASES = [
     dict(D=128, kv_type="q8_0", NQ=256, H=4, Hkv=4, N=256, mask="causal"),      # prefill, no split
     dict(D=64, kv_type="q4_0", NQ=256, H=4, Hkv=4, N=256, mask="causal"),
@@ -113,7 +122,7 @@ MQ_CASES = [
 
 
 @pytest.mark.parametrize("case", MQ_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
-def test_mq_sweep(dev, case):
+def test_mq_sweep(dev, mq_on, case):
     p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
@@ -136,19 +145,19 @@ MQ64_CASES = [
 
 
 @pytest.mark.parametrize("case", MQ64_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
-def test_mq_rpw64_sweep(dev, rpw64, case):
+def test_mq_rpw64_sweep(dev, mq_on, rpw64, case):
     p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
 @pytest.mark.parametrize("chunk", [64, 1000])
-def test_mq_rpw64_split(dev, rpw64, chunk):
+def test_mq_rpw64_split(dev, mq_on, rpw64, chunk):
     """256-row workgroups with split-KV partials (16 subtiles merged per tile)."""
     p = make_problem(D=128, NQ=260, H=2, N=1024, kv_type="q8_0", seed=23)
     assert attn_rel_err(run_gpu(p, kv_chunk=chunk), p.oracle()) <= RTOL
 
 
-def test_mq_matches_split_kernel(dev):
+def test_mq_matches_split_kernel(dev, mq_on):
     """The two kernels on one problem (multi-query vs split-KV forced)."""
     p = make_problem(D=128, NQ=64, H=4, Hkv=2, N=512, kv_type="q4_0", seed=24)
     a = run_gpu(p)
@@ -162,20 +171,20 @@ def test_mq_matches_split_kernel(dev):
 
 
 @pytest.mark.parametrize("chunk", [32, 96, 512, 100000])
-def test_mq_chunking_invariance(dev, chunk):
+def test_mq_chunking_invariance(dev, mq_on, chunk):
     p = make_problem(D=128, NQ=48, H=8, Hkv=2, N=1024, kv_type="q8_0", seed=17)
     assert attn_rel_err(run_gpu(p, kv_chunk=chunk), p.oracle()) <= RTOL
 
 
 @pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
-def test_mq_extreme_rescale(dev, kt):
+def test_mq_extreme_rescale(dev, mq_on, kt):
     p = make_problem(D=128, NQ=64, H=2, N=1024, kv_type=kt, seed=18, extreme=True)
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
 @pytest.mark.parametrize("rpw", [0, 32])
 @pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
-def test_mq_rescale_ramp(dev, kt, rpw):
+def test_mq_rescale_ramp(dev, mq_on, kt, rpw):
     """Scores rising along the sequence: many deferred-max steps and rescales."""
     fattn.set_option(fattn.OPT_MQ_ROWS_PER_WAVE, rpw)
     try:
@@ -186,7 +195,7 @@ def test_mq_rescale_ramp(dev, kt, rpw):
     assert attn_rel_err(got, p.oracle()) <= RTOL
 
 
-def test_mq_fully_masked_rows_are_nan(dev):
+def test_mq_fully_masked_rows_are_nan(dev, mq_on):
     p = make_problem(D=128, NQ=40, H=2, N=256, kv_type="q4_0", mask="zero", seed=19)
     m = orc.f16_bits_to_f32(p.mask_bits)
     m[5, :] = -np.inf
