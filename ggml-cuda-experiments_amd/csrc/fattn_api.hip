@@ -88,6 +88,7 @@ Geom geom(int kt, int vt, int D) {
         if (vt == VT_F16T) return geom_of<FATTN_TYPE_F16, VT_F16T, DD>();
         return geom_of<FATTN_TYPE_F16, FATTN_TYPE_F16, DD>();
     };
+    if (D == 256) return pick(std::integral_constant<int, 256>());
     return D == 128 ? pick(std::integral_constant<int, 128>()) : pick(std::integral_constant<int, 64>());
 }
 
@@ -110,7 +111,7 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     const Geom G = geom(pl.kt, pl.vt, pl.D);
     const int quantum = kStep * kSplitWaves;
     const int64_t steps = (N + kStep - 1) / kStep;
-    const int vgpr_wgs = (pl.kt == FATTN_TYPE_F16 || pl.gran == 4) ? 2 : 4;  // __launch_bounds__ waves/SIMD
+    const int vgpr_wgs = (pl.kt == FATTN_TYPE_F16 || pl.gran == 4 || pl.D == 256) ? 2 : 4;  // __launch_bounds__ waves/SIMD
     const int rv_max = std::min<int64_t>(kRows, (int64_t)a.R * std::min<int64_t>(a.QPT, NQ));
     int spw = 1, nbuf = 1;
     if (kv_chunk > 0) {
@@ -239,7 +240,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     const fattn_tensor &q = p->q, &k = p->k, &v = p->v, &mk = p->mask;
     if (q.type != FATTN_TYPE_F32 || q.nb[0] != 4) return FATTN_ERR_UNSUPPORTED_TYPE;
     const int64_t D = q.ne[0];
-    if (D != 64 && D != 128) return FATTN_ERR_UNSUPPORTED_HEAD_DIM;
+    if (D != 64 && D != 128 && D != 256) return FATTN_ERR_UNSUPPORTED_HEAD_DIM;
     if (k.ne[0] != D || v.ne[0] != D) return FATTN_ERR_INVALID_ARG;
     const int64_t NQ = q.ne[1], H = q.ne[2], S = q.ne[3];
     const int64_t N = k.ne[1], Hkv = k.ne[2], Skv = k.ne[3];
@@ -333,7 +334,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // are packed (R = rk2, a power of two <= 64).
     // (below 256 packed rows per kv head the split kernel measures faster:
     // config 5, 64 rows, 15.5 vs 37.6 us at 4 heads; FATTN_OPT_MQ_MIN_ROWS)
-    const bool mq_ok = !g_opt_mq_disable && is_quant(k.type) && g16 && NQ * a.rk2 >= 32 && a.rk2 <= 64 &&
+    const bool mq_ok = !g_opt_mq_disable && is_quant(k.type) && g16 && D <= 128 && NQ * a.rk2 >= 32 && a.rk2 <= 64 &&
                        (a.rk2 & (a.rk2 - 1)) == 0;
     pl.mq = mq_ok && NQ * a.rk2 >= g_opt_mq_min_rows;
     if (pl.mq) {
@@ -551,10 +552,12 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
     }
-    if (pl.mq) {
-        if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_mq<FATTN_TYPE_Q8_0, D>(pl, st, ev);
-        if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_mq<FATTN_TYPE_Q4_0, D>(pl, st, ev);
-        return FATTN_ERR_UNSUPPORTED_TYPE;
+    if constexpr (D <= 128) {
+        if (pl.mq) {
+            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_mq<FATTN_TYPE_Q8_0, D>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_mq<FATTN_TYPE_Q4_0, D>(pl, st, ev);
+            return FATTN_ERR_UNSUPPORTED_TYPE;
+        }
     }
     if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_gran<FATTN_TYPE_Q8_0, FATTN_TYPE_Q8_0, D>(pl, st, ev);
     if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_gran<FATTN_TYPE_Q4_0, FATTN_TYPE_Q4_0, D>(pl, st, ev);
@@ -648,7 +651,7 @@ const char* fattn_strerror(int s) {
         case FATTN_OK: return "ok";
         case FATTN_ERR_INVALID_ARG: return "invalid argument";
         case FATTN_ERR_UNSUPPORTED_TYPE: return "unsupported tensor type";
-        case FATTN_ERR_UNSUPPORTED_HEAD_DIM: return "unsupported head dim (64, 128)";
+        case FATTN_ERR_UNSUPPORTED_HEAD_DIM: return "unsupported head dim (64, 128, 256)";
         case FATTN_ERR_BAD_STRIDE: return "unsupported strides / layout";
         case FATTN_ERR_WORKSPACE: return "workspace too small";
         case FATTN_ERR_LAUNCH: return "HIP launch failed";
@@ -698,6 +701,7 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
     Events ev;
     ev.begin = (hipEvent_t)ev_begin;
     ev.end = (hipEvent_t)ev_end;
+    if (pl.D == 256) return launch_types<256>(pl, st, ev);
     return pl.D == 128 ? launch_types<128>(pl, st, ev) : launch_types<64>(pl, st, ev);
 }
 

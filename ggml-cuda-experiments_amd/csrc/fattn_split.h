@@ -576,7 +576,7 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
 }
 
 template <int KT, int VT, int D, int GRAN, bool HM>
-__global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4) ? 2 : 4) void fattn_split_kernel(
+__global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || D == 256) ? 2 : 4) void fattn_split_kernel(
     const SplitArgs a) {
     using C = SplitCfg<KT, VT, D>;
     using P = StepPlan<KT, VT, D, GRAN>;

@@ -67,7 +67,7 @@ def test_single_chunk_needs_no_workspace():
 
 
 @pytest.mark.parametrize("bad", [
-    dict(D=96), dict(D=256), dict(H=30, Hkv=8), dict(N=0), dict(kt=fattn.TYPE_F32), dict(kt=5),
+    dict(D=96), dict(D=80), dict(D=512), dict(H=30, Hkv=8), dict(N=0), dict(kt=fattn.TYPE_F32), dict(kt=5),
 ])
 def test_rejects_invalid(bad):
     p = _params(**bad)

@@ -422,6 +422,12 @@ for D in (64, 128):
         CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=5, H=32, Hkv=1, N=64, mask="neginf_blocks"))
         CASES.append(dict(D=D, kv_type=kt, layout="pos", NQ=1, H=2, Hkv=2, N=1, mask="random"))
         CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=4, H=2, Hkv=2, N=33, mask="random", S=3))
+# head_dim 256: split-KV kernel only
+for kt in ("f16", "q8_0", "q4_0"):
+    for layout in ("head", "pos", "padded"):
+        CASES.append(dict(D=256, kv_type=kt, layout=layout, NQ=1, H=4, Hkv=4, N=512, mask="random"))
+    CASES.append(dict(D=256, kv_type=kt, layout="head", NQ=9, H=8, Hkv=2, N=300, mask="causal"))
+    CASES.append(dict(D=256, kv_type=kt, layout="head", NQ=1, H=2, Hkv=2, N=4096, mask="random"))  # chunk merge
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
