@@ -60,7 +60,7 @@ enum fattn_status {
     FATTN_OK = 0,
     FATTN_ERR_INVALID_ARG = -1,     /* NULL pointer, bad shape, ne not divisible */
     FATTN_ERR_UNSUPPORTED_TYPE = -2,
-    FATTN_ERR_UNSUPPORTED_HEAD_DIM = -3,
+    FATTN_ERR_UNSUPPORTED_HEAD_DIM = -3,  /* D must be 64, 128 or 256 (256: split-KV kernel only) */
     FATTN_ERR_BAD_STRIDE = -4,       /* layout the kernels cannot address */
     FATTN_ERR_WORKSPACE = -5,        /* workspace too small */
     FATTN_ERR_LAUNCH = -6,           /* HIP launch failure */
