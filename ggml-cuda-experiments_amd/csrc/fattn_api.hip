@@ -122,18 +122,19 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
             spw++;
         }
     } else {
-        // Quantised K/V: about one 4-wave workgroup per CU, each wave streaming
-        // its slice with two steps in flight -- the measured optimum on the
-        // decode shapes (config 3: 4 steps per wave, config 4: 2), which also
-        // keeps the chunk count per tile (the cross-workgroup merge) small.
-        // f16 (one step in flight): every wave's work co-resident.
-        if (pl.kt != FATTN_TYPE_F16) {
+        // About one 4-wave workgroup per CU, each wave streaming its slice with
+        // two steps in flight -- the measured optimum on the decode shapes
+        // (config 3: 4 steps per wave, config 4: 2, config 2 (f16): 2 -- 10.3
+        // vs 11.9 us at one step), which also keeps the chunk count per tile
+        // (the cross-workgroup merge) small.  Fewer in flight where LDS is short.
+        {
             const int64_t total = steps * Y * S;
             spw = (int)std::max<int64_t>(1, (total + (int64_t)kCUs * kSplitWaves / 2) / ((int64_t)kCUs * kSplitWaves));
             spw = (int)std::min<int64_t>(spw, (steps + kSplitWaves - 1) / kSplitWaves);
         }
         for (;;) {
-            nbuf = (spw == 1 || pl.kt == FATTN_TYPE_F16) ? 1 : 2;
+            nbuf = spw == 1 ? 1 : 2;
+            while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
             const int wgs_cu = std::max(1, std::min(vgpr_wgs, kLdsPerCU / G.lds_bytes(nbuf)));
             const int64_t slots = (int64_t)kCUs * wgs_cu * kSplitWaves;
             const int64_t need = (int64_t)((steps + spw - 1) / spw) * Y * S;  // waves at this spw
@@ -143,10 +144,12 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
             spw++;
         }
     }
-    nbuf = std::min(spw, (pl.kt == FATTN_TYPE_F16) ? 1 : 2);
+    nbuf = std::min(spw, 2);
+    while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
     if (kv_chunk <= 0 && g_opt_split_spw > 0) {
         spw = (int)std::min<int64_t>(g_opt_split_spw, (steps + kSplitWaves - 1) / kSplitWaves);
         nbuf = std::min(spw, 2);
+        while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
         const int64_t nch = (N + (int64_t)spw * quantum - 1) / ((int64_t)spw * quantum);
         if (nch > 1 && !combine_ok(nch, rv_max, pl.D)) return FATTN_ERR_INVALID_ARG;
     }
