@@ -1,25 +1,33 @@
 #!/usr/bin/env python3
 """Benchmark the hot path: Q8_0-KV flash-decoding attention on MI355X.
 
-Workload (BASELINE.json metric "attn TFLOPS & HBM GB/s per GPU; head_dim=128
-seq=4096 Q8_0 KV", configs[2]): 32 heads, head_dim 128, KV length 4096, one
-query row, Q8_0 K and V in ggml block layout (per-head contiguous), f16 mask
-row, f32 Q / O.  One step = one FLASH_ATTN_EXT call (split-KV kernel + combine)
-over one sequence.  Each step reads a different one of R independent KV caches
-(R * 35.7 MB > the 256 MiB Infinity Cache), so the number is HBM, not cache.
+One GPU (default; BASELINE.json metric "attn TFLOPS & HBM GB/s per GPU;
+head_dim=128 seq=4096 Q8_0 KV", configs[2]): 32 heads, head_dim 128, KV length
+4096, one query row, Q8_0 K and V in ggml block layout (per-head contiguous),
+f16 mask row, f32 Q / O.  One step = one FLASH_ATTN_EXT call (one launch: the
+split-KV chunk merge is fused) over the whole problem.  Each step reads a
+different one of R independent KV caches (R * 35.7 MB > the 256 MiB Infinity
+Cache), so the number is HBM, not cache.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): heads x batch
-shard embarrassingly; every rank decodes its own sequence (weak scaling), the
-data path has no collective, and after the K timed steps the ranks' outputs are
-collected with ONE RCCL all_gather over xGMI (inside the timed region).
+N GPUs (`--gpus N`, or launched by torch.distributed.run): BASELINE.json
+configs[4] -- n_q = 64 query rows, 32 heads, N = 4096, Q8_0 -- head-sharded
+(SURVEY.md §8e): rank r owns kv heads [r*Hkv/N, (r+1)*Hkv/N) and their q heads
+(fattn.shard.shard_heads / head_views, zero-copy slices of the same global
+problem on every rank), runs the unchanged single-GPU kernel on its slice, and
+after the K timed steps the ranks' outputs meet in ONE RCCL all_gather over
+xGMI (inside the timed region) plus the permute into the ggml dst layout.
+Total work is fixed as N grows: "scaling": "strong".  The line also carries
+the per-step gather cost and kernel+gather per step, measured separately
+(kernel-only and kernel+gather reported apart).  `--gpus N` with
+no launcher starts N child ranks itself (before touching the GPU).
 
-Prints ONE JSON line (rank 0).  `value` = whole-job algorithmic bytes / time
-(GB/s); `roofline` prices the dominant kernel (fattn_split_kernel) from HIP
-events around that kernel alone; `cpu_baseline` times the reference's own CPU
-oracle (src/utils.h compiled from /root/reference into oracle/_ref) on a bounded
-sample of the same workload; `prefill` (N=1) prices fattn_pf_kernel against
-the dense f16 MFMA peak on the compute-bound prefill shape (n_q = N = 4096,
-north_star's MFMA-utilisation target), 5 graph-captured launches.
+Prints ONE JSON line (rank 0).  `value` = whole-job algorithmic bytes / wall
+time (GB/s); `roofline` prices the dominant kernel from HIP events on its
+launch stream; `cpu_baseline` times the reference's own CPU oracle
+(src/utils.h compiled from /root/reference into oracle/_ref) on the host
+cores, single-thread and on the box's thread share, median of >= 5 runs;
+`prefill` (N=1) prices fattn_pf_kernel against the dense f16 MFMA peak on the
+compute-bound prefill shape (n_q = N = 4096, north_star's MFMA target).
 """
 from __future__ import annotations
 
@@ -27,6 +35,9 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -36,6 +47,13 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_F16_PEAK_TFLOPS = 2500.0
+METRIC = "attn TFLOPS & HBM GB/s per GPU; head_dim=128 seq=4096 Q8_0 KV"
+
+# BASELINE.json configs used as bench workloads (the others are parity cases)
+WORKLOADS = {
+    "config3": dict(kv_type="q8_0", heads=32, kv_heads=32, kv_len=4096, n_q=1, head_dim=128),
+    "config5": dict(kv_type="q8_0", heads=32, kv_heads=32, kv_len=4096, n_q=64, head_dim=128),
+}
 
 
 def hip_events(n):
@@ -55,12 +73,23 @@ def hip_events(n):
     return hip, evs
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds: float, threads: int):
-    """The reference's CPU oracle (kernel_test.h:50-62 calling src/utils.h, built
-    from /root/reference into oracle/_ref) on the config-3 shape with the Q8_0
-    K/V dequantised to f32 beforehand (dequant not timed).  Repeats the whole
-    32-head problem until `seconds` elapse (at least once)."""
-    import numpy as np
+    """The reference's CPU oracle (kernel_test.h:50-62 calling src/utils.h:5-49,
+    built from /root/reference into oracle/_ref; the restated oracle when that
+    library is absent) on the config-3 shape, Q8_0 K/V dequantised to f32
+    beforehand (not timed).  Two modes: (i) one thread, exactly the
+    reference's loops; (ii) heads split over `threads` threads.  Each mode:
+    the whole 32-head problem repeated >= 5 times within ~seconds/2; median."""
     from oracle import oracle as orc
     D, H, Hkv, N = 128, 32, 32, 4096
     kind = "reference" if orc.ref_available() else "port"
@@ -68,28 +97,57 @@ def cpu_baseline(seconds: float, threads: int):
     q, k, v, m = (orc.random(n) for n in (D * H, D * N * Hkv, D * N * Hkv, N))
     kq = orc.dequantize(orc.quantize(k.reshape(-1, D), orc.TYPE_Q8_0), orc.TYPE_Q8_0, D).reshape(-1)
     vq = orc.dequantize(orc.quantize(v.reshape(-1, D), orc.TYPE_Q8_0), orc.TYPE_Q8_0, D).reshape(-1)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        orc.kernel_test_cpu(q, kq, vq, m, N, D, H, Hkv, impl="ref" if kind == "reference" else "oracle",
-                            n_threads=threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
     bytes_per = (D * H * 4) * 2 + 2 * Hkv * N * (D // 32 * 34) + N * 2
-    return {"value": round(bytes_per * reps / el / 1e9, 4), "unit": "GB/s", "cores": threads if kind == "reference" else 1,
-            "kind": kind,
-            "sample": f"{reps} x full config-3 problem (32 heads x 4096 x 128, Q8_0 K/V dequantised untimed), "
-                      f"{el:.1f} s, heads split over {threads} threads, reference src/utils.h loops",
-            "ms_per_problem": round(el / reps * 1e3, 2), "host_cpu": _cpu_model()}
+
+    def mode(nt):
+        runs, t_all = [], time.perf_counter()
+        while len(runs) < 5 or (time.perf_counter() - t_all < seconds / 2 and len(runs) < 200):
+            t0 = time.perf_counter()
+            orc.kernel_test_cpu(q, kq, vq, m, N, D, H, Hkv, impl="ref" if kind == "reference" else "oracle",
+                                n_threads=nt)
+            runs.append(time.perf_counter() - t0)
+        med = statistics.median(runs)
+        return {"value": round(bytes_per / med / 1e9, 4), "unit": "GB/s", "cores": nt, "runs": len(runs),
+                "ms_per_problem_median": round(med * 1e3, 2)}
+
+    single = mode(1)
+    multi = mode(threads)
+    return {**multi, "kind": kind,
+            "sample": f"full config-3 problem (32 heads x 4096 x 128, Q8_0 K/V dequantised untimed), median of "
+                      f"{multi['runs']} runs, heads split over {threads} threads (the box's thread share: "
+                      f"OMP_NUM_THREADS; nproc reports the whole host), reference src/utils.h loops",
+            "single_thread": single, "nproc": os.cpu_count(), "host_cpu": _cpu_model()}
 
 
-def prefill_measure(dev, hip, evs, kvn="q8_0", pf_dequant=0, pf_pipe=0, causal=False, steps=5):
+def measured_copy_peak(dev):
+    """Measured HBM ceiling for the roofline's secondary fraction: a 1 GiB
+    device-to-device copy (torch's copy kernel), read + write bytes / time,
+    median of 10 (fraction against a measured copy-kernel peak)."""
+    import torch
+    n = 1 << 30
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty(n, dtype=torch.uint8, device=dev)
+    a.fill_(1)
+    ts = []
+    for _ in range(12):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    del a, b
+    ms = statistics.median(ts[2:])
+    return round(2 * n / (ms * 1e-3) / 1e9, 1)
+
+
+def prefill_measure(dev, hip, evs, kvn="q8_0", causal=False, steps=5):
     """The MFMA-bound prefill shape of SURVEY.md §8d (n_q = N = 4096, 32 heads,
-    head_dim 128, Q8_0 K/V, random f16 mask, non-causal): `steps` launches of
-    fattn_pf_kernel captured in one HIP graph, HIP events around the replay on
-    the launch stream.  Two rotated KV caches (compute-bound: the cache state
-    barely matters).  Returns the TFLOP/s roofline object."""
+    head_dim 128, Q8_0 K/V, random f16 mask, non-causal): `steps` launches
+    captured in one HIP graph, HIP events around the replay on the launch
+    stream.  Two rotated KV caches (compute-bound: the cache state barely
+    matters).  The masked form's live-block flag pass (pf_mask_flags_kernel)
+    and the flag re-zeroing are inside the timed region."""
     import torch
     import fattn
     D, H, N, NQ, R = 128, 32, 4096, 4096, 2
@@ -141,99 +199,109 @@ def prefill_measure(dev, hip, evs, kvn="q8_0", pf_dequant=0, pf_pipe=0, causal=F
     pairs = NQ * (NQ + 1) // 2 if causal else NQ * N
     flops = 4 * pairs * D * H
     tf = flops / (ms * 1e-3) / 1e12
-    pre = kvn != "f16" and pf_dequant == 2
-    f16k = "fattn_pfp_kernel<f16,D128>" if pf_pipe == 2 else "fattn_pf_kernel<f16,D128>"
-    kname = (f"pf_dequant_rows_kernel<{kvn}> x2 + {f16k}" if pre
-             else f16k if kvn == "f16" else f"fattn_pf_kernel<{kvn},D128>")
-    return {"workload": f"prefill_{kvn}_h{H}_d{D}_n{N}_q{NQ}_{'causal' if causal else 'mask'}", "kernel": kname,
-            "kernel_ms_avg": round(ms, 5), "flops_per_step": flops,
+    return {"workload": f"prefill_{kvn}_h{H}_d{D}_n{N}_q{NQ}_{'causal' if causal else 'mask'}",
+            "kernel": att.describe(), "kernel_ms_avg": round(ms, 5), "flops_per_step": flops,
             "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None}}
 
 
-def _cpu_model():
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
-
-
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="auto", choices=["auto", "config3", "config5"],
+                    help="auto: config3 on one GPU, config5 (head-sharded) on several")
     ap.add_argument("--rotate", type=int, default=16, help="independent KV caches cycled through")
-    ap.add_argument("--kv-type", default="q8_0", choices=["q8_0", "q4_0", "f16"])
-    ap.add_argument("--heads", type=int, default=32)
-    ap.add_argument("--kv-heads", type=int, default=0)
-    ap.add_argument("--kv-len", type=int, default=4096)
-    ap.add_argument("--n-q", type=int, default=1)
-    ap.add_argument("--head-dim", type=int, default=128)
+    ap.add_argument("--kv-type", default=None, choices=["q8_0", "q4_0", "f16"])
+    ap.add_argument("--heads", type=int, default=None)
+    ap.add_argument("--kv-heads", type=int, default=None)
+    ap.add_argument("--kv-len", type=int, default=None)
+    ap.add_argument("--n-q", type=int, default=None)
+    ap.add_argument("--head-dim", type=int, default=None)
     ap.add_argument("--layout", default="head", choices=["head", "pos"])
     ap.add_argument("--kv-chunk", type=int, default=0)
     ap.add_argument("--spw", type=int, default=0, help="split kernel: steps per wave (0 = planner)")
     ap.add_argument("--inflight", type=int, default=0, help="split kernel: steps in flight per wave (0 = planner)")
     ap.add_argument("--no-mask", action="store_true", help="no mask tensor (diagnostics; the metric uses a mask)")
     ap.add_argument("--pf-stagger", type=int, default=2)
-    ap.add_argument("--pf-waves", type=int, default=0, help="prefill kernel waves (4 or 8; 0 = library default)")
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
-    ap.add_argument("--pf-dequant", type=int, default=0,
-                    help="quantised prefill: 0 auto, 1 in-kernel dequantisation, 2 f16 pre-pass")
     ap.add_argument("--no-mq", action="store_true", help="never pick the multi-query kernel (split-KV kernel only)")
     ap.add_argument("--split-prio", type=int, default=0,
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
-    ap.add_argument("--pf-pipe", type=int, default=0,
-                    help="prefill over f16 images: 0 auto, 1 fattn_pf_kernel, 2 software-pipelined fattn_pfp_kernel")
+    ap.add_argument("--dec", type=int, default=0,
+                    help="split-KV decode: 0 auto (loader-wave kernel), 1 split kernel only, 2 loader kernel")
+    ap.add_argument("--dec-loaders", type=int, default=0, help="loader waves per decode workgroup (1, 2; 0 = default)")
+    ap.add_argument("--dec-compute", type=int, default=0, help="compute waves per decode workgroup (4, 8; 0 = default)")
+    ap.add_argument("--dec-diag", type=int, default=0, help="decode diagnostics: 1 no compute, 2 no DMA")
+    ap.add_argument("--dec-ahead", type=int, default=0, help="decode: steps in flight per loader wave (0 = default)")
+    ap.add_argument("--wave-merge", type=int, default=-1, help="split/dec one-row tiles: 0 per-wave merge, 1 LDS merge")
     ap.add_argument("--prefill-causal", action="store_true",
                     help="causal mask on the prefill measurement (fully masked blocks are skipped)")
     ap.add_argument("--prefill-kv", default="q8_0", choices=["q8_0", "q4_0", "f16"],
                     help="K/V type of the prefill measurement (the metric's is q8_0)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS, else os.cpu_count()")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefill", action="store_true", help="skip the prefill-shape MFMA measurement")
-    args = ap.parse_args()
+    ap.add_argument("--no-scale-ref", action="store_true", help="N=1: skip the config-5 strong-scaling reference")
+    ap.add_argument("--no-copy-peak", action="store_true", help="skip the measured copy-kernel peak")
+    return ap.parse_args(argv)
 
+
+def apply_options(args):
+    import fattn
+    opts = [(args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT), (args.pf, fattn.OPT_PF),
+            (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO),
+            (args.dec, fattn.OPT_DEC), (args.dec_loaders, fattn.OPT_DEC_LOADERS),
+            (args.dec_compute, fattn.OPT_DEC_COMPUTE), (args.dec_diag, fattn.OPT_DEC_DIAG),
+            (args.dec_ahead, fattn.OPT_DEC_AHEAD)]
+    for val, opt in opts:
+        if val:
+            fattn.set_option(opt, val)
+    fattn.set_option(fattn.OPT_PF_STAGGER, args.pf_stagger)
+    if args.wave_merge >= 0:
+        fattn.set_option(fattn.OPT_SPLIT_WAVE_MERGE, args.wave_merge)
+
+
+def shape_of(args, workload):
+    """The workload's shape; explicit flags override the preset."""
+    w = dict(WORKLOADS[workload])
+    for k in w:
+        v = getattr(args, k)
+        if v is not None:
+            w[k] = v
+    return w
+
+
+# FATTN_BENCH_REHEARSE=1: rehearse the multi-rank path on a one-GPU box -- every
+# rank on cuda:0, gloo instead of RCCL, collectives staged through host memory
+# (never the measured configuration: the driver's N-GPU runs use RCCL)
+REHEARSE = os.environ.get("FATTN_BENCH_REHEARSE") == "1"
+
+
+def _gather(x):
+    from fattn.shard import gather_heads
+    return gather_heads(x.cpu()).to(x.device) if REHEARSE else gather_heads(x)
+
+
+def run_decode(args, dev, shape, rank=0, world=1, tag=""):
+    """Time K steps of the decode workload `shape` (one FLASH_ATTN_EXT per step),
+    head-sharded over `world` ranks.  Returns the measurement dict (rank 0 holds
+    the max over ranks)."""
     import torch
     import torch.distributed as dist
     import fattn
+    from fattn.shard import head_views, shard_heads
 
-    if args.spw:
-        fattn.set_option(fattn.OPT_SPLIT_STEPS, args.spw)
-    if args.inflight:
-        fattn.set_option(fattn.OPT_SPLIT_INFLIGHT, args.inflight)
-    if args.pf:
-        fattn.set_option(fattn.OPT_PF, args.pf)
-    fattn.set_option(fattn.OPT_PF_STAGGER, args.pf_stagger)
-    if args.pf_waves:
-        fattn.set_option(fattn.OPT_PF_WAVES, args.pf_waves)
-    if args.pf_dequant:
-        fattn.set_option(fattn.OPT_PF_DEQUANT, args.pf_dequant)
-    if args.no_mq:
-        fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
-    if args.split_prio:
-        fattn.set_option(fattn.OPT_SPLIT_PRIO, args.split_prio)
-    if args.pf_pipe:
-        fattn.set_option(fattn.OPT_PF_PIPE, args.pf_pipe)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-
-    D, H, N, NQ = args.head_dim, args.heads, args.kv_len, args.n_q
-    Hkv = args.kv_heads or H
-    typ = fattn.TYPE_NAMES[args.kv_type]
+    D, H, N, NQ = shape["head_dim"], shape["heads"], shape["kv_len"], shape["n_q"]
+    Hkv = shape["kv_heads"] or H
+    typ = fattn.TYPE_NAMES[shape["kv_type"]]
     rb = fattn.row_size(typ, D)
     R = args.rotate
+    sh = shard_heads(H, Hkv, world, rank)
     g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
+    g.manual_seed(1234)  # the same global problem on every rank; each reads only its slice
 
     # --- synthetic inputs, resident in HBM before timing
     kv_sets = []
@@ -250,23 +318,28 @@ def main():
     q = torch.rand((1, NQ, H, D), generator=g, device=dev) * 2 - 1
     npad = (N + 63) // 64 * 64
     mask = (torch.rand((NQ, npad), generator=g, device=dev) * 2 - 1).to(torch.float16)
-    outs = torch.empty((R, 1, NQ, H, D), dtype=torch.float32, device=dev)
+    Hl = sh.n_heads
+    outs = torch.empty((R, 1, NQ, Hl, D), dtype=torch.float32, device=dev)
 
-    att = fattn.Attention(fattn.q_view(q), fattn.kv_view(kv_sets[0][0], typ, D, N, Hkv, layout=args.layout),
-                          fattn.kv_view(kv_sets[0][1], typ, D, N, Hkv, layout=args.layout),
-                          None if args.no_mask else fattn.mask_view(mask), outs[0], 1.0 / D ** 0.5,
+    qv = fattn.q_view(q)
+    kv = fattn.kv_view(kv_sets[0][0], typ, D, N, Hkv, layout=args.layout)
+    vv = fattn.kv_view(kv_sets[0][1], typ, D, N, Hkv, layout=args.layout)
+    qs, ks, vs = head_views(qv, kv, vv, sh)  # zero-copy slice (identity at world 1)
+    k_off, v_off = ks.ptr - kv.ptr, vs.ptr - vv.ptr
+    att = fattn.Attention(qs, ks, vs, None if args.no_mask else fattn.mask_view(mask), outs[0], 1.0 / D ** 0.5,
                           kv_chunk=args.kv_chunk)
+    kname = att.describe()
 
     def step(i, stream=None, ev=None):
         kvs = kv_sets[i % R]
-        att.retarget(k=kvs[0].data_ptr(), v=kvs[1].data_ptr(), dst=outs[i % R].data_ptr())
+        att.retarget(k=kvs[0].data_ptr() + k_off, v=kvs[1].data_ptr() + v_off, dst=outs[i % R].data_ptr())
         if ev is None:
             att(stream)
         else:
             att(stream, ev[0], ev[1])
 
-    # 1) dominant-kernel duration: eager launches with HIP events recorded by
-    #    libfattn around the main kernel only (not part of the timed region)
+    # 1) dominant-kernel duration, eager launches with HIP events recorded by
+    #    libfattn around the kernel (not part of the timed region): median
     n_ev = min(args.steps, 200)
     hip, evs = hip_events(2 * n_ev)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -280,16 +353,13 @@ def main():
     for i in range(n_ev):
         hip.hipEventElapsedTime(C.byref(f), evs[2 * i], evs[2 * i + 1])
         kms.append(f.value)
-    kms.sort()
-    kern_ms_avg = sum(kms) / len(kms)
+    kern_ms_median = statistics.median(kms)
 
     # 2) the timed job: the K steps (step i reads KV cache i % R) captured
-    #    back-to-back into one HIP graph -- the launch-bound inner loop lives on
-    #    the device, not in Python -- and replayed once inside the timed region.
-    #    One step is exactly one launch of fattn_split_kernel (the chunk merge is
-    #    fused), so HIP events around the replay on the launch stream give the
-    #    kernel's average in-stream duration over the timed region; it agrees
-    #    with rocprofv3's per-dispatch average (profiles/).
+    #    back-to-back into one HIP graph and replayed once inside the timed
+    #    region; at world > 1 the ranks' outputs then meet in ONE all_gather.
+    #    HIP events around the replay on the launch stream give the kernel's
+    #    average in-stream duration over the timed region.
     K = args.steps
     gs = torch.cuda.Stream(dev)
     gs.wait_stream(torch.cuda.current_stream(dev))
@@ -305,99 +375,193 @@ def main():
         graph.replay()   # untimed warm replay
     torch.cuda.synchronize()
     if world > 1:
+        _gather(outs)  # warm the communicator
         dist.barrier()
     torch.cuda.synchronize()
-    gathered = torch.empty((world,) + tuple(outs.shape), dtype=torch.float32, device=dev) if world > 1 else None
     ev0, ev1 = evs[0], evs[1]
     t0 = time.perf_counter()
     hip.hipEventRecord(ev0, gs.cuda_stream)
     with torch.cuda.stream(gs):
-        graph.replay()   # launches on the current stream: gs, between the events
+        graph.replay()
     hip.hipEventRecord(ev1, gs.cuda_stream)
     if world > 1:
-        dist.all_gather_into_tensor(gathered, outs)   # the single RCCL gather over xGMI
+        with torch.cuda.stream(gs):
+            full = _gather(outs)   # the single RCCL gather over xGMI + permute to [R][1][NQ][H][D]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-
     hip.hipEventSynchronize(ev1)
-    kern_ms_eager = kern_ms_avg
-    if hip.hipEventElapsedTime(C.byref(f), ev0, ev1) == 0:
-        kern_ms_avg = f.value / K          # in-stream average over the timed region
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms_avg], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms_avg = float(t[0]), float(t[1])
+    hip.hipEventElapsedTime(C.byref(f), ev0, ev1)
+    kern_ms_avg = f.value / K
 
-    bytes_step = (NQ * H * D * 4) * 2 + 2 * Hkv * N * rb + (0 if args.no_mask else NQ * N * 2)
-    flops_step = 4 * NQ * N * D * H
-    total_bytes = bytes_step * args.steps * world
-    value = total_bytes / elapsed / 1e9
-    achieved = bytes_step / (kern_ms_avg * 1e-3) / 1e9
-    achieved_tf = flops_step / (kern_ms_avg * 1e-3) / 1e12
-    # which kernel the planner picks (fattn_api.hip make_plan): the multi-query
-    # kernel for quantised K/V with >= 256 packed rows per kv head (16-B layout)
-    rk2 = H // Hkv
-    heads_ok = NQ * rk2 >= 32 and rk2 <= 64 and rk2 & (rk2 - 1) == 0
-    mq_ok = (not args.no_mq and args.kv_type != "f16" and args.layout == "head" and heads_ok and N % 32 == 0)
-    pf_ok = mq_ok or (not args.no_mq and args.kv_type == "f16" and args.layout == "head" and heads_ok)
-    # the prefill kernel takes it when the 256-row workgroups fill the chip
-    pf = (pf_ok and args.pf != 1 and D == 128 and args.kv_chunk <= 0 and N % 64 == 0 and
-          (args.pf == 2 or Hkv * ((NQ * rk2 + 255) // 256) >= 256))
-    mq = mq_ok and NQ * rk2 >= 256 and not pf
-    kname = (f"fattn_pf_kernel<{args.kv_type},D{D}>" if pf else f"fattn_mq_kernel<{args.kv_type},D{D}>" if mq
-             else f"fattn_split_kernel<{args.kv_type},{args.kv_type},D{D}>")
-    # compute-bound once arithmetic intensity passes the ridge (peak flops / peak bytes)
-    mfma_bound = flops_step / bytes_step > MFMA_F16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    res = {"kernel": kname, "kernel_ms_avg": kern_ms_avg, "kernel_ms_median": kern_ms_median, "elapsed": elapsed}
+    if world > 1:
+        assert tuple(full.shape) == (R, 1, NQ, H, D)
+        # 3) per-step cost of the gather, and kernel + gather per step (eager),
+        #    reported apart from the kernel (BASELINE.md multi-GPU rule)
+        one = outs[0]
+        gts, ets = [], []
+        for i in range(25):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            _gather(one)
+            torch.cuda.synchronize()
+            gts.append(time.perf_counter() - t)
+        for i in range(25):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            step(i, stream)
+            _gather(outs[i % R])
+            torch.cuda.synchronize()
+            ets.append(time.perf_counter() - t)
+        res["gather_ms_median"] = statistics.median(gts[5:]) * 1e3
+        res["step_with_gather_ms_median"] = statistics.median(ets[5:]) * 1e3
+        t = torch.tensor([elapsed, kern_ms_avg, kern_ms_median, res["gather_ms_median"],
+                          res["step_with_gather_ms_median"]], dtype=torch.float64,
+                         device="cpu" if REHEARSE else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        (res["elapsed"], res["kernel_ms_avg"], res["kernel_ms_median"], res["gather_ms_median"],
+         res["step_with_gather_ms_median"]) = (float(x) for x in t.tolist())
+    for e in evs:
+        hip.hipEventDestroy(e)
+
+    # algorithmic bytes: Q + K + V + mask + O at stored precision,
+    # each once; per rank its slice plus the (replicated) mask
+    mask_b = 0 if args.no_mask else NQ * N * 2
+    job_bytes = (NQ * H * D * 4) * 2 + 2 * Hkv * N * rb + mask_b
+    rank_bytes = (NQ * Hl * D * 4) * 2 + 2 * sh.n_kv * N * rb + mask_b
+    res.update(job_bytes=job_bytes, rank_bytes=rank_bytes, flops=4 * NQ * N * D * H, rank_flops=4 * NQ * N * D * Hl,
+               workload=f"decode_{shape['kv_type']}_h{H}_hkv{Hkv}_d{D}_n{N}_q{NQ}", shard=sh, R=R)
+    return res
+
+
+def roofline(res, args, traffic=None, copy_peak=None):
+    ach = res["rank_bytes"] / (res["kernel_ms_avg"] * 1e-3) / 1e9
+    ach_tf = res["rank_flops"] / (res["kernel_ms_avg"] * 1e-3) / 1e12
+    if res["rank_flops"] / res["rank_bytes"] > MFMA_F16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9):
+        return {"bound": "mfma", "achieved": round(ach_tf, 2), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach_tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": res["kernel"]}
+    r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": res["kernel"],
+         "frac_median_kernel": round(res["rank_bytes"] / (res["kernel_ms_median"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if copy_peak:
+        r["peak_measured_copy"] = copy_peak
+        r["frac_of_measured_copy"] = round(ach / copy_peak, 4)
+    return r
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: start N ranks through torch.distributed.run
+    as a child process (nothing here has touched the GPU) and exit with its code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def main():
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if "WORLD_SIZE" in os.environ and args.gpus not in (1, world):
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    import fattn
+
+    apply_options(args)
+    if REHEARSE:
+        local_rank = 0
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        if REHEARSE:
+            dist.init_process_group("gloo", init_method="env://")
+        else:
+            dist.init_process_group("nccl", init_method="env://", device_id=dev)
+    workload = args.workload if args.workload != "auto" else ("config3" if world == 1 else "config5")
+    shape = shape_of(args, workload)
+    res = run_decode(args, dev, shape, rank, world)
 
     if rank == 0:
         traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic_r01.json")
+        tf = os.path.join(ROOT, "profiles", "traffic_r02.json")
         if os.path.exists(tf):
             try:
                 tj = json.load(open(tf))
-                if tj.get("workload") == f"decode_{args.kv_type}_h{H}_hkv{Hkv}_d{D}_n{N}_q{NQ}":
+                if tj.get("workload") == res["workload"] and world == 1:
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        res = {
-            "metric": "attn TFLOPS & HBM GB/s per GPU; head_dim=128 seq=4096 Q8_0 KV",
+        copy_peak = None if args.no_copy_peak or world > 1 else measured_copy_peak(dev)
+        sh = res["shard"]
+        K = args.steps
+        value = res["job_bytes"] * K / res["elapsed"] / 1e9
+        line = {
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": K,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "ms_per_step": round(res["elapsed"] / K * 1e3, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f16",
             "data": "synthetic (uniform [-1,1) Q/K/V, K/V quantised on device to ggml blocks; random f16 mask)",
-            "config": {"workload": f"decode_{args.kv_type}_h{H}_hkv{Hkv}_d{D}_n{N}_q{NQ}", "heads": H,
-                       "kv_heads": Hkv, "head_dim": D, "kv_len": N, "n_q": NQ, "kv_type": args.kv_type,
-                       "kv_layout": args.layout, "kv_rotation": R, "parallelism": f"heads_x_batch_shard{world}",
-                       "bytes_per_step": bytes_step, "flops_per_step": flops_step},
-            "tflops": round(flops_step * args.steps * world / elapsed / 1e12, 4),
-            "kernel_ms_avg": round(kern_ms_avg, 5),
-            "kernel_ms_eager_avg": round(kern_ms_eager, 5),
-            "kernel_timing": "HIP events around the timed graph replay on the launch stream, / steps",
-            "roofline": ({"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": MFMA_F16_PEAK_TFLOPS,
-                          "unit": "TFLOP/s", "frac": round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic,
-                          "kernel": kname} if mfma_bound else
-                         {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname}),
+            "config": {"workload": res["workload"], "heads": shape["heads"], "kv_heads": shape["kv_heads"],
+                       "head_dim": shape["head_dim"], "kv_len": shape["kv_len"], "n_q": shape["n_q"],
+                       "kv_type": shape["kv_type"], "kv_layout": args.layout, "kv_rotation": res["R"],
+                       "parallelism": (f"head_shard_{sh.n_heads}heads_per_rank_x{world}" if world > 1
+                                       else "single_gpu"),
+                       "bytes_per_step": res["job_bytes"], "flops_per_step": res["flops"]},
+            "tflops": round(res["flops"] * K / res["elapsed"] / 1e12, 4),
+            "kernel_ms_avg": round(res["kernel_ms_avg"], 5),
+            "kernel_ms_median": round(res["kernel_ms_median"], 5),
+            "kernel_timing": "avg: HIP events around the timed graph replay on the launch stream, / steps; "
+                             "median: per-launch HIP events, eager",
+            "roofline": roofline(res, args, traffic, copy_peak),
         }
-        if world == 1 and not args.no_prefill and NQ == 1:
-            # north_star's second target: MFMA utilisation on the prefill shape
-            res["prefill"] = prefill_measure(dev, hip, evs, args.prefill_kv, args.pf_dequant, args.pf_pipe,
-                                             args.prefill_causal)
-        if world == 1 and not args.no_cpu_baseline and NQ == 1:  # kernel_test.h's CPU path is one query row
-            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, min(args.cpu_threads, os.cpu_count() or 1))
-        print(json.dumps(res), flush=True)
-    for e in evs:
-        hip.hipEventDestroy(e)
+        if world > 1:
+            if REHEARSE:
+                line["rehearsal"] = "FATTN_BENCH_REHEARSE: all ranks on one GPU, gloo, not a measurement"
+            line["per_rank"] = {"heads": sh.n_heads, "kv_heads": sh.n_kv, "bytes": res["rank_bytes"]}
+            line["gather"] = {"collective": "all_gather_into_tensor (RCCL over xGMI), once after the K steps",
+                              "per_step_gather_ms_median": round(res["gather_ms_median"], 4),
+                              "per_step_kernel_plus_gather_ms_median": round(res["step_with_gather_ms_median"], 4)}
+        if world > 1:
+            print(json.dumps(line), flush=True)
+
+    if world == 1:
+        if not args.no_scale_ref and workload == "config3":
+            # the strong-scaling reference: config 5 (the multi-GPU workload) on this one GPU
+            r5 = run_decode(args, dev, shape_of(argparse.Namespace(**{k: None for k in WORKLOADS["config5"]}),
+                                                "config5"))
+            line["strong_scaling_ref"] = {
+                "workload": r5["workload"], "value": round(r5["job_bytes"] * args.steps / r5["elapsed"] / 1e9, 2),
+                "unit": "GB/s", "ms_per_step": round(r5["elapsed"] / args.steps * 1e3, 5),
+                "kernel_ms_avg": round(r5["kernel_ms_avg"], 5), "kernel": r5["kernel"],
+                "note": "bench.py --gpus N runs this workload head-sharded; strong-scaling efficiency = "
+                        "value(N) / (N * this value)"}
+        if not args.no_prefill and shape["n_q"] == 1:
+            hip, evs = hip_events(2)
+            line["prefill"] = prefill_measure(dev, hip, evs, args.prefill_kv, args.prefill_causal)
+        if not args.no_cpu_baseline and shape["n_q"] == 1:  # kernel_test.h's CPU path is one query row
+            threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

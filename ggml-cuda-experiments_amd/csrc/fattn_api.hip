@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -17,30 +18,51 @@
 #include "fattn_quant.h"
 #include "fattn_mq.h"
 #include "fattn_pf.h"
-#include "fattn_pf4.h"
-#include "fattn_pfp.h"
 #include "fattn_split.h"
+#include "fattn_dec.h"
 
 using namespace fattn;
 
 namespace {
 
-constexpr int kCUs = 256;
+constexpr int kCUsDefault = 256;  // MI355X; used when no device can be queried (host-only planning)
+constexpr int kMaxDevices = 64;
 
-// fattn_set_option overrides
-int g_opt_mq_rpw = 0;
-int g_opt_mq_disable = 0;
-int g_opt_split_spw = 0;
-int g_opt_split_nbuf = 0;
-int g_opt_pf = 0;  // 0 auto, 1 never, 2 whenever eligible
-int g_opt_pf_stagger = 2;
-int g_opt_pf_waves = 8;
-int g_opt_pf_dequant = 0;  // 0 auto, 1 in the prefill kernel, 2 pre-pass to f16 rows
-int g_opt_mq_min_rows = 256;  // multi-query kernel from this many packed rows per kv head (>= 32)
-int g_opt_pf_no_skip = 0;     // 1: masked prefill without the live-block pre-pass (FATTN_OPT_PF_SKIP)
-int g_opt_split_prio = 0;     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
-int g_opt_no_wave_merge = 0;  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
-int g_opt_pf_pipe = 0;     // f16 images: 0 auto, 1 fattn_pf_kernel, 2 fattn_pfp_kernel
+// compute units of the current device, queried once per device
+int device_cus() {
+    static std::atomic<int> cache[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+        (void)hipGetLastError();
+        return kCUsDefault;
+    }
+    int n = cache[dev].load(std::memory_order_relaxed);
+    if (n > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        n = kCUsDefault;
+    }
+    cache[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
+
+// fattn_set_option overrides (process-wide; atomics, so a planner running on
+// another host thread never reads a torn or stale-forever value -- overrides
+// are still meant to be set before launches, by tests and benchmarks)
+std::atomic<int> g_opt_mq_rpw{0};
+std::atomic<int> g_opt_mq_disable{0};
+std::atomic<int> g_opt_split_spw{0};
+std::atomic<int> g_opt_split_nbuf{0};
+std::atomic<int> g_opt_pf{0};  // 0 auto, 1 never, 2 whenever eligible
+std::atomic<int> g_opt_pf_stagger{2};
+std::atomic<int> g_opt_mq_min_rows{256};  // multi-query kernel from this many packed rows per kv head (>= 32)
+std::atomic<int> g_opt_pf_no_skip{0};     // 1: masked prefill without the live-block pre-pass (FATTN_OPT_PF_SKIP)
+std::atomic<int> g_opt_split_prio{0};     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
+std::atomic<int> g_opt_no_wave_merge{0};  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
+std::atomic<int> g_opt_dec{1};         // split-KV decode: 0 auto (loader-wave kernel), 1 split kernel only, 2 loader kernel
+std::atomic<int> g_opt_dec_compute{4}; // compute waves per fattn_dec_kernel workgroup (4 or 8)
+std::atomic<int> g_opt_dec_diag{0};
+std::atomic<int> g_opt_dec_ahead{8};  // steps in flight per loader wave (FATTN_OPT_DEC_AHEAD)    // fattn_dec_kernel diagnostics (1 no compute, 2 no DMA)
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -53,14 +75,13 @@ struct Plan {
     dim3 grid;
     int lds;
     size_t ws_bytes, cnt_bytes, ml_bytes;
+    int cus;  // compute units of the device the plan is for
     bool mq;  // multi-query kernel (fattn_mq.h)
-    bool pf;  // prefill kernel (fattn_pf.h, or fattn_pf4.h when pf_waves == 4)
-    int pf_waves;
-    bool pf_pre;            // quantised K/V converted to f16 rows in the workspace first
-    bool pf_pipe;           // f16 images: the software-pipelined kernel (fattn_pfp.h)
+    bool dec; // split-KV decode with loader waves (fattn_dec.h)
+    int nlw;  // its loader waves
+    int ncw;  // its compute waves
+    bool pf;  // prefill kernel (fattn_pf.h)
     bool pf_flags;          // masked prefill: live-block flags pre-pass (tile-range skipping)
-    int64_t pf_rows;        // rows per converted tensor (Skv * Hkv * N)
-    int64_t hkv;            // kv heads
     int nw;   // its waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
 };
 
@@ -129,14 +150,14 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
         // (the cross-workgroup merge) small.  Fewer in flight where LDS is short.
         {
             const int64_t total = steps * Y * S;
-            spw = (int)std::max<int64_t>(1, (total + (int64_t)kCUs * kSplitWaves / 2) / ((int64_t)kCUs * kSplitWaves));
+            spw = (int)std::max<int64_t>(1, (total + (int64_t)pl.cus * kSplitWaves / 2) / ((int64_t)pl.cus * kSplitWaves));
             spw = (int)std::min<int64_t>(spw, (steps + kSplitWaves - 1) / kSplitWaves);
         }
         for (;;) {
             nbuf = spw == 1 ? 1 : 2;
             while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
             const int wgs_cu = std::max(1, std::min(vgpr_wgs, kLdsPerCU / G.lds_bytes(nbuf)));
-            const int64_t slots = (int64_t)kCUs * wgs_cu * kSplitWaves;
+            const int64_t slots = (int64_t)pl.cus * wgs_cu * kSplitWaves;
             const int64_t need = (int64_t)((steps + spw - 1) / spw) * Y * S;  // waves at this spw
             const int64_t nch = (N + (int64_t)spw * quantum - 1) / ((int64_t)spw * quantum);
             const bool reducer_ok = nch == 1 || combine_ok(nch, rv_max, pl.D);
@@ -154,7 +175,7 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
         if (nch > 1 && !combine_ok(nch, rv_max, pl.D)) return FATTN_ERR_INVALID_ARG;
     }
     if (g_opt_split_nbuf > 0) {
-        nbuf = std::min(spw, g_opt_split_nbuf);
+        nbuf = std::min(spw, (int)g_opt_split_nbuf);
         while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
     }
     a.nbuf = nbuf;
@@ -188,6 +209,69 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     return FATTN_OK;
 }
 
+// Loader-wave decode sizing (fattn_dec_kernel): about one workgroup per CU,
+// each chunk at least one step per compute wave; the chunk's steps get an LDS
+// ring of as many step images as fit (all of them on the decode shapes, so
+// every byte is requested at kernel start).
+int size_dec(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t NQ) {
+    SplitArgs& a = pl.a;
+    const Geom G = geom(pl.kt, pl.vt, pl.D);
+    const int64_t steps = (N + kStep - 1) / kStep;
+    const int64_t tiles = Y * S;
+    const int rv_max = std::min<int64_t>(kRows, (int64_t)a.R * std::min<int64_t>(a.QPT, NQ));
+    const bool wm_ok = rv_max == 1 && pl.D == 128 && !g_opt_no_wave_merge;
+    const int ncw = g_opt_dec_compute;
+    int64_t cs;  // steps per chunk
+    if (kv_chunk > 0) {
+        cs = (kv_chunk + kStep - 1) / kStep;
+    } else {
+        const int64_t nch = std::max<int64_t>(1, (pl.cus + tiles / 2) / tiles);
+        cs = (steps + nch - 1) / nch;
+        cs = std::max<int64_t>(cs, std::min<int64_t>(steps, ncw));
+    }
+    int64_t nch;
+    for (;;) {
+        nch = (steps + cs - 1) / cs;
+        const bool ok = nch == 1 || (wm_ok && nch * ncw <= kWaveMergeParts) || combine_ok(nch, rv_max, pl.D);
+        if (ok) break;
+        cs++;
+    }
+    const int nlw = 2;  // steps per chunk >= 2 (cs >= min(steps, ncw); one-step chunks: spl 0, rejected below)
+    const int step_bytes = G.step_bytes;
+    int nslot = (int)std::min<int64_t>(cs, std::min<int64_t>(kDecMaxSlots, (kLdsPerCU - kDecHdr) / step_bytes));
+    if (nslot < cs) nslot -= nslot % nlw;  // ring: equal rings per loader
+    if (nslot < nlw) return FATTN_ERR_INVALID_ARG;
+    a.nbuf = nslot;
+    a.split_prio = 0;
+    a.wave_bytes = 0;
+    a.chunk_len = (int)(cs * kStep);
+    a.n_chunks = (int)nch;
+    a.ncp = 1;
+    while (a.ncp < a.n_chunks) a.ncp <<= 1;
+    a.wave_merge = a.n_chunks > 1 && wm_ok && a.n_chunks * ncw <= kWaveMergeParts;
+    a.dec_diag = g_opt_dec_diag;
+    a.dec_ahead = g_opt_dec_ahead;
+    const int combine_bytes = kRows * pl.D * 4 + kRows * 64 * 4 + kRows * 4;
+    pl.lds = std::max({kDecHdr + nslot * step_bytes, ncw * G.merge_bytes, combine_bytes});
+    pl.dec = true;
+    pl.nlw = nlw;
+    pl.ncw = ncw;
+    pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
+    if (a.n_chunks > 1 && a.wave_merge) {
+        const size_t parts = (size_t)S * Y * a.n_chunks * ncw;
+        pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
+        pl.ml_bytes = (parts * 2 * sizeof(float) + 255) / 256 * 256;
+        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + parts * pl.D * 4;
+    } else if (a.n_chunks > 1) {
+        pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
+        pl.ml_bytes = ((size_t)S * Y * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
+        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + (size_t)S * Y * a.n_chunks * kRows * pl.D * 4;
+    } else {
+        pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
+    }
+    return FATTN_OK;
+}
+
 template <int NW, int RPW>
 int mq_lds_bytes_r(int kt, int D) {
     if (kt == FATTN_TYPE_Q8_0)
@@ -207,7 +291,7 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     if (kv_chunk > 0) {
         nch = (N + kv_chunk - 1) / kv_chunk;
     } else {
-        const int64_t want = pl.nw == 8 ? kCUs : 2 * kCUs;
+        const int64_t want = pl.nw == 8 ? pl.cus : 2 * pl.cus;
         nch = (want + base - 1) / base;
         nch = std::min<int64_t>(nch, std::max<int64_t>(1, tiles / 4));  // >= 4 tiles per workgroup
     }
@@ -240,6 +324,7 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
 // Validate and build the launch plan.  Returns FATTN_OK or an error.
 int make_plan(const fattn_params* p, Plan& pl) {
     if (!p || !p->q.data || !p->k.data || !p->v.data || !p->dst) return FATTN_ERR_INVALID_ARG;
+    pl.cus = device_cus();
     const fattn_tensor &q = p->q, &k = p->k, &v = p->v, &mk = p->mask;
     if (q.type != FATTN_TYPE_F32 || q.nb[0] != 4) return FATTN_ERR_UNSUPPORTED_TYPE;
     const int64_t D = q.ne[0];
@@ -343,7 +428,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     if (pl.mq) {
         // 256 rows per workgroup once that still gives one workgroup per CU
         const int64_t wg256 = Hkv * S * ((NQ * a.rk2 + 255) / 256);
-        pl.nw = g_opt_mq_rpw ? (g_opt_mq_rpw == 32 ? 8 : 4) : wg256 >= kCUs ? 8 : 4;
+        pl.nw = g_opt_mq_rpw ? (g_opt_mq_rpw == 32 ? 8 : 4) : wg256 >= pl.cus ? 8 : 4;
         a.R = a.rk2;
         a.QPT = (pl.nw == 8 ? 256 : 64) / a.R;
         a.R_inv = 1.0f / (float)a.R;
@@ -354,11 +439,10 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // the (kv head x query tile x seq) workgroups alone fill the chip
     // (f16 K/V rows, not transposed V: the same kernel, images filled by DMA)
     pl.pf = false;
-    pl.pf_pre = false;
     const bool heads_ok = NQ * a.rk2 >= 32 && a.rk2 <= 64 && (a.rk2 & (a.rk2 - 1)) == 0;
     const bool pf_f16 = !g_opt_mq_disable && k.type == FATTN_TYPE_F16 && !v_trans && g16 && heads_ok;
     if ((mq_ok || pf_f16) && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
-        p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= kCUs)) {
+        p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= pl.cus)) {
         pl.pf = true;
         pl.mq = false;
         a.R = a.rk2;
@@ -366,7 +450,6 @@ int make_plan(const fattn_params* p, Plan& pl) {
         a.n_hsub = 1;
         a.QPT = kPfRows / a.R;
         a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
-        pl.pf_pre = is_quant(k.type) && g_opt_pf_dequant == 2 && g_opt_pf_waves == 8;
     }
     const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
     if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
@@ -375,30 +458,30 @@ int make_plan(const fattn_params* p, Plan& pl) {
         a.pf_stagger = g_opt_pf_stagger;
         a.n_chunks = 1;
         a.ncp = 1;
-        pl.pf_waves = pl.kt == FATTN_TYPE_F16 ? 8 : g_opt_pf_waves;
-        pl.hkv = Hkv;
-        pl.pf_rows = Skv * Hkv * N;
         pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
-        // auto = fattn_pf_kernel: the pipelined kernel measures slower so far
-        // (DESIGN.md §9); kept behind the option while its schedule is worked on
-        pl.pf_pipe = (pl.kt == FATTN_TYPE_F16 || pl.pf_pre) && g_opt_pf_pipe == 2;
-        if (pl.pf_pipe)
-            pl.lds = PfpCfg::ldsBytes;
-        else if (pl.kt == FATTN_TYPE_F16 || pl.pf_pre)
-            pl.lds = PfCfg<FATTN_TYPE_F16, 128>::ldsBytes;
-        else if (pl.pf_waves == 4)
-            pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? Pf4Cfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : Pf4Cfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
-        else
-            pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
+        pl.lds = pl.kt == FATTN_TYPE_F16    ? PfCfg<FATTN_TYPE_F16, 128>::ldsBytes
+                 : pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
+                                            : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
-        // workspace: [live-block flags, n_qt x N/64 bytes (masked fattn_pf_kernel)]
-        //            [pre-pass: K rows | V rows, f16 [Skv][Hkv][N][D] each]
-        pl.pf_flags = has_mask && pl.pf_waves == 8 && !pl.pf_pipe && !g_opt_pf_no_skip;
+        // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
+        // share the front of the workspace with the split-KV arrival counters
+        // a later decode on the same workspace relies on, so the launch
+        // re-zeroes them behind the prefill kernel (workspace contract,
+        // include/fattn.h: every launch leaves the workspace re-armed).
+        pl.pf_flags = has_mask && !g_opt_pf_no_skip;
         if (pl.pf_flags) pl.cnt_bytes = ((size_t)a.n_qt * (N / kPfKeys) + 255) / 256 * 256;
-        pl.ws_bytes = pl.cnt_bytes + (pl.pf_pre ? 2 * (size_t)pl.pf_rows * D * 2 : 0);
+        pl.ws_bytes = pl.cnt_bytes;
         return FATTN_OK;
     }
-    const int rc = pl.mq ? size_mq(pl, p->kv_chunk, Y, S, N) : size_split(pl, p->kv_chunk, Y, S, N, NQ);
+    pl.dec = false;
+    const bool dec_ok = g16 && g_opt_dec != 1;
+    int rc = FATTN_ERR_INVALID_ARG;
+    if (pl.mq) rc = size_mq(pl, p->kv_chunk, Y, S, N);
+    else if (dec_ok) rc = size_dec(pl, p->kv_chunk, Y, S, N, NQ);
+    if (!pl.mq && rc != FATTN_OK) {  // not the loader kernel, or a shape it does not take (one-step chunks)
+        pl.dec = false;
+        rc = size_split(pl, p->kv_chunk, Y, S, N, NQ);
+    }
     if (rc != FATTN_OK) return rc;
     return FATTN_OK;
 }
@@ -412,14 +495,18 @@ struct Events {
 template <typename F>
 int launch_kernel(const void* kern, const Plan& pl, hipStream_t st, const Events& ev, F&& go) {
     (void)hipGetLastError();
-    static int lds_set = 65536;  // per kernel instantiation (F is unique per launch site); benign race
-    if (pl.lds > lds_set) {
+    // large dynamic LDS must be allowed per kernel and per device: cached per
+    // (launch site = F's instantiation, device); a lost race only repeats the call
+    static std::atomic<int> lds_set[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
+    if (pl.lds > 65536 && pl.lds > lds_set[dev].load(std::memory_order_relaxed)) {
         // the query loads the code object (HIP loads kernels lazily; setting an
         // attribute of a kernel whose module is not loaded yet fails)
         hipFuncAttributes fa;
         (void)hipFuncGetAttributes(&fa, kern);
         if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, pl.lds) == hipSuccess) {
-            lds_set = pl.lds;
+            lds_set[dev].store(pl.lds, std::memory_order_relaxed);
         } else if (std::getenv("FATTN_DEBUG")) {
             std::fprintf(stderr, "fattn: hipFuncSetAttribute(%d B LDS) failed; launching anyway\n", pl.lds);
         }
@@ -452,8 +539,29 @@ int launch_split(const Plan& pl, hipStream_t st, const Events& ev) {
                          : launch_split_hm<KT, VT, D, GRAN, false>(pl, st, ev);
 }
 
+template <int KT, int VT, int D, bool HM, int NLW, int NCW>
+int launch_dec_hm(const Plan& pl, hipStream_t st, const Events& ev) {
+    auto kern = fattn_dec_kernel<KT, VT, D, HM, NLW, NCW>;
+    return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        hipLaunchKernelGGL(kern, pl.grid, dim3((NCW + NLW) * kWave), pl.lds, st, pl.a);
+    });
+}
+
+template <int KT, int VT, int D, int NCW>
+int launch_dec_w(const Plan& pl, hipStream_t st, const Events& ev) {
+    // two loader waves (one loader measured 20 us on config 3 against 15.7)
+    return pl.a.has_mask ? launch_dec_hm<KT, VT, D, true, 2, NCW>(pl, st, ev)
+                         : launch_dec_hm<KT, VT, D, false, 2, NCW>(pl, st, ev);
+}
+
+template <int KT, int VT, int D>
+int launch_dec(const Plan& pl, hipStream_t st, const Events& ev) {
+    return pl.ncw == 8 ? launch_dec_w<KT, VT, D, 8>(pl, st, ev) : launch_dec_w<KT, VT, D, 4>(pl, st, ev);
+}
+
 template <int KT, int VT, int D>
 int launch_gran(const Plan& pl, hipStream_t st, const Events& ev) {
+    if (pl.dec) return launch_dec<KT, VT, D>(pl, st, ev);
     if constexpr (VT == VT_F16T) {
         return launch_split<KT, VT, D, 16>(pl, st, ev);
     } else {
@@ -478,28 +586,13 @@ int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
 
 template <int KT, bool HM>
 int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    if constexpr (KT != FATTN_TYPE_F16) {
-        if (pl.pf_waves == 4) {
-            auto kern4 = fattn_pf4_kernel<KT, 128, HM>;
-            return launch_kernel((const void*)kern4, pl, st, ev, [&] {
-                hipLaunchKernelGGL(kern4, pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
-            });
-        }
-    }
-    if constexpr (KT == FATTN_TYPE_F16) {
-        if (pl.pf_pipe) {
-            auto kernp = fattn_pfp_kernel<HM>;
-            return launch_kernel((const void*)kernp, pl, st, ev, [&] {
-                hipLaunchKernelGGL(kernp, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
-            });
-        }
-    }
     auto kern = fattn_pf_kernel<KT, 128, HM>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         if (HM && pl.a.pf_flags)
             hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,
                                pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
         hipLaunchKernelGGL(kern, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
+        if (HM && pl.a.pf_flags) (void)hipMemsetAsync((void*)pl.a.pf_flags, 0, pl.cnt_bytes, st);
     });
 }
 
@@ -508,47 +601,10 @@ int launch_pf(const Plan& pl, hipStream_t st, const Events& ev) {
     return pl.a.has_mask ? launch_pf_hm<KT, true>(pl, st, ev) : launch_pf_hm<KT, false>(pl, st, ev);
 }
 
-// Quantised prefill through the pre-pass: K and V rows -> f16 rows in the
-// workspace, then the f16 prefill kernel over them.  The events bracket both
-// launches (the conversion is part of the operation).
-template <int KT>
-int launch_pf_pre(const Plan& plq, hipStream_t st, const Events& ev) {
-    Plan pl = plq;
-    SplitArgs& a = pl.a;
-    constexpr int D = 128;
-    const int64_t rowF = D * 2, units = pl.pf_rows * (2 * D / QK);
-    uint8_t* wk = (uint8_t*)a.ws_o;
-    uint8_t* wv = wk + pl.pf_rows * rowF;
-    const int N = a.N, Hkv = (int)pl.hkv;
-    (void)hipGetLastError();
-    if (ev.begin) (void)hipEventRecord(ev.begin, st);
-    const unsigned nblk = (unsigned)((units + 255) / 256);
-    hipLaunchKernelGGL((pf_dequant_rows_kernel<KT, D>), dim3(nblk), dim3(256), 0, st, a.k, a.k_nb1, a.k_nb2, a.k_nb3,
-                       N, Hkv, wk, units);
-    hipLaunchKernelGGL((pf_dequant_rows_kernel<KT, D>), dim3(nblk), dim3(256), 0, st, a.v, a.v_nb1, a.v_nb2, a.v_nb3,
-                       N, Hkv, wv, units);
-    if (hipGetLastError() != hipSuccess) return FATTN_ERR_LAUNCH;
-    a.k = wk;
-    a.v = wv;
-    a.k_nb1 = a.v_nb1 = rowF;
-    a.k_nb2 = a.v_nb2 = (int64_t)N * rowF;
-    a.k_nb3 = a.v_nb3 = (int64_t)Hkv * N * rowF;
-    a.k_span = a.v_span = (uint32_t)((int64_t)N * rowF);
-    pl.kt = pl.vt = FATTN_TYPE_F16;
-    Events e2;
-    e2.end = ev.end;
-    return launch_pf<FATTN_TYPE_F16>(pl, st, e2);
-}
-
 template <int D>
 int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
     if constexpr (D == 128) {
         if (pl.pf) {
-            if (pl.pf_pre) {
-                if (pl.kt == FATTN_TYPE_Q8_0) return launch_pf_pre<FATTN_TYPE_Q8_0>(pl, st, ev);
-                if (pl.kt == FATTN_TYPE_Q4_0) return launch_pf_pre<FATTN_TYPE_Q4_0>(pl, st, ev);
-                return FATTN_ERR_UNSUPPORTED_TYPE;
-            }
             if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_pf<FATTN_TYPE_F16>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0>(pl, st, ev);
@@ -607,14 +663,10 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 7) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_stagger = value;
             return FATTN_OK;
-        case FATTN_OPT_PF_WAVES:
-            if (value != 4 && value != 8) return FATTN_ERR_INVALID_ARG;
-            g_opt_pf_waves = value;
-            return FATTN_OK;
+        case FATTN_OPT_PF_WAVES:  // removed experiments: only the default remains
+            return value == 8 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_PF_DEQUANT:
-            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
-            g_opt_pf_dequant = value;
-            return FATTN_OK;
+            return value == 0 || value == 1 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_MQ_MIN_ROWS:
             if (value < 32) return FATTN_ERR_INVALID_ARG;
             g_opt_mq_min_rows = value;
@@ -632,12 +684,28 @@ int fattn_set_option(int option, int value) {
             g_opt_no_wave_merge = value;
             return FATTN_OK;
         case FATTN_OPT_PF_PIPE:
-            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
-            g_opt_pf_pipe = value;
-            return FATTN_OK;
+            return value == 0 || value == 1 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_SPLIT_STEPS:
             if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;
             g_opt_split_spw = value;
+            return FATTN_OK;
+        case FATTN_OPT_DEC:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_dec = value;
+            return FATTN_OK;
+        case FATTN_OPT_DEC_LOADERS:
+            return value == 2 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
+        case FATTN_OPT_DEC_COMPUTE:
+            if (value != 4 && value != 8) return FATTN_ERR_INVALID_ARG;
+            g_opt_dec_compute = value;
+            return FATTN_OK;
+        case FATTN_OPT_DEC_AHEAD:
+            if (value < 1 || value > 8) return FATTN_ERR_INVALID_ARG;
+            g_opt_dec_ahead = value;
+            return FATTN_OK;
+        case FATTN_OPT_DEC_DIAG:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_dec_diag = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:
             if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
@@ -686,6 +754,31 @@ size_t fattn_workspace_size(const fattn_params* p) {
     return pl.ws_bytes;
 }
 
+int fattn_describe(const fattn_params* p, char* out, size_t cap) {
+    Plan pl;
+    const int rc = make_plan(p, pl);
+    if (rc != FATTN_OK) return rc;
+    auto tn = [](int t) {
+        return t == FATTN_TYPE_Q8_0 ? "q8_0" : t == FATTN_TYPE_Q4_0 ? "q4_0" : t == VT_F16T ? "f16T" : "f16";
+    };
+    char kern[160];
+    const char* hm = pl.a.has_mask ? "mask" : "nomask";
+    if (pl.pf)
+        std::snprintf(kern, sizeof kern, "%sfattn_pf_kernel<%s,D%d,%s>", pl.pf_flags ? "pf_mask_flags_kernel + " : "",
+                      tn(pl.kt), pl.D, hm);
+    else if (pl.mq)
+        std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>", tn(pl.kt), pl.D, pl.nw, hm);
+    else if (pl.dec)
+        std::snprintf(kern, sizeof kern, "fattn_dec_kernel<%s,%s,D%d,%s,%dloaders,%dcompute>", tn(pl.kt), tn(pl.vt),
+                      pl.D, hm, pl.nlw, pl.ncw);
+    else
+        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s>", tn(pl.kt), tn(pl.vt), pl.D,
+                      pl.gran, hm);
+    const int n = std::snprintf(out, cap, "%s grid(%u,%u,%u) lds %d chunk %d steps/slots %d ws %zu", kern, pl.grid.x,
+                                pl.grid.y, pl.grid.z, pl.lds, pl.a.chunk_len, pl.a.nbuf, pl.ws_bytes);
+    return n < 0 || (size_t)n >= cap ? FATTN_ERR_INVALID_ARG : FATTN_OK;
+}
+
 int fattn_ext(const fattn_params* p, void* stream) { return fattn_ext_events(p, stream, nullptr, nullptr); }
 
 int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* ev_end) {
@@ -722,7 +815,10 @@ int fattn_ext_f16_launch(const void* q, const void* k, const void* v, const void
     const int64_t vb0 = v_type == FATTN_TYPE_F16 ? 2 : (int64_t)fattn_row_size(v_type, 32);
     p.k = {k, k_type, 0, {ne10, ne11, ne12, ne13}, {kb0, nb11, nb12, nb13}};
     p.v = {v, v_type, 0, {ne10, ne11, ne12, ne13}, {vb0, nb11, nb12, nb13}};
-    if (mask) p.mask = {mask, FATTN_TYPE_F16, 0, {ne11, ne31, 1, 1}, {2, nb31, (int64_t)nb31 * ne31, (int64_t)nb31 * ne31}};
+    // mask rows hold nb31 / 2 halves: ggml pads them (GGML_KQ_MASK_PAD) past ne11,
+    // which an odd ne11 needs (the kernels read rows in dword pieces)
+    if (mask)
+        p.mask = {mask, FATTN_TYPE_F16, 0, {nb31 / 2, ne31, 1, 1}, {2, nb31, (int64_t)nb31 * ne31, (int64_t)nb31 * ne31}};
     p.dst = dst;
     p.scale = scale;
     p.workspace = workspace;
@@ -745,16 +841,27 @@ static void fill_row_params(fattn_params& p, const float* query, const void* key
     p.scale = scale;
 }
 
+// The ABI (kernel_test.h:155's inline sizing) does not name r_kv_heads, and
+// the plan -- rows per tile, chunks, merge layout -- depends on it: size for
+// the largest plan over every r that divides num_heads, with and without a mask.
 size_t fattn_row_workspace_size(int head_dim, int kv_size, int num_heads) {
-    fattn_params p;
+    if (num_heads <= 0) return 0;
+    size_t best = 0;
     static const float dummy_f[4] = {0, 0, 0, 0};
-    fill_row_params(p, dummy_f, dummy_f, dummy_f, nullptr, (float*)dummy_f, head_dim, kv_size, num_heads,
-                    1.0f, head_dim * kv_size, 1);
-    Plan pl;
-    p.q.data = (const void*)(uintptr_t)16;  // alignment-only placeholders
-    p.k.data = p.v.data = (const void*)(uintptr_t)16;
-    if (make_plan(&p, pl) != FATTN_OK) return 0;
-    return pl.ws_bytes;
+    for (int r = 1; r <= num_heads; r++) {
+        if (num_heads % r) continue;
+        for (int m = 0; m < 2; m++) {
+            fattn_params p;
+            fill_row_params(p, dummy_f, dummy_f, dummy_f, m ? dummy_f : nullptr, (float*)dummy_f, head_dim, kv_size,
+                            num_heads, 1.0f, head_dim * kv_size, r);
+            p.q.data = (const void*)(uintptr_t)16;  // alignment-only placeholders
+            p.k.data = p.v.data = (const void*)(uintptr_t)16;
+            if (m) p.mask.data = (const void*)(uintptr_t)16;
+            Plan pl;
+            if (make_plan(&p, pl) == FATTN_OK) best = std::max(best, pl.ws_bytes);
+        }
+    }
+    return best;
 }
 
 int fattn_row(const float* query, const void* key, const void* value, const void* mask, void* tmp, size_t tmp_bytes,
@@ -797,13 +904,41 @@ int fattn_quantize(int type, const float* src, void* dst, int64_t k, int64_t n_r
     hipStream_t st = (hipStream_t)stream;
     const int64_t nb = k * n_rows / QK;
     if (type == FATTN_TYPE_Q8_0)
-        hipLaunchKernelGGL(quant_q8_0_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, src,
+        hipLaunchKernelGGL(quant_kernel<FATTN_TYPE_Q8_0>, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, src,
                            (uint8_t*)dst, nb);
     else if (type == FATTN_TYPE_Q4_0)
-        hipLaunchKernelGGL(quant_q4_0_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, src,
+        hipLaunchKernelGGL(quant_kernel<FATTN_TYPE_Q4_0>, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, src,
                            (uint8_t*)dst, nb);
     else
         return FATTN_ERR_UNSUPPORTED_TYPE;
+    return hipGetLastError() == hipSuccess ? FATTN_OK : FATTN_ERR_LAUNCH;
+}
+
+int fattn_cpy(const fattn_tensor* src, const fattn_tensor* dst, void* stream) {
+    if (!src || !dst || !src->data || !dst->data) return FATTN_ERR_INVALID_ARG;
+    if (src->type != FATTN_TYPE_F32 || src->nb[0] != 4) return FATTN_ERR_UNSUPPORTED_TYPE;
+    const int t = dst->type;
+    if (t != FATTN_TYPE_F16 && t != FATTN_TYPE_Q8_0 && t != FATTN_TYPE_Q4_0) return FATTN_ERR_UNSUPPORTED_TYPE;
+    for (int i = 0; i < 4; i++)
+        if (src->ne[i] != dst->ne[i] || src->ne[i] <= 0) return FATTN_ERR_INVALID_ARG;
+    const int64_t ue = t == FATTN_TYPE_F16 ? 1 : QK;
+    if (src->ne[0] % ue) return FATTN_ERR_INVALID_ARG;
+    if (dst->nb[0] != (int64_t)fattn_row_size(t, ue)) return FATTN_ERR_BAD_STRIDE;
+    if ((uintptr_t)src->data % 4 || src->nb[1] % 4 || src->nb[2] % 4 || src->nb[3] % 4) return FATTN_ERR_ALIGNMENT;
+    if ((uintptr_t)dst->data % 2 || dst->nb[1] % 2 || dst->nb[2] % 2 || dst->nb[3] % 2) return FATTN_ERR_ALIGNMENT;
+    CpyArgs a;
+    a.src = (const uint8_t*)src->data;
+    a.dst = (uint8_t*)dst->data;
+    a.ne0 = src->ne[0]; a.ne1 = src->ne[1]; a.ne2 = src->ne[2]; a.ne3 = src->ne[3];
+    a.snb1 = src->nb[1]; a.snb2 = src->nb[2]; a.snb3 = src->nb[3];
+    a.dnb1 = dst->nb[1]; a.dnb2 = dst->nb[2]; a.dnb3 = dst->nb[3];
+    const int64_t units = a.ne0 / ue * a.ne1 * a.ne2 * a.ne3;
+    const dim3 grid((unsigned)((units + 255) / 256));
+    hipStream_t st = (hipStream_t)stream;
+    (void)hipGetLastError();
+    if (t == FATTN_TYPE_F16) hipLaunchKernelGGL(cpy_f32_kernel<FATTN_TYPE_F16>, grid, dim3(256), 0, st, a, units);
+    else if (t == FATTN_TYPE_Q8_0) hipLaunchKernelGGL(cpy_f32_kernel<FATTN_TYPE_Q8_0>, grid, dim3(256), 0, st, a, units);
+    else hipLaunchKernelGGL(cpy_f32_kernel<FATTN_TYPE_Q4_0>, grid, dim3(256), 0, st, a, units);
     return hipGetLastError() == hipSuccess ? FATTN_OK : FATTN_ERR_LAUNCH;
 }
 

@@ -648,48 +648,4 @@ __global__ __launch_bounds__(256) void pf_mask_flags_kernel(const uint8_t* __res
     if (threadIdx.x == 0) flags[(int64_t)qt * ntiles + s] = any ? 1 : 0;
 }
 
-// ---- prefill pre-pass: quantised K or V rows -> dense f16 rows [Skv][Hkv][N][D],
-// h(q * d) with one f16 rounding -- the same values the in-kernel
-// dequantisation writes to the images, so both paths give identical results.
-// One thread per half ggml block (16 elements, 32 B out): a wave writes 2 KiB
-// contiguous.
-template <int KT, int D>
-__global__ __launch_bounds__(256) void pf_dequant_rows_kernel(const uint8_t* __restrict__ src, int64_t nb1, int64_t nb2,
-                                                              int64_t nb3, int N, int Hkv, uint8_t* __restrict__ dst,
-                                                              int64_t nunits) {
-    constexpr int NB = D / QK;
-    constexpr int BB = TypeInfo<KT>::block_bytes;
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= nunits) return;
-    const int h = (int)(t & 1), b = (int)((t >> 1) % NB);
-    const int64_t row = t / (2 * NB);
-    const int n = (int)(row % N);
-    const int64_t hk = row / N;
-    const uint16_t* p16 = (const uint16_t*)(src + (hk / Hkv) * nb3 + (hk % Hkv) * nb2 + (int64_t)n * nb1 + b * BB);
-    const f16x2 d = bcast_h(p16[0]);
-    // Q8_0: qs bytes 16h..16h+15; Q4_0: all 16 qs bytes (low / high nibbles)
-    const uint16_t* qs = p16 + 1 + (KT == FATTN_TYPE_Q8_0 ? 8 * h : 0);
-    uint32_t q[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) q[j] = (uint32_t)qs[2 * j] | ((uint32_t)qs[2 * j + 1] << 16);
-    u32x4 out[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        f16x2 h0, h1, h2, h3;
-        if constexpr (KT == FATTN_TYPE_Q8_0) {
-            i8x4_to_h2x2(q[2 * k], h0, h1);
-            i8x4_to_h2x2(q[2 * k + 1], h2, h3);
-        } else {
-            const uint32_t sft = 4 * h;
-            u4x4_to_h2x2((q[2 * k] >> sft) & 0x0F0F0F0Fu, h0, h1);
-            u4x4_to_h2x2((q[2 * k + 1] >> sft) & 0x0F0F0F0Fu, h2, h3);
-        }
-        h0 *= d; h1 *= d; h2 *= d; h3 *= d;
-        out[k] = u32x4{as_u32(h0), as_u32(h1), as_u32(h2), as_u32(h3)};
-    }
-    uint8_t* o = dst + row * (D * 2) + (4 * b + 2 * h) * 16;
-    *(u32x4*)o = out[0];
-    *(u32x4*)(o + 16) = out[1];
-}
-
 }  // namespace fattn

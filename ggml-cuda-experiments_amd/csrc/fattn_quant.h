@@ -65,24 +65,14 @@ __global__ __launch_bounds__(256) void dequant_f16_kernel(const uint16_t* __rest
     dst[i] = (float)__builtin_bit_cast(f16, src[i]);
 }
 
-__global__ __launch_bounds__(256) void quant_q8_0_kernel(const float* __restrict__ src, uint8_t* __restrict__ dst,
-                                                         int64_t nblocks) {
+// One ggml block of 32 values -> Q8_0 {f16 d; int8 qs[32]} (quantize_row_q8_0_ref)
+__device__ __forceinline__ void quant_block_q8_0(const float (&xv)[QK], uint8_t* blk) {
 #pragma clang fp contract(off)
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nblocks) return;
-    const float* x = src + i * QK;
-    float xv[QK];
-#pragma unroll
-    for (int j = 0; j < QK; j += 4) {
-        const f32x4 v = *(const f32x4*)(x + j);
-        xv[j] = v.x; xv[j + 1] = v.y; xv[j + 2] = v.z; xv[j + 3] = v.w;
-    }
     float amax = 0.0f;
 #pragma unroll
     for (int j = 0; j < QK; j++) amax = fmaxf(amax, fabsf(xv[j]));
     const float d = amax / 127.0f;
     const float id = d != 0.0f ? 1.0f / d : 0.0f;
-    uint8_t* blk = dst + i * kQ8Bytes;
     const uint16_t dh = __builtin_bit_cast(uint16_t, (f16)opaque(d));
     blk[0] = dh & 0xff;
     blk[1] = dh >> 8;
@@ -90,18 +80,9 @@ __global__ __launch_bounds__(256) void quant_q8_0_kernel(const float* __restrict
     for (int j = 0; j < QK; j++) blk[2 + j] = (uint8_t)(int8_t)roundf(xv[j] * id);
 }
 
-__global__ __launch_bounds__(256) void quant_q4_0_kernel(const float* __restrict__ src, uint8_t* __restrict__ dst,
-                                                         int64_t nblocks) {
+// One ggml block of 32 values -> Q4_0 {f16 d; u8 qs[16]} (quantize_row_q4_0_ref)
+__device__ __forceinline__ void quant_block_q4_0(const float (&xv)[QK], uint8_t* blk) {
 #pragma clang fp contract(off)
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nblocks) return;
-    const float* x = src + i * QK;
-    float xv[QK];
-#pragma unroll
-    for (int j = 0; j < QK; j += 4) {
-        const f32x4 v = *(const f32x4*)(x + j);
-        xv[j] = v.x; xv[j + 1] = v.y; xv[j + 2] = v.z; xv[j + 3] = v.w;
-    }
     float amax = 0.0f, mx = 0.0f;
 #pragma unroll
     for (int j = 0; j < QK; j++) {
@@ -112,7 +93,6 @@ __global__ __launch_bounds__(256) void quant_q4_0_kernel(const float* __restrict
     }
     const float d = mx * -0.125f;  // == mx / -8 exactly (power of two), keeps -0.0
     const float id = d != 0.0f ? 1.0f / d : 0.0f;
-    uint8_t* blk = dst + i * kQ4Bytes;
     const uint16_t dh = __builtin_bit_cast(uint16_t, (f16)opaque(d));
     blk[0] = dh & 0xff;
     blk[1] = dh >> 8;
@@ -123,6 +103,62 @@ __global__ __launch_bounds__(256) void quant_q4_0_kernel(const float* __restrict
         const uint8_t q0 = (uint8_t)(t0 < 15 ? t0 : 15);
         const uint8_t q1 = (uint8_t)(t1 < 15 ? t1 : 15);
         blk[2 + j] = (uint8_t)(q0 | (q1 << 4));
+    }
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void quant_kernel(const float* __restrict__ src, uint8_t* __restrict__ dst,
+                                                    int64_t nblocks) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nblocks) return;
+    const float* x = src + i * QK;
+    float xv[QK];
+#pragma unroll
+    for (int j = 0; j < QK; j += 4) {
+        const f32x4 v = *(const f32x4*)(x + j);
+        xv[j] = v.x; xv[j + 1] = v.y; xv[j + 2] = v.z; xv[j + 3] = v.w;
+    }
+    if constexpr (T == FATTN_TYPE_Q8_0)
+        quant_block_q8_0(xv, dst + i * kQ8Bytes);
+    else
+        quant_block_q4_0(xv, dst + i * kQ4Bytes);
+}
+
+// Strided f32 -> F16 / Q8_0 / Q4_0 copy: ggml's GGML_OP_CPY into a KV-cache view
+// (upstream ggml cpy f32 -> f16/q8_0/q4_0).  src and dst
+// have the same ne (ne0 = row length, a multiple of 32 for the block types)
+// and any byte strides nb1..nb3; rows are contiguous (src nb0 = 4, dst nb0 =
+// element / block size).  One thread per 32-element block (per element for
+// F16): the writes of one token's K rows land straight in the cache, whether
+// it is laid out [Hkv][N][row] (head stride > row) or [N][Hkv][row].
+struct CpyArgs {
+    const uint8_t* src;
+    uint8_t* dst;
+    int64_t ne0, ne1, ne2, ne3;
+    int64_t snb1, snb2, snb3;
+    int64_t dnb1, dnb2, dnb3;
+};
+
+template <int T>
+__global__ __launch_bounds__(256) void cpy_f32_kernel(const CpyArgs a, int64_t units) {
+    constexpr int UE = T == FATTN_TYPE_F16 ? 1 : QK;  // elements per unit
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= units) return;
+    const int64_t upr = a.ne0 / UE;
+    const int64_t b = i % upr, r = i / upr;
+    const int64_t i1 = r % a.ne1, i2 = (r / a.ne1) % a.ne2, i3 = r / (a.ne1 * a.ne2);
+    const float* x = (const float*)(a.src + i1 * a.snb1 + i2 * a.snb2 + i3 * a.snb3) + b * UE;
+    uint8_t* y = a.dst + i1 * a.dnb1 + i2 * a.dnb2 + i3 * a.dnb3;
+    if constexpr (T == FATTN_TYPE_F16) {
+        *(uint16_t*)(y + b * 2) = __builtin_bit_cast(uint16_t, (f16)x[0]);
+    } else {
+        float xv[QK];
+#pragma unroll
+        for (int j = 0; j < QK; j++) xv[j] = x[j];
+        if constexpr (T == FATTN_TYPE_Q8_0)
+            quant_block_q8_0(xv, y + b * kQ8Bytes);
+        else
+            quant_block_q4_0(xv, y + b * kQ4Bytes);
     }
 }
 

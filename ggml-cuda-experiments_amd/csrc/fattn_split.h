@@ -78,6 +78,8 @@ struct SplitArgs {
     int split_prio;     // split kernel wave priorities: 0 staggered 3/2/1/0, 1 none, 2 staggered while issuing
     int wave_merge;     // split kernel, one-row tiles: every wave publishes its own partial and
                         // the last-arriving WAVE merges them (no LDS merge, no barriers)
+    int dec_diag;       // fattn_dec_kernel diagnostics: 1 = no compute, 2 = no DMA (never in the product path)
+    int dec_ahead;      // fattn_dec_kernel: steps in flight per loader wave (capped by vmcnt)
 };
 
 template <int KT, int VT, int D>
@@ -207,7 +209,10 @@ __device__ __forceinline__ u32x4 ld_buf(const i32x4& srd, uint32_t off) {
 }
 
 template <int BYTES, bool NT = false>
-__device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds, uint32_t off) {
+__device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds_any, uint32_t off) {
+    // wave-uniform by construction; readfirstlane keeps it an SGPR operand even
+    // where divergent code around the call hides that from the compiler
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_any);
     uint32_t keep;
     if constexpr (BYTES == 16 && NT) {
         asm volatile(
@@ -466,9 +471,19 @@ __device__ unsigned long long* g_stamps;
             atomicMax(&g_stamps[blk_ * kSplitWaves * 16 + (k)], (unsigned long long)(v));      \
         }                                                                                       \
     } while (0)
+// fattn_dec_kernel: [block][8 waves][16] (tools/dec_stamps.py)
+#define FATTN_STAMP8(k)                                                                         \
+    do {                                                                                        \
+        if (lane == 0 && g_stamps) {                                                            \
+            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                     \
+            const int64_t blk_ = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
+            g_stamps[(blk_ * 8 + wave) * 16 + (k)] = t_;                                        \
+        }                                                                                       \
+    } while (0)
 #else
 #define FATTN_STAMP(k) do { } while (0)
 #define FATTN_STAMP_MAX(k, v) do { } while (0)
+#define FATTN_STAMP8(k) do { } while (0)
 #endif
 
 // ---------------------------------------------------------------- kernel
@@ -486,7 +501,7 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
 // fa_reduce math as combine_tile (src/flash_row_float.h:415-472), fixed order.
 constexpr int kWaveMergeParts = 64;  // parts per tile (one (m, l) pair per lane)
 constexpr int kWaveMergeBatch = 32;  // parts loaded per round trip
-template <int D, bool VQ8>
+template <int D, bool VQ8, int NW = kSplitWaves>
 __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f32x4 (&o)[D / 16], float m_run,
                                                     float l_tot, int chunk, int wave, int lane, int qt, int hs,
                                                     int ik2, int iq3) {
@@ -495,9 +510,9 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     constexpr int NC = D / 16;
     constexpr float kNegInf = -__builtin_inff();
     const int g = lane >> 4, m = lane & 15;
-    const int NP = a.n_chunks * kSplitWaves;
+    const int NP = a.n_chunks * NW;
     const int64_t tile = (int64_t)iq3 * gridDim.y + blockIdx.y;
-    const int part = chunk * kSplitWaves + wave;
+    const int part = chunk * NW + wave;
     float* po = a.ws_o + (tile * NP + part) * D;  // row 0 of the part: [NP][D] per tile
     auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
     if (m == 0) {  // column 0 = the tile's row; its dims sit on lanes 0, 16, 32, 48
@@ -516,10 +531,12 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
         if (g == 0) st_sc1_x2(a.ws_ml + 2 * (tile * NP + part), u32x2{bits(m_run), bits(l_tot)});
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FATTN_STAMP8(10);
     uint32_t* cnt = a.ws_cnt + tile * kCntStride;
     uint32_t old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __builtin_amdgcn_readfirstlane(old);
+    FATTN_STAMP8(11);
     if (old != (uint32_t)(NP - 1)) return;
     if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---- merge: every load issued before one wait (parts past NP: out of range, zeros)
@@ -546,6 +563,7 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
     uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8 + 4));  //          l of part p
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FATTN_STAMP8(12);
     reg_fence(mlm);
     reg_fence(mll);
     fence();
@@ -573,6 +591,328 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + 2 * lane;
     const float inv = 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
     *(f32x2*)out = f32x2{L == 0.0f ? __builtin_nanf("") : acc0 * inv, L == 0.0f ? __builtin_nanf("") : acc1 * inv};
+    FATTN_STAMP8(13);
+}
+
+// Tail of a split-KV workgroup: the compute waves' (O, m, l) states merge --
+// through the last-arriving wave (one-row tiles, wave_merge) or through LDS
+// (wave w's image at smem + w * region) and then across the tile's chunks via
+// the last-arriving workgroup (combine_tile).  `active`: this wave holds a
+// state (fattn_dec_kernel's loader waves do not, and only join the barriers;
+// waves >= NW must be inactive).  `sync_first`: the images alias
+// step buffers, so wait for every wave before writing them.
+template <int KT, int VT, int D, int NW = kSplitWaves>
+__device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D / 16], float m_run, float l_run,
+                                               float (&corr)[D / QK], int wave, int lane, int qt, int hs, int ik2,
+                                               int iq3, int y, int chunk, uint8_t* smem, int region, bool active,
+                                               bool sync_first) {
+    using C = SplitCfg<KT, VT, D>;
+    constexpr int NB = D / QK;
+    constexpr int NC = D / 16;
+    constexpr float kNegInf = -__builtin_inff();
+    constexpr bool kVQ8 = C::VTT == FATTN_TYPE_Q8_0;
+    constexpr bool kVQ = C::VTT != FATTN_TYPE_F16;
+    constexpr float kVOff = kVQ8 ? 1152.0f : 1032.0f;
+    const int g = lane >> 4;
+    const int m = lane & 15;
+    // ---- per-wave state -> LDS (this wave's own region), then merge the 4 waves
+    if (!active) {  // loader waves (fattn_dec_kernel): no state; they only join the barriers
+        if (a.n_chunks > 1 && a.wave_merge && D == 128) return;
+    }
+    const float l_tot = grp4_sum(l_run);
+    if constexpr (kVQ) {
+        // O^T tiles of block b (columns 32b..32b+31) carry kVOff * sum(P'_b) too
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const float cb = kVOff * grp4_sum(corr[b]);
+            o[2 * b] -= cb;
+            o[2 * b + 1] -= cb;
+        }
+    }
+    if constexpr (D == 128) {
+        if (a.wave_merge) {
+            wave_merge_epilogue<D, kVQ8, NW>(a, o, m_run, l_tot, chunk, wave, lane, qt, hs, ik2, iq3);
+            return;
+        }
+    }
+    constexpr int MS = C::kMergeStride;
+    // the merge images alias step buffers other waves may still be reading
+    if (sync_first) __syncthreads();
+    float* mo = (float*)(smem + wave * region);    // [16][MS]
+    float* mml = (float*)(smem + wave * region + kRows * MS * 4);  // [16][2]
+    // valid rows of this tile form a prefix [0, rv); only those are merged
+    const int rv = tile_rows(a, qt, hs);
+    if (m >= rv || !active) {
+        // nothing of this column is needed
+    } else if constexpr (kVQ8) {
+        // tile E_b holds columns 32b + 2(4g+reg), O_b the odd neighbours
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const f32x4 e = o[2 * b], od = o[2 * b + 1];
+            *(f32x4*)(mo + m * MS + 32 * b + 8 * g) = f32x4{e.x, od.x, e.y, od.y};
+            *(f32x4*)(mo + m * MS + 32 * b + 8 * g + 4) = f32x4{e.z, od.z, e.w, od.w};
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < NC; c++) *(f32x4*)(mo + m * MS + 16 * c + 4 * g) = o[c];
+    }
+    if (g == 0 && m < rv && active) {
+        mml[2 * m] = m_run;
+        mml[2 * m + 1] = l_tot;
+    }
+    __syncthreads();
+    FATTN_STAMP(11);
+
+    constexpr int EPT = D / 16;  // outputs per thread: 16 rows x D over 256 threads
+    const int tm = threadIdx.x / 16;
+    const int tj = threadIdx.x % 16;
+    const int d0 = tj * EPT;
+    float M = kNegInf;
+    float mw[NW], lw[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const float* ml = (const float*)(smem + w * region + kRows * MS * 4);
+        mw[w] = tm < rv ? ml[2 * tm] : kNegInf;
+        lw[w] = tm < rv ? ml[2 * tm + 1] : 0.0f;
+        M = fmaxf(M, mw[w]);
+    }
+    float L = 0.0f;
+    float acc[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; e++) acc[e] = 0.0f;
+    if (tm < rv) {
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const float wt = (mw[w] == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mw[w] - M);
+            L += wt * lw[w];
+            const float* ow = (const float*)(smem + w * region) + tm * MS + d0;
+#pragma unroll
+            for (int e = 0; e < EPT; e++) acc[e] += wt * ow[e];
+        }
+    }
+    auto dst_row = [&](int r) -> float* {
+        const int rq = div_R(a, r);
+        const int riq1 = qt * a.QPT + rq;
+        const int riq2 = ik2 * a.rk2 + hs * a.R + (r - rq * a.R);
+        return a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D;
+    };
+    if (a.n_chunks == 1) {
+        if (tm < rv) {
+            float* out = dst_row(tm) + d0;
+            const float inv = 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
+#pragma unroll
+            for (int e = 0; e < EPT; e += 4) {
+                f32x4 v;
+                v.x = L == 0.0f ? __builtin_nanf("") : acc[e] * inv;
+                v.y = L == 0.0f ? __builtin_nanf("") : acc[e + 1] * inv;
+                v.z = L == 0.0f ? __builtin_nanf("") : acc[e + 2] * inv;
+                v.w = L == 0.0f ? __builtin_nanf("") : acc[e + 3] * inv;
+                *(f32x4*)(out + e) = v;
+            }
+        }
+        FATTN_STAMP(12);
+        return;
+    }
+
+#ifdef FATTN_DIAG_NOPUBLISH
+    // diagnostic build only: stop after the 4-wave merge
+    if (acc[0] == 12345.0f) a.dst[0] = L;
+    return;
+#endif
+    // ---- several chunks: the workgroup that arrives last for the tile merges
+    // all partials (no second launch).  Hand-off (MI355X_MICROARCH.md,
+    // inter-workgroup visibility, first row of the sc1 table): partial bytes
+    // stored sc1 (write-through), each storing wave drains vmcnt, barrier, ONE
+    // agent-scope atomic add per workgroup on the tile's own 256-B line; the
+    // last adder reads the others' partials with sc1 loads -- all of them in
+    // one round trip -- while its own stays in LDS.
+    const int64_t tile = (int64_t)iq3 * gridDim.y + y;
+    if (tm < rv) {
+        const int64_t slot = (tile * a.n_chunks + chunk) * kRows + tm;
+        auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
+#pragma unroll
+        for (int e = 0; e < EPT; e += 4)
+            st_sc1(a.ws_o + slot * D + d0 + e, u32x4{bits(acc[e]), bits(acc[e + 1]), bits(acc[e + 2]), bits(acc[e + 3])});
+        if (tj == 0) st_sc1_x2(a.ws_ml + 2 * slot, u32x2{bits(M), bits(L)});
+    }
+    // every storing wave drains: the merging workgroup reads its own partial back too
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef FATTN_DIAG_NOATOMIC
+    return;  // diagnostic build only: stop after the published stores drained
+#endif
+    __syncthreads();  // every storing wave has drained; every wave is done reading the merge image
+    int* last_flag = (int*)smem;
+    if (threadIdx.x == 0) {
+        uint32_t* cnt = a.ws_cnt + tile * kCntStride;
+        const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (uint32_t)(a.n_chunks - 1);
+        // every chunk has arrived: re-arm the counter for the next launch
+        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *last_flag = last;
+    }
+    __syncthreads();
+    FATTN_STAMP(12);
+    if (!*last_flag) return;
+    combine_tile<D, (D == 128 && KT != FATTN_TYPE_F16) ? 8 : 2>(a, tile, qt, hs, ik2, iq3, rv, 0, smem);
+    FATTN_STAMP(13);
+}
+
+// One 32-position step of one wave: S^T = K.Q^T for the step's two 16-row
+// key tiles, scale + mask, online softmax of the wave's 16 packed columns,
+// O^T += V^T.P^T.  `buf` is the step's LDS image [K rows | V rows | mask rows];
+// `wait_v()` runs between the softmax and P.V (the split kernel waits there
+// for the step's V, which it issues last).  `first`: o, l are still zero.
+// Shared by fattn_split_kernel and fattn_dec_kernel (fattn_dec.h).
+template <int KT, int VT, int D, bool HM, typename WaitV>
+__device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* buf, const f16x8 (&qop)[D / QK], int mq,
+                                           int g, int i16, int nvalid, bool first, float& m_run, float& l_run,
+                                           f32x4 (&o)[D / 16], float (&corr)[D / QK], WaitV&& wait_v) {
+    using C = SplitCfg<KT, VT, D>;
+    constexpr int NB = D / QK;
+    constexpr int NC = D / 16;
+    constexpr float kNegInf = -__builtin_inff();
+    constexpr bool kVQ8 = C::VTT == FATTN_TYPE_Q8_0;
+    constexpr bool kVQ = C::VTT != FATTN_TYPE_F16;
+    const float log2e = 1.4426950408889634f;
+    const uint8_t* kb = buf;
+    const uint8_t* vb = buf + C::kBytes;
+    const uint8_t* mb = buf + C::kBytes + C::vBytes;
+
+    // -- S^T = K.Q^T for the two 16-row tiles
+    f32x4 st[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        st[t] = f32x4{0, 0, 0, 0};
+        if constexpr (KT == FATTN_TYPE_F16) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) st[t] = mfma16(k_operand<KT, D>(kb, 16 * t + i16, g, b, 0), qop[b], st[t]);
+        } else {
+            const RowScales<KT, D> ks = row_scales<KT, D>(kb + (16 * t + i16) * C::rowK);
+#pragma unroll
+            for (int b = 0; b < NB; b++)
+                st[t] = mfma16(k_operand<KT, D>(kb, 16 * t + i16, g, b, scale_bits(ks, b)), qop[b], st[t]);
+        }
+    }
+
+    // -- scale + mask (log2 domain); positions past this wave's slice -> -inf
+    float sv[8];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        float mk[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (HM) {
+            const uint8_t* mp = mb + (mq < a.QPT ? mq : 0) * (kStep * 2) + (16 * t + 4 * g) * 2;
+            const u32x2 mw = *(const u32x2*)mp;
+            const f16x2 m01 = as_h2(mw.x), m23 = as_h2(mw.y);
+            mk[0] = (float)m01.x; mk[1] = (float)m01.y; mk[2] = (float)m23.x; mk[3] = (float)m23.y;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) sv[4 * t + r] = st[t][r] * a.scale_log2 + mk[r] * log2e;
+    }
+    if (nvalid < kStep) {  // wave-uniform: only a slice's partial last step
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (16 * (j >> 2) + 4 * g + (j & 3) >= nvalid) sv[j] = kNegInf;
+    }
+
+    // -- online softmax for column m (the 4 lanes l, l^16, l^32, l^48 share it)
+    float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
+                       fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
+    tmax = grp4_max(tmax);
+    const float m_new = fmaxf(m_run, tmax);
+    const float m_use = (m_new == kNegInf) ? 0.0f : m_new;
+    // rescale only when a max moved (never at the first step: o, l are still 0)
+    if (!first && __builtin_amdgcn_ballot_w64(m_new != m_run)) {
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+        l_run *= alpha;
+#pragma unroll
+        for (int c = 0; c < NC; c++) o[c] *= alpha;
+        if constexpr (kVQ) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) corr[b] *= alpha;
+        }
+    }
+    m_run = m_new;
+    float pv[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) pv[j] = __builtin_amdgcn_exp2f(sv[j] - m_use);
+    l_run += ((pv[0] + pv[1]) + (pv[2] + pv[3])) + ((pv[4] + pv[5]) + (pv[6] + pv[7]));
+
+    f16x8 pb;
+    pb.s0 = (f16)pv[0]; pb.s1 = (f16)pv[1]; pb.s2 = (f16)pv[2]; pb.s3 = (f16)pv[3];
+    pb.s4 = (f16)pv[4]; pb.s5 = (f16)pv[5]; pb.s6 = (f16)pv[6]; pb.s7 = (f16)pv[7];
+
+    // -- O^T += V^T.P^T (V of step s landed)
+    wait_v();
+    if constexpr (C::VTT == FATTN_TYPE_F16) {
+#pragma unroll
+        for (int c = 0; c < NC; c++) o[c] = mfma16(v_operand_f16<VT, D>(vb, c, g, i16), pb, o[c]);
+    } else {
+        const int rA = 4 * g, rB = 16 + 4 * g;
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            constexpr int BB = TypeInfo<C::VTT>::block_bytes;
+            // block-b scales of this lane's 8 rows (4g..4g+3, 16+4g..16+4g+3):
+            // the dword holding each, then f16 pairs {row r, row r+1}
+            uint32_t sw[8];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                sw[r] = *(const uint32_t*)(vb + (rA + r) * C::rowV + ((BB * b) & ~3));
+                sw[4 + r] = *(const uint32_t*)(vb + (rB + r) * C::rowV + ((BB * b) & ~3));
+            }
+            const uint32_t sel = ((BB * b) & 2) ? 0x07060302u : 0x05040100u;  // b is unrolled
+            const f16x2 d01 = as_h2(perm_b32(sw[1], sw[0], sel)), d23 = as_h2(perm_b32(sw[3], sw[2], sel));
+            const f16x2 d45 = as_h2(perm_b32(sw[5], sw[4], sel)), d67 = as_h2(perm_b32(sw[7], sw[6], sel));
+            // P'_b = P * d_b (element j <-> row of element j of the A operand)
+            f16x8 pbd;
+            pbd.s01 = pb.s01 * d01;
+            pbd.s23 = pb.s23 * d23;
+            pbd.s45 = pb.s45 * d45;
+            pbd.s67 = pb.s67 * d67;
+            const f16x2 one2 = {(f16)1.0f, (f16)1.0f};
+            corr[b] = __builtin_amdgcn_fdot2(pbd.s01, one2, corr[b], false);
+            corr[b] = __builtin_amdgcn_fdot2(pbd.s23, one2, corr[b], false);
+            corr[b] = __builtin_amdgcn_fdot2(pbd.s45, one2, corr[b], false);
+            corr[b] = __builtin_amdgcn_fdot2(pbd.s67, one2, corr[b], false);
+            if constexpr (kVQ8) {
+                // one u16 per row carries columns 2i (-> tile E_b) and 2i+1 (-> tile O_b)
+                const uint8_t* cp = vb + b * BB + 2 + 2 * i16;
+                uint32_t w[8];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    w[r] = *(const uint16_t*)(cp + (rA + r) * C::rowV);
+                    w[4 + r] = *(const uint16_t*)(cp + (rB + r) * C::rowV);
+                }
+                u32x4 ae, ao;  // f16 pairs 1152 + q (exact)
+#pragma unroll
+                for (int pr = 0; pr < 4; pr++) {
+                    // bytes [e_r, o_r, e_r+1, o_r+1] -> xor 0x80 -> f16 magic 0x64xx
+                    const uint32_t t2 = (w[2 * pr] | (w[2 * pr + 1] << 16)) ^ 0x80808080u;
+                    ae[pr] = perm_b32(0x64646464u, t2, 0x04020400u);
+                    ao[pr] = perm_b32(0x64646464u, t2, 0x04030401u);
+                }
+                o[2 * b] = mfma16(__builtin_bit_cast(f16x8, ae), pbd, o[2 * b]);
+                o[2 * b + 1] = mfma16(__builtin_bit_cast(f16x8, ao), pbd, o[2 * b + 1]);
+            } else {  // Q4_0: byte i carries column i (low nibble) and 16+i (high nibble)
+                const uint8_t* cp = vb + b * BB + 2 + i16;
+                uint32_t w[8];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    w[r] = cp[(rA + r) * C::rowV];
+                    w[4 + r] = cp[(rB + r) * C::rowV];
+                }
+                u32x4 al, ah;  // f16 pairs 1032 + (nib - 8) (exact)
+#pragma unroll
+                for (int pr = 0; pr < 4; pr++) {
+                    const uint32_t x = w[2 * pr] | (w[2 * pr + 1] << 16);
+                    al[pr] = (x & 0x000F000Fu) | 0x64006400u;
+                    ah[pr] = ((x >> 4) & 0x000F000Fu) | 0x64006400u;
+                }
+                o[2 * b] = mfma16(__builtin_bit_cast(f16x8, al), pbd, o[2 * b]);
+                o[2 * b + 1] = mfma16(__builtin_bit_cast(f16x8, ah), pbd, o[2 * b + 1]);
+            }
+        }
+    }
+
 }
 
 template <int KT, int VT, int D, int GRAN, bool HM>
@@ -585,12 +925,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     constexpr int NB = D / QK;   // 32-wide k-steps of QK^T (= ggml blocks per row)
     constexpr int NC = D / 16;   // 16-wide output column groups (MFMA tiles of O^T)
     constexpr float kNegInf = -__builtin_inff();
-    constexpr bool kVQ8 = C::VTT == FATTN_TYPE_Q8_0;
-    constexpr bool kVQ = C::VTT != FATTN_TYPE_F16;
     // quantised V: the A operand is the exact integer code plus the magic-number
     // offset (1152 for Q8_0, 1032 for Q4_0) with the block scale folded into P;
-    // corr[b] accumulates sum(P * d_b) so the offset comes off once at the end
-    constexpr float kVOff = kVQ8 ? 1152.0f : 1032.0f;
+    // corr[b] accumulates sum(P * d_b) so the offset comes off once in the epilogue
 
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane lets the compiler see it, so the
@@ -693,7 +1030,6 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
 #pragma unroll
     for (int b = 0; b < NB; b++) corr[b] = 0.0f;
 
-    const float log2e = 1.4426950408889634f;
     int cur = 0;  // buffer of step s
     for (int s = 0; s < nsteps; s++) {
         const int ahead = min(nbuf - 1, nsteps - 1 - s);  // steps issued after step s
@@ -710,147 +1046,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
         cur = (cur + 1 == nbuf) ? 0 : cur + 1;
         continue;
 #endif
-        const uint8_t* buf = wbuf + cur * C::stepBytes;
-        const uint8_t* kb = buf;
-        const uint8_t* vb = buf + C::kBytes;
-        const uint8_t* mb = buf + C::kBytes + C::vBytes;
         const int n0 = w_lo + s * kStep;
-        const int nvalid = min(kStep, w_hi - n0);
-
-        // -- S^T = K.Q^T for the two 16-row tiles
-        f32x4 st[2];
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            st[t] = f32x4{0, 0, 0, 0};
-            if constexpr (KT == FATTN_TYPE_F16) {
-#pragma unroll
-                for (int b = 0; b < NB; b++) st[t] = mfma16(k_operand<KT, D>(kb, 16 * t + i16, g, b, 0), qop[b], st[t]);
-            } else {
-                const RowScales<KT, D> ks = row_scales<KT, D>(kb + (16 * t + i16) * C::rowK);
-#pragma unroll
-                for (int b = 0; b < NB; b++)
-                    st[t] = mfma16(k_operand<KT, D>(kb, 16 * t + i16, g, b, scale_bits(ks, b)), qop[b], st[t]);
-            }
-        }
-
-        // -- scale + mask (log2 domain); positions past this wave's slice -> -inf
-        float sv[8];
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            float mk[4] = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (HM) {
-                const uint8_t* mp = mb + (mq < a.QPT ? mq : 0) * (kStep * 2) + (16 * t + 4 * g) * 2;
-                const u32x2 mw = *(const u32x2*)mp;
-                const f16x2 m01 = as_h2(mw.x), m23 = as_h2(mw.y);
-                mk[0] = (float)m01.x; mk[1] = (float)m01.y; mk[2] = (float)m23.x; mk[3] = (float)m23.y;
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r++) sv[4 * t + r] = st[t][r] * a.scale_log2 + mk[r] * log2e;
-        }
-        if (nvalid < kStep) {  // wave-uniform: only a slice's partial last step
-#pragma unroll
-            for (int j = 0; j < 8; j++)
-                if (16 * (j >> 2) + 4 * g + (j & 3) >= nvalid) sv[j] = kNegInf;
-        }
-
-        // -- online softmax for column m (the 4 lanes l, l^16, l^32, l^48 share it)
-        float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
-                           fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
-        tmax = grp4_max(tmax);
-        const float m_new = fmaxf(m_run, tmax);
-        const float m_use = (m_new == kNegInf) ? 0.0f : m_new;
-        // rescale only when a max moved (never at the first step: o, l are still 0)
-        if (s > 0 && __builtin_amdgcn_ballot_w64(m_new != m_run)) {
-            const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
-            l_run *= alpha;
-#pragma unroll
-            for (int c = 0; c < NC; c++) o[c] *= alpha;
-            if constexpr (kVQ) {
-#pragma unroll
-                for (int b = 0; b < NB; b++) corr[b] *= alpha;
-            }
-        }
-        m_run = m_new;
-        float pv[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) pv[j] = __builtin_amdgcn_exp2f(sv[j] - m_use);
-        l_run += ((pv[0] + pv[1]) + (pv[2] + pv[3])) + ((pv[4] + pv[5]) + (pv[6] + pv[7]));
-
-        f16x8 pb;
-        pb.s0 = (f16)pv[0]; pb.s1 = (f16)pv[1]; pb.s2 = (f16)pv[2]; pb.s3 = (f16)pv[3];
-        pb.s4 = (f16)pv[4]; pb.s5 = (f16)pv[5]; pb.s6 = (f16)pv[6]; pb.s7 = (f16)pv[7];
-
-        // -- O^T += V^T.P^T (V of step s landed)
-        wait_steps<NI>(ahead);
-        if constexpr (C::VTT == FATTN_TYPE_F16) {
-#pragma unroll
-            for (int c = 0; c < NC; c++) o[c] = mfma16(v_operand_f16<VT, D>(vb, c, g, i16), pb, o[c]);
-        } else {
-            const int rA = 4 * g, rB = 16 + 4 * g;
-#pragma unroll
-            for (int b = 0; b < NB; b++) {
-                constexpr int BB = TypeInfo<C::VTT>::block_bytes;
-                // block-b scales of this lane's 8 rows (4g..4g+3, 16+4g..16+4g+3):
-                // the dword holding each, then f16 pairs {row r, row r+1}
-                uint32_t sw[8];
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    sw[r] = *(const uint32_t*)(vb + (rA + r) * C::rowV + ((BB * b) & ~3));
-                    sw[4 + r] = *(const uint32_t*)(vb + (rB + r) * C::rowV + ((BB * b) & ~3));
-                }
-                const uint32_t sel = ((BB * b) & 2) ? 0x07060302u : 0x05040100u;  // b is unrolled
-                const f16x2 d01 = as_h2(perm_b32(sw[1], sw[0], sel)), d23 = as_h2(perm_b32(sw[3], sw[2], sel));
-                const f16x2 d45 = as_h2(perm_b32(sw[5], sw[4], sel)), d67 = as_h2(perm_b32(sw[7], sw[6], sel));
-                // P'_b = P * d_b (element j <-> row of element j of the A operand)
-                f16x8 pbd;
-                pbd.s01 = pb.s01 * d01;
-                pbd.s23 = pb.s23 * d23;
-                pbd.s45 = pb.s45 * d45;
-                pbd.s67 = pb.s67 * d67;
-                const f16x2 one2 = {(f16)1.0f, (f16)1.0f};
-                corr[b] = __builtin_amdgcn_fdot2(pbd.s01, one2, corr[b], false);
-                corr[b] = __builtin_amdgcn_fdot2(pbd.s23, one2, corr[b], false);
-                corr[b] = __builtin_amdgcn_fdot2(pbd.s45, one2, corr[b], false);
-                corr[b] = __builtin_amdgcn_fdot2(pbd.s67, one2, corr[b], false);
-                if constexpr (kVQ8) {
-                    // one u16 per row carries columns 2i (-> tile E_b) and 2i+1 (-> tile O_b)
-                    const uint8_t* cp = vb + b * BB + 2 + 2 * i16;
-                    uint32_t w[8];
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        w[r] = *(const uint16_t*)(cp + (rA + r) * C::rowV);
-                        w[4 + r] = *(const uint16_t*)(cp + (rB + r) * C::rowV);
-                    }
-                    u32x4 ae, ao;  // f16 pairs 1152 + q (exact)
-#pragma unroll
-                    for (int pr = 0; pr < 4; pr++) {
-                        // bytes [e_r, o_r, e_r+1, o_r+1] -> xor 0x80 -> f16 magic 0x64xx
-                        const uint32_t t2 = (w[2 * pr] | (w[2 * pr + 1] << 16)) ^ 0x80808080u;
-                        ae[pr] = perm_b32(0x64646464u, t2, 0x04020400u);
-                        ao[pr] = perm_b32(0x64646464u, t2, 0x04030401u);
-                    }
-                    o[2 * b] = mfma16(__builtin_bit_cast(f16x8, ae), pbd, o[2 * b]);
-                    o[2 * b + 1] = mfma16(__builtin_bit_cast(f16x8, ao), pbd, o[2 * b + 1]);
-                } else {  // Q4_0: byte i carries column i (low nibble) and 16+i (high nibble)
-                    const uint8_t* cp = vb + b * BB + 2 + i16;
-                    uint32_t w[8];
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        w[r] = cp[(rA + r) * C::rowV];
-                        w[4 + r] = cp[(rB + r) * C::rowV];
-                    }
-                    u32x4 al, ah;  // f16 pairs 1032 + (nib - 8) (exact)
-#pragma unroll
-                    for (int pr = 0; pr < 4; pr++) {
-                        const uint32_t x = w[2 * pr] | (w[2 * pr + 1] << 16);
-                        al[pr] = (x & 0x000F000Fu) | 0x64006400u;
-                        ah[pr] = ((x >> 4) & 0x000F000Fu) | 0x64006400u;
-                    }
-                    o[2 * b] = mfma16(__builtin_bit_cast(f16x8, al), pbd, o[2 * b]);
-                    o[2 * b + 1] = mfma16(__builtin_bit_cast(f16x8, ah), pbd, o[2 * b + 1]);
-                }
-            }
-        }
+        split_step<KT, VT, D, HM>(a, wbuf + cur * C::stepBytes, qop, mq, g, i16, min(kStep, w_hi - n0), s == 0, m_run,
+                                  l_run, o, corr, [&] { wait_steps<NI>(ahead); });
 
         // -- refill this buffer with step s + nbuf
         if (s + nbuf < nsteps) {
@@ -872,142 +1070,8 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     return;
 #endif
     FATTN_STAMP(10);
-
-    // ---- per-wave state -> LDS (this wave's own region), then merge the 4 waves
-    const float l_tot = grp4_sum(l_run);
-    if constexpr (kVQ) {
-        // O^T tiles of block b (columns 32b..32b+31) carry kVOff * sum(P'_b) too
-#pragma unroll
-        for (int b = 0; b < NB; b++) {
-            const float cb = kVOff * grp4_sum(corr[b]);
-            o[2 * b] -= cb;
-            o[2 * b + 1] -= cb;
-        }
-    }
-    if constexpr (D == 128) {
-        if (a.wave_merge) {
-            wave_merge_epilogue<D, kVQ8>(a, o, m_run, l_tot, chunk, wave, lane, qt, hs, ik2, iq3);
-            return;
-        }
-    }
-    constexpr int MS = C::kMergeStride;
-    float* mo = (float*)wbuf;                      // [16][MS]
-    float* mml = (float*)(wbuf + kRows * MS * 4);  // [16][2]
-    // valid rows of this tile form a prefix [0, rv); only those are merged
-    const int rv = tile_rows(a, qt, hs);
-    if (m >= rv) {
-        // nothing of this column is needed
-    } else if constexpr (kVQ8) {
-        // tile E_b holds columns 32b + 2(4g+reg), O_b the odd neighbours
-#pragma unroll
-        for (int b = 0; b < NB; b++) {
-            const f32x4 e = o[2 * b], od = o[2 * b + 1];
-            *(f32x4*)(mo + m * MS + 32 * b + 8 * g) = f32x4{e.x, od.x, e.y, od.y};
-            *(f32x4*)(mo + m * MS + 32 * b + 8 * g + 4) = f32x4{e.z, od.z, e.w, od.w};
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < NC; c++) *(f32x4*)(mo + m * MS + 16 * c + 4 * g) = o[c];
-    }
-    if (g == 0 && m < rv) {
-        mml[2 * m] = m_run;
-        mml[2 * m + 1] = l_tot;
-    }
-    __syncthreads();
-    FATTN_STAMP(11);
-
-    constexpr int EPT = D / 16;  // outputs per thread: 16 rows x D over 256 threads
-    const int tm = threadIdx.x / 16;
-    const int tj = threadIdx.x % 16;
-    const int d0 = tj * EPT;
-    float M = kNegInf;
-    float mw[kSplitWaves], lw[kSplitWaves];
-#pragma unroll
-    for (int w = 0; w < kSplitWaves; w++) {
-        const float* ml = (const float*)(smem + w * a.wave_bytes + kRows * MS * 4);
-        mw[w] = tm < rv ? ml[2 * tm] : kNegInf;
-        lw[w] = tm < rv ? ml[2 * tm + 1] : 0.0f;
-        M = fmaxf(M, mw[w]);
-    }
-    float L = 0.0f;
-    float acc[EPT];
-#pragma unroll
-    for (int e = 0; e < EPT; e++) acc[e] = 0.0f;
-    if (tm < rv) {
-#pragma unroll
-        for (int w = 0; w < kSplitWaves; w++) {
-            const float wt = (mw[w] == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mw[w] - M);
-            L += wt * lw[w];
-            const float* ow = (const float*)(smem + w * a.wave_bytes) + tm * MS + d0;
-#pragma unroll
-            for (int e = 0; e < EPT; e++) acc[e] += wt * ow[e];
-        }
-    }
-    auto dst_row = [&](int r) -> float* {
-        const int rq = div_R(a, r);
-        const int riq1 = qt * a.QPT + rq;
-        const int riq2 = ik2 * a.rk2 + hs * a.R + (r - rq * a.R);
-        return a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D;
-    };
-    if (a.n_chunks == 1) {
-        if (tm < rv) {
-            float* out = dst_row(tm) + d0;
-            const float inv = 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
-#pragma unroll
-            for (int e = 0; e < EPT; e += 4) {
-                f32x4 v;
-                v.x = L == 0.0f ? __builtin_nanf("") : acc[e] * inv;
-                v.y = L == 0.0f ? __builtin_nanf("") : acc[e + 1] * inv;
-                v.z = L == 0.0f ? __builtin_nanf("") : acc[e + 2] * inv;
-                v.w = L == 0.0f ? __builtin_nanf("") : acc[e + 3] * inv;
-                *(f32x4*)(out + e) = v;
-            }
-        }
-        FATTN_STAMP(12);
-        return;
-    }
-
-#ifdef FATTN_DIAG_NOPUBLISH
-    // diagnostic build only: stop after the 4-wave merge
-    if (acc[0] == 12345.0f) a.dst[0] = L;
-    return;
-#endif
-    // ---- several chunks: the workgroup that arrives last for the tile merges
-    // all partials (no second launch).  Hand-off (MI355X_MICROARCH.md,
-    // inter-workgroup visibility, first row of the sc1 table): partial bytes
-    // stored sc1 (write-through), each storing wave drains vmcnt, barrier, ONE
-    // agent-scope atomic add per workgroup on the tile's own 256-B line; the
-    // last adder reads the others' partials with sc1 loads -- all of them in
-    // one round trip -- while its own stays in LDS.
-    const int64_t tile = (int64_t)iq3 * gridDim.y + y;
-    if (tm < rv) {
-        const int64_t slot = (tile * a.n_chunks + chunk) * kRows + tm;
-        auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
-#pragma unroll
-        for (int e = 0; e < EPT; e += 4)
-            st_sc1(a.ws_o + slot * D + d0 + e, u32x4{bits(acc[e]), bits(acc[e + 1]), bits(acc[e + 2]), bits(acc[e + 3])});
-        if (tj == 0) st_sc1_x2(a.ws_ml + 2 * slot, u32x2{bits(M), bits(L)});
-    }
-    // every storing wave drains: the merging workgroup reads its own partial back too
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef FATTN_DIAG_NOATOMIC
-    return;  // diagnostic build only: stop after the published stores drained
-#endif
-    __syncthreads();  // every storing wave has drained; every wave is done reading the merge image
-    int* last_flag = (int*)smem;
-    if (threadIdx.x == 0) {
-        uint32_t* cnt = a.ws_cnt + tile * kCntStride;
-        const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == (uint32_t)(a.n_chunks - 1);
-        // every chunk has arrived: re-arm the counter for the next launch
-        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *last_flag = last;
-    }
-    __syncthreads();
-    FATTN_STAMP(12);
-    if (!*last_flag) return;
-    combine_tile<D, (D == 128 && KT != FATTN_TYPE_F16) ? 8 : 2>(a, tile, qt, hs, ik2, iq3, rv, 0, smem);
-    FATTN_STAMP(13);
+    split_epilogue<KT, VT, D>(a, o, m_run, l_run, corr, wave, lane, qt, hs, ik2, iq3, y, chunk, smem, a.wave_bytes, true,
+                              false);
 }
 
 // ---------------------------------------------------------------- combine

@@ -34,6 +34,7 @@ ERRORS = {
 EXPORTS = (
     "fattn_workspace_size", "fattn_workspace_init", "fattn_ext", "fattn_ext_events", "fattn_ext_f16_launch", "fattn_row_workspace_size", "fattn_row",
     "fattn_dequantize", "fattn_quantize", "fattn_strerror", "fattn_row_size", "fattn_version", "fattn_set_option",
+    "fattn_describe", "fattn_cpy",
 )
 OPT_MQ_ROWS_PER_WAVE = 1
 OPT_MQ_DISABLE = 2
@@ -48,6 +49,11 @@ OPT_SPLIT_WAVE_MERGE = 10
 OPT_SPLIT_PRIO = 11
 OPT_PF_SKIP = 12
 OPT_MQ_MIN_ROWS = 13
+OPT_DEC = 14
+OPT_DEC_LOADERS = 15
+OPT_DEC_COMPUTE = 16
+OPT_DEC_DIAG = 17
+OPT_DEC_AHEAD = 18
 
 
 class FattnError(RuntimeError):
@@ -110,6 +116,10 @@ def lib() -> C.CDLL:
         L.fattn_row_size.restype = sz
         L.fattn_row_size.argtypes = [C.c_int, i64]
         L.fattn_version.restype = C.c_char_p
+        L.fattn_cpy.restype = C.c_int
+        L.fattn_cpy.argtypes = [C.POINTER(FattnTensor), C.POINTER(FattnTensor), vp]
+        L.fattn_describe.restype = C.c_int
+        L.fattn_describe.argtypes = [C.POINTER(FattnParams), C.c_char_p, sz]
         _lib = L
     return _lib
 
@@ -175,6 +185,13 @@ def ext_params(q: View, k: View, v: View, mask: Optional[View], dst_ptr: int, sc
 
 def workspace_size(p: FattnParams) -> int:
     return int(lib().fattn_workspace_size(C.byref(p)))
+
+
+def describe(p: FattnParams) -> str:
+    """The kernel(s) and plan fattn_ext would launch for these params (diagnostic)."""
+    buf = C.create_string_buffer(512)
+    _check(lib().fattn_describe(C.byref(p), buf, len(buf)), "fattn_describe")
+    return buf.value.decode()
 
 
 def flash_attn_ext(p: FattnParams, stream=None, ev_begin=None, ev_end=None):
@@ -248,6 +265,9 @@ class Attention:
         if dst is not None:
             self.p.dst = dst
 
+    def describe(self) -> str:
+        return describe(self.p)
+
     def __call__(self, stream=None, ev_begin=None, ev_end=None):
         flash_attn_ext(self.p, stream, ev_begin, ev_end)
         return self.dst
@@ -262,6 +282,13 @@ def quantize(x, typ: int, stream=None):
     out = torch.empty((rows, row_size(typ, k)), dtype=torch.uint8, device=x.device)
     _check(lib().fattn_quantize(typ, _tptr(x), _tptr(out), k, rows, _stream(stream)), "fattn_quantize")
     return out
+
+
+def cpy(src: View, dst: View, stream=None):
+    """GGML_OP_CPY f32 -> F16 / Q8_0 / Q4_0 into a strided view (the KV-cache
+    write, include/fattn.h fattn_cpy); src/dst are ggml views of device memory."""
+    s, d = src.c(), dst.c()
+    _check(lib().fattn_cpy(C.byref(s), C.byref(d), _stream(stream)), "fattn_cpy")
 
 
 def dequantize(blocks, typ: int, k: int, stream=None):

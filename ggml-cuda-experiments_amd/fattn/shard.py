@@ -48,14 +48,46 @@ def shard_heads(H: int, Hkv: int, world: int, rank: int) -> HeadShard:
     return HeadShard(rank, world, kv0, kv0 + per, kv0 * r, (kv0 + per) * r)
 
 
+def narrow(view, dim: int, start: int, count: int):
+    """Zero-copy sub-view of a ggml view (fattn.View): elements [start, start+count)
+    of ggml dimension `dim` -- the pointer moves by start * nb[dim], the
+    strides stay.  `view.ptr` may be a device pointer or a byte offset."""
+    from fattn import View
+    if not 0 <= start <= start + count <= view.ne[dim]:
+        raise ValueError(f"narrow dim {dim} [{start}, {start + count}) of {view.ne[dim]}")
+    ne = list(view.ne)
+    ne[dim] = count
+    return View(view.ptr + start * view.nb[dim], view.type, tuple(ne), tuple(view.nb))
+
+
+def head_views(q, k, v, sh: HeadShard):
+    """The rank's FLASH_ATTN_EXT sub-problem, zero-copy: q heads [h0, h1) and
+    kv heads [kv0, kv1) (ggml dim 2 of q / k / v).  The mask is shared by all
+    heads (a row per query) and the rank's dst is its own contiguous
+    [S][n_q][h1-h0][D]; the GQA map ik2 = iq2 / r (src/flash-llama.h:128-140)
+    holds inside the slice because h0 = kv0 * r."""
+    return narrow(q, 2, sh.h0, sh.n_heads), narrow(k, 2, sh.kv0, sh.n_kv), narrow(v, 2, sh.kv0, sh.n_kv)
+
+
+def assemble_heads(parts):
+    """[world] x [..., S, n_q, H/world, D] per-rank outputs stacked on a leading
+    axis -> [..., S, n_q, H, D] in the ggml dst layout (src/flash-llama.h:434):
+    rank w holds heads [w*Hl, (w+1)*Hl).  Works on torch tensors and numpy."""
+    world = parts.shape[0]
+    *lead, S, NQ, Hl, D = parts.shape[1:]
+    nl = len(lead)
+    perm = tuple(range(1, 1 + nl)) + (1 + nl, 2 + nl, 0, 3 + nl, 4 + nl)
+    x = parts.permute(*perm) if hasattr(parts, "permute") else parts.transpose(perm)
+    return x.reshape(*lead, S, NQ, world * Hl, D)
+
+
 def gather_heads(local, group=None):
-    """local: this rank's output [S][n_q][H/world][D] (contiguous).  Returns the
-    full [S][n_q][H][D] on every rank via one all_gather_into_tensor."""
+    """local: this rank's output [..., S, n_q, H/world, D] (contiguous).  Returns
+    the full [..., S, n_q, H, D] on every rank via ONE all_gather_into_tensor
+    (RCCL over xGMI on the GPU box, gloo on the CPU) and assemble_heads."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    S, NQ, Hl, D = local.shape
-    buf = torch.empty((world * S, NQ, Hl, D), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(buf, local.contiguous(), group=group)
-    # [world][S][NQ][Hl][D] -> [S][NQ][world*Hl][D]: rank w holds heads [w*Hl, (w+1)*Hl)
-    return buf.view(world, S, NQ, Hl, D).permute(1, 2, 0, 3, 4).reshape(S, NQ, world * Hl, D)
+    buf = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(buf.view(world * local.shape[0], *local.shape[1:]), local.contiguous(), group=group)
+    return assemble_heads(buf)

@@ -10,11 +10,18 @@
 // additive: a pass/fail threshold and exit code (the reference prints a diff
 // with no threshold), warmup + repeated timing (median), and K/V types.
 //
-//   --no-kv-parallel     one KV chunk per head (the flash_attn_ext path, kernel_test.h:180-199)
+//   --no-kv-parallel     the flash_attn_ext branch (kernel_test.h:180-199): the call goes
+//                        through fattn_ext_f16_launch with kernel_test.h:191-198's argument
+//                        list -- 32-row padded mask (row 0 = the mask, kernel_test.h:74-85),
+//                        ne31 = 32, nb31 = kv_size*2, nb01 = nb02 = head_dim*4, V not
+//                        transposed.  The default branch is flash_attn_row + fa_reduce
+//                        (kernel_test.h:161-162): fattn_row with V transposed.
 //   --n-warps N          accepted for compatibility (kernel_test.h:9-13); the gfx950
-//                        kernel always runs 4 wave64s per workgroup
-//   --kv-size N          KV length, min 256 (kernel_test.h:14-18)
+//                        kernels pick their own wave counts
+//   --kv-size N          KV length, min 256 on the GPU path (kernel_test.h:14-18)
 //   --kv-type T          f16 (default, as the reference) | q8_0 | q4_0
+//   --cpu-only           the CPU reference alone (BASELINE config 1: no GPU is touched,
+//                        any kv_size); with --dump FILE its f32 output is written raw
 //   --head-dim D --heads H --kv-heads Hkv --iters I --tol T
 #include <hip/hip_runtime.h>
 
@@ -145,7 +152,8 @@ int parse_type(const std::string& s) {
 int main(int argc, const char* argv[]) {
     int kv_size = 512, num_warps = 8, head_dim = 128, num_heads = 32, num_kv_heads = 8, iters = 20;
     int kv_type = FATTN_TYPE_F16;
-    bool parallel_kv = true;
+    bool parallel_kv = true, cpu_only = false;
+    const char* dump = nullptr;
     float tol = 1e-3f;
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
@@ -158,7 +166,9 @@ int main(int argc, const char* argv[]) {
         };
         if (a == "--no-kv-parallel") parallel_kv = false;
         else if (a == "--n-warps") num_warps = atoi(next());
-        else if (a == "--kv-size") kv_size = std::max(256, atoi(next()));
+        else if (a == "--kv-size") kv_size = atoi(next());
+        else if (a == "--cpu-only") cpu_only = true;
+        else if (a == "--dump") dump = next();
         else if (a == "--kv-type") kv_type = parse_type(next());
         else if (a == "--head-dim") head_dim = atoi(next());
         else if (a == "--heads") num_heads = atoi(next());
@@ -172,16 +182,12 @@ int main(int argc, const char* argv[]) {
     }
     if (num_warps != 8 && num_warps != 4 && num_warps != 2 && num_warps != 1)
         printf("invalid num_warps, should be 2, 4, 8\n");  // kernel_test.h:176-178 (informational)
-
-    hipDeviceProp_t prop;
-    HIP_CHECK(hipGetDeviceProperties(&prop, 0));
-    printf("GPU: %s (%s), CUs: %d, LDS/block max: %zu KB, HBM: %zu MB\n", prop.name, prop.gcnArchName,
-           prop.multiProcessorCount, prop.sharedMemPerBlock / 1024, prop.totalGlobalMem >> 20);
+    if (!cpu_only) kv_size = std::max(256, kv_size);      // kernel_test.h:14-18
 
     const int D = head_dim, H = num_heads, Hkv = num_kv_heads, N = kv_size;
     const float scale = 1.0f / sqrtf((float)D);
-    if (H % Hkv) {
-        fprintf(stderr, "heads must be a multiple of kv-heads\n");
+    if (H <= 0 || Hkv <= 0 || N <= 0 || D <= 0 || H % Hkv) {
+        fprintf(stderr, "heads must be a positive multiple of kv-heads\n");
         return 2;
     }
     std::vector<float> query((size_t)D * H), key((size_t)D * N * Hkv), value((size_t)D * N * Hkv), mask(N);
@@ -190,20 +196,43 @@ int main(int argc, const char* argv[]) {
     random_fill(value);
     random_fill(mask);
 
+    if (cpu_only) {  // BASELINE config 1: kernel_test.h:50-66 on the host, nothing else
+        std::vector<float> out((size_t)D * H);
+        cpu_reference(query, key, value, mask, out, N, D, H, Hkv, scale);
+        print_array("Reference", out.data(), std::min(16, D * H));
+        if (dump) {
+            FILE* f = fopen(dump, "wb");
+            if (!f || fwrite(out.data(), sizeof(float), out.size(), f) != out.size()) {
+                fprintf(stderr, "cannot write %s\n", dump);
+                return 2;
+            }
+            fclose(f);
+        }
+        return 0;
+    }
+
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, 0));
+    printf("GPU: %s (%s), CUs: %d, LDS/block max: %zu KB, HBM: %zu MB\n", prop.name, prop.gcnArchName,
+           prop.multiProcessorCount, prop.sharedMemPerBlock / 1024, prop.totalGlobalMem >> 20);
+
     hipStream_t stream;
     HIP_CHECK(hipStreamCreate(&stream));
     float *d_q, *d_out, *d_kf, *d_vf;
-    void *d_k, *d_v, *d_mask, *d_ws;
+    void *d_k, *d_v, *d_mask;
     const size_t rb = fattn_row_size(kv_type, D);
     HIP_CHECK(hipMalloc(&d_q, sizeof(float) * D * H));
     HIP_CHECK(hipMalloc(&d_out, sizeof(float) * D * H));
     HIP_CHECK(hipMalloc(&d_k, rb * N * Hkv));
     HIP_CHECK(hipMalloc(&d_v, rb * N * Hkv));
-    HIP_CHECK(hipMalloc(&d_mask, 2 * (size_t)N));
+    // mask f16: one row for flash_attn_row; 32 rows (row 0 = the mask, the rest
+    // zeros) for flash_attn_ext (kernel_test.h:74-85)
+    const int mask_rows = parallel_kv ? 1 : 32;
+    HIP_CHECK(hipMalloc(&d_mask, 2 * (size_t)N * mask_rows));
     HIP_CHECK(hipMemcpyAsync(d_q, query.data(), sizeof(float) * D * H, hipMemcpyHostToDevice, stream));
-    std::vector<uint16_t> mask16(N);
+    std::vector<uint16_t> mask16((size_t)N * mask_rows, f2h(0.0f));
     for (int i = 0; i < N; i++) mask16[i] = f2h(mask[i]);
-    HIP_CHECK(hipMemcpyAsync(d_mask, mask16.data(), 2 * (size_t)N, hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipMemcpyAsync(d_mask, mask16.data(), 2 * mask16.size(), hipMemcpyHostToDevice, stream));
 
     // K/V storage.  f16: K [Hkv][N][D]; V transposed [Hkv][D][N] on the parallel
     // path (-DFA_KV_BLOCK_256, kernel_test.h:96-105), row-major otherwise.
@@ -246,45 +275,59 @@ int main(int argc, const char* argv[]) {
     cpu_reference(query, kref, vref, mask, qkv, N, D, H, Hkv, scale);
     print_array("Reference", qkv.data(), 16);
 
-    // GPU launch description
-    fattn_params p;
-    std::memset(&p, 0, sizeof(p));
-    p.q = {d_q, FATTN_TYPE_F32, 0, {D, 1, H, 1}, {4, (int64_t)D * H * 4, (int64_t)D * 4, (int64_t)D * H * 4}};
-    const int64_t eb = kv_type == FATTN_TYPE_F16 ? 2 : (int64_t)fattn_row_size(kv_type, 32);
-    p.k = {d_k, kv_type, 0, {D, N, Hkv, 1}, {eb, (int64_t)rb, (int64_t)rb * N, (int64_t)rb * N * Hkv}};
-    if (vtrans)
-        p.v = {d_v, kv_type, 0, {D, N, Hkv, 1}, {(int64_t)N * 2, 2, (int64_t)rb * N, (int64_t)rb * N * Hkv}};
-    else
-        p.v = {d_v, kv_type, 0, {D, N, Hkv, 1}, {eb, (int64_t)rb, (int64_t)rb * N, (int64_t)rb * N * Hkv}};
-    p.mask = {d_mask, FATTN_TYPE_F16, 0, {N, 1, 1, 1}, {2, (int64_t)N * 2, (int64_t)N * 2, (int64_t)N * 2}};
-    p.dst = d_out;
-    p.scale = scale;
-    p.kv_chunk = parallel_kv ? 0 : N;  // --no-kv-parallel: whole KV per workgroup
-    const size_t ws = fattn_workspace_size(&p);
-    HIP_CHECK(hipMalloc(&d_ws, std::max<size_t>(ws, 16)));
-    p.workspace = d_ws;
-    p.workspace_bytes = std::max<size_t>(ws, 16);
-    if (int zr = fattn_workspace_init(d_ws, p.workspace_bytes, stream)) {
+    // GPU launch: fattn_row (kernel_test.h:161-162) or the positional
+    // flash_attn_ext argument list (kernel_test.h:191-198); both on `stream`,
+    // the first call untimed (warmup), then `iters` event-timed calls
+    void* d_ws = nullptr;
+    size_t ws_bytes = 0;
+    const int r_kv_heads = H / Hkv;
+    if (parallel_kv) {
+        if (kv_type != FATTN_TYPE_F16) {
+            fprintf(stderr, "the flash_attn_row branch takes f16 K/V (use --no-kv-parallel for %s)\n",
+                    kv_type == FATTN_TYPE_Q8_0 ? "q8_0" : "q4_0");
+            return 2;
+        }
+        ws_bytes = fattn_row_workspace_size(D, N, H);
+    } else {
+        ws_bytes = 1 << 24;  // covers every plan of these shapes; zero-filled once (fattn_workspace_init)
+    }
+    HIP_CHECK(hipMalloc(&d_ws, std::max<size_t>(ws_bytes, 16)));
+    ws_bytes = std::max<size_t>(ws_bytes, 16);
+    if (int zr = fattn_workspace_init(d_ws, ws_bytes, stream)) {
         fprintf(stderr, "fattn_workspace_init failed: %s\n", fattn_strerror(zr));
         return 2;
     }
-
-    int rc = fattn_ext(&p, stream);
+    auto launch = [&]() -> int {
+        if (parallel_kv)
+            return fattn_row(d_q, d_k, d_v, d_mask, d_ws, ws_bytes, d_out, D, N, H, scale, D * N, r_kv_heads, stream);
+        return fattn_ext_f16_launch(d_q, d_k, d_v, d_mask, d_out, scale,
+                                    D, 1, H, 1,
+                                    D, N, Hkv, 1,
+                                    32, N * 2,
+                                    D * 4, D * 4, D * H * 4,
+                                    (int)rb, (int)rb * N, (int)rb * N * Hkv,
+                                    D, H, 1, 1,
+                                    kv_type, kv_type, d_ws, ws_bytes, stream);
+    };
+    int rc = launch();
     if (rc) {
-        fprintf(stderr, "fattn_ext failed: %s\n", fattn_strerror(rc));
+        fprintf(stderr, "launch failed: %s\n", fattn_strerror(rc));
         return 2;
     }
     HIP_CHECK(hipStreamSynchronize(stream));
-    // timing: warmup done above; median of `iters` event-timed launches
     hipEvent_t start, stop;
     HIP_CHECK(hipEventCreate(&start));
     HIP_CHECK(hipEventCreate(&stop));
     std::vector<float> times;
     for (int it = 0; it < iters; it++) {
         HIP_CHECK(hipEventRecord(start, stream));
-        rc = fattn_ext(&p, stream);
+        rc = launch();
         HIP_CHECK(hipEventRecord(stop, stream));
         HIP_CHECK(hipEventSynchronize(stop));
+        if (rc) {
+            fprintf(stderr, "launch failed: %s\n", fattn_strerror(rc));
+            return 2;
+        }
         float ms = 0;
         HIP_CHECK(hipEventElapsedTime(&ms, start, stop));
         times.push_back(ms);

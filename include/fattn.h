@@ -140,10 +140,23 @@ enum {
                                        and the kernel walks only the live KV range, longest query tiles
                                        first (default; the workspace holds n_qt * N/64 flag bytes),
                                        1 = no pre-pass (every tile fetched; all -inf wave blocks still skipped) */,
-    FATTN_OPT_MQ_MIN_ROWS = 13      /* multi-query kernel only from this many packed (query x head) rows per kv
+    FATTN_OPT_MQ_MIN_ROWS = 13,     /* multi-query kernel only from this many packed (query x head) rows per kv
                                        head (default 256, minimum 32); fewer rows take the split-KV kernel */
+    FATTN_OPT_DEC = 14,             /* split-KV decode: 0 = auto, 1 = fattn_split_kernel (default), 2 = the
+                                       loader-wave kernel fattn_dec_kernel where the 16-B row layout allows */
+    FATTN_OPT_DEC_LOADERS = 15,     /* loader waves per fattn_dec_kernel workgroup: 2 (the only value kept) */
+    FATTN_OPT_DEC_COMPUTE = 16,     /* compute waves per fattn_dec_kernel workgroup: 4 (default) or 8 */
+    FATTN_OPT_DEC_DIAG = 17,        /* diagnostics only: 1 = fattn_dec_kernel skips the compute, 2 = skips the
+                                       K/V DMA (results are garbage) */
+    FATTN_OPT_DEC_AHEAD = 18        /* fattn_dec_kernel: 32-position steps in flight per loader wave (1..8,
+                                       default 8; vmcnt caps it at 63 / instructions per step) */
 };
 int fattn_set_option(int option, int value);
+
+/* Diagnostic: the kernel(s) fattn_ext would launch for `p` and the plan's
+ * grid / LDS / chunk / workspace, as text (NUL-terminated, at most cap bytes).
+ * Returns FATTN_OK or the error fattn_ext would return. */
+int fattn_describe(const fattn_params* p, char* out, size_t cap);
 
 /* flash-llama.h:7-32 argument list (K and V share nb11..nb13, flash-llama.h:123-125;
  * mask rows padded to ne31, nb31 bytes per row). */
@@ -167,6 +180,15 @@ int fattn_row(const float* query, const void* key, const void* value, const void
  * quantize:   f32 -> Q8_0/Q4_0 (bit-exact with ggml quantize_row_*_ref). */
 int fattn_dequantize(int type, const void* src, float* dst, int64_t k, int64_t n_rows, void* stream);
 int fattn_quantize(int type, const float* src, void* dst, int64_t k, int64_t n_rows, void* stream);
+
+/* GGML_OP_CPY f32 -> F16 / Q8_0 / Q4_0 into a strided view: the KV-cache write
+ * (quantize-on-write; upstream ggml cpy_f32_q /
+ * cpy_f32_f16, absent from the reference).  src: f32, nb[0] = 4; dst: same ne,
+ * nb[0] = element / block bytes, any nb[1..3] -- e.g. one token's Hkv rows
+ * written into a [Hkv][N][row] cache (nb1 = N * row bytes) or a [N][Hkv][row]
+ * cache (nb1 = row bytes).  ne[0] a multiple of 32 for Q8_0 / Q4_0.  Values
+ * bit-exact with ggml quantize_row_*_ref / f16 round-to-nearest-even. */
+int fattn_cpy(const fattn_tensor* src, const fattn_tensor* dst, void* stream);
 
 const char* fattn_strerror(int status);
 /* bytes of one row of k elements (0 if unsupported) */

@@ -100,3 +100,21 @@ def test_rejects_null():
 def test_row_workspace_size():
     assert fattn.lib().fattn_row_workspace_size(128, 4096, 32) > 0
     assert fattn.lib().fattn_row_workspace_size(96, 4096, 32) == 0
+
+
+def test_cpy_rejects_bad_views():
+    """fattn_cpy validates before launching anything (no GPU needed)."""
+    f32 = fattn.View(16, fattn.TYPE_F32, (128, 8, 1, 1), (4, 512, 4096, 4096))
+    q8 = fattn.View(16, fattn.TYPE_Q8_0, (128, 8, 1, 1), (34, 136, 1088, 1088))
+    L = fattn.lib()
+
+    def rc(s, d):
+        a, b = s.c(), d.c()
+        return L.fattn_cpy(C.byref(a), C.byref(b), None)
+
+    assert rc(q8, q8) == -2                                                            # src must be f32
+    assert rc(f32, fattn.View(16, fattn.TYPE_Q8_0, (96, 8, 1, 1), (34, 136, 1088, 1088))) == -1  # ne differ
+    assert rc(fattn.View(16, 0, (100, 8, 1, 1), (4, 400, 3200, 3200)),
+              fattn.View(16, fattn.TYPE_Q8_0, (100, 8, 1, 1), (34, 136, 1088, 1088))) == -1  # not whole blocks
+    assert rc(f32, fattn.View(16, fattn.TYPE_Q8_0, (128, 8, 1, 1), (18, 136, 1088, 1088))) == -4  # wrong nb0
+    assert rc(fattn.View(18, fattn.TYPE_F32, (128, 8, 1, 1), (4, 512, 4096, 4096)), q8) == -7      # misaligned

@@ -1,0 +1,305 @@
+"""GPU parity, round 2: the reference's own fixtures and call sites through the
+HIP path, the head-sharded multi-GPU slices on one GPU, one workspace shared
+by a prefill and a decode, fattn_row at the reference's default GQA shape,
+and the loader-wave decode kernel (fattn_dec.h) on the BASELINE configs.
+
+Bar as in test_gpu_parity.py: attention within 1e-3 normwise relative error
+per output row against the oracle -- here mostly against outputs the
+REFERENCE's src/utils.h produced (tests/golden/, oracle/gen_golden.py).
+"""
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import fattn
+from fattn.shard import assemble_heads, head_views, shard_heads
+from gpu_util import run_gpu, upload, views
+from oracle import oracle as orc
+from problems import attn_rel_err, make_problem
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-3
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _kernel_test_inputs(D, H, Hkv, N):
+    """kernel_test.h:45-48: glibc rand() from seed 1, fill order Q, K, V, mask."""
+    orc.srand(1)
+    return orc.random(D * H), orc.random(D * N * Hkv), orc.random(D * N * Hkv), orc.random(N)
+
+
+def _t(a, dev):
+    import torch
+    return torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else np.ascontiguousarray(a)).to(dev)
+
+
+# ------------------------------------------------------------------ reference fixtures through the HIP path
+
+def test_golden_kernel_test_default_row(dev):
+    """tests/golden/kernel_test_default.npz (the reference's CPU output for
+    kernel_test.h's defaults: 32 q / 8 kv heads, D=128, kv_size=512) against
+    fattn_row -- the flash_attn_row + fa_reduce call of kernel_test.h:161-162
+    (V transposed, -DFA_KV_BLOCK_256, kernel_test.h:96-105)."""
+    import torch
+    z = np.load(os.path.join(GOLDEN, "kernel_test_default.npz"))
+    D, H, Hkv, N = (int(x) for x in z["meta"])
+    q, k, v, m = _kernel_test_inputs(D, H, Hkv, N)
+    assert np.array_equal(q[:16], z["q_head"]) and np.array_equal(m[:16], z["m_head"])
+    vt = orc.f32_to_f16_bits(np.ascontiguousarray(v.reshape(Hkv, N, D).transpose(0, 2, 1)))
+    qkv = torch.empty(H * D, dtype=torch.float32, device=dev)
+    fattn.row(_t(q, dev), _t(orc.f32_to_f16_bits(k), dev), _t(vt, dev), _t(orc.f32_to_f16_bits(m), dev), qkv, D, N,
+              H, 1.0 / np.sqrt(np.float32(D)), D * N, H // Hkv)
+    torch.cuda.synchronize()
+    assert attn_rel_err(qkv.cpu().numpy().reshape(H, D), z["out"].reshape(H, D)) <= RTOL
+
+
+def _reference_ext_call(dev, q, k16, v16, m, D, H, Hkv, N, k_type=fattn.TYPE_F16):
+    """kernel_test.h:191-198 byte for byte: the flash_attn_ext_f16 argument list
+    with the 32-row padded mask (row 0 = the mask, rows 1..31 zeros,
+    kernel_test.h:74-85), ne31 = 32, nb31 = kv_size*2, nb01 = nb02 =
+    head_dim*4, V not transposed."""
+    import torch
+    padded = np.zeros((32, N), dtype=np.uint16)
+    padded[0] = orc.f32_to_f16_bits(m)
+    dq, dk, dv, dm = _t(q, dev), _t(k16, dev), _t(v16, dev), _t(padded, dev)
+    dst = torch.full((H * D,), float("nan"), dtype=torch.float32, device=dev)
+    ws = torch.zeros(1 << 22, dtype=torch.uint8, device=dev)
+    rb = fattn.row_size(k_type, D)
+    rc = fattn.lib().fattn_ext_f16_launch(
+        dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dm.data_ptr(), dst.data_ptr(), 1.0 / np.sqrt(np.float32(D)),
+        D, 1, H, 1,
+        D, N, Hkv, 1,
+        32, N * 2,
+        D * 4, D * 4, D * H * 4,
+        rb, rb * N, rb * N * Hkv,
+        D, H, 1, 1,
+        k_type, k_type, ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, fattn.strerror(rc)
+    torch.cuda.synchronize()
+    return dst.cpu().numpy().reshape(H, D)
+
+
+def test_golden_kernel_test_default_ext_call(dev):
+    """The same fixture through kernel_test.h's --no-kv-parallel branch, called
+    exactly as kernel_test.h:191-198 calls flash_attn_ext_f16."""
+    z = np.load(os.path.join(GOLDEN, "kernel_test_default.npz"))
+    D, H, Hkv, N = (int(x) for x in z["meta"])
+    q, k, v, m = _kernel_test_inputs(D, H, Hkv, N)
+    got = _reference_ext_call(dev, q, orc.f32_to_f16_bits(k), orc.f32_to_f16_bits(v), m, D, H, Hkv, N)
+    assert attn_rel_err(got, z["out"].reshape(H, D)) <= RTOL
+
+
+def test_golden_kernel_test_q8_0_ext_call(dev):
+    """tests/golden/kernel_test_q8_0.npz: the reference's attention arithmetic on
+    Q8_0-rounded K/V (H=4, D=128, N=256), against the HIP kernel reading the
+    Q8_0 blocks, through the kernel_test.h:191-198 argument list."""
+    z = np.load(os.path.join(GOLDEN, "kernel_test_q8_0.npz"))
+    D, H, Hkv, N = (int(x) for x in z["meta"])
+    q, k, v, m = _kernel_test_inputs(D, H, Hkv, N)
+    kq = orc.quantize(k.reshape(-1, D), orc.TYPE_Q8_0).reshape(-1)
+    vq = orc.quantize(v.reshape(-1, D), orc.TYPE_Q8_0).reshape(-1)
+    got = _reference_ext_call(dev, q, kq, vq, m, D, H, Hkv, N, fattn.TYPE_Q8_0)
+    assert attn_rel_err(got, z["out"].reshape(H, D)) <= RTOL
+
+
+def test_golden_cfg1_row(dev):
+    """BASELINE config 1's fixture (H=1, D=64, N=128; full inputs and the
+    reference's output) through fattn_row on the GPU."""
+    import torch
+    z = np.load(os.path.join(GOLDEN, "kernel_test_cfg1.npz"))
+    D, H, Hkv, N = (int(x) for x in z["meta"])
+    vt = orc.f32_to_f16_bits(np.ascontiguousarray(z["value"].reshape(Hkv, N, D).transpose(0, 2, 1)))
+    qkv = torch.empty(H * D, dtype=torch.float32, device=dev)
+    fattn.row(_t(z["query"], dev), _t(orc.f32_to_f16_bits(z["key"]), dev), _t(vt, dev),
+              _t(orc.f32_to_f16_bits(z["mask"]), dev), qkv, D, N, H, 1.0 / np.sqrt(np.float32(D)), D * N, 1)
+    torch.cuda.synchronize()
+    assert attn_rel_err(qkv.cpu().numpy().reshape(H, D), z["out"].reshape(H, D)) <= RTOL
+
+
+# ------------------------------------------------------------------ call-site details
+
+def test_row_gqa_full_size(dev):
+    """fattn_row at N=4096 with the reference's default GQA 32/8
+    (r_kv_heads = 4): fattn_row_workspace_size must cover the r = 4 plan."""
+    import torch
+    D, H, Hkv, N = 128, 32, 8, 4096
+    rng = np.random.default_rng(7)
+    q = (1 - 2 * rng.random(H * D, dtype=np.float32))
+    k = (1 - 2 * rng.random(Hkv * N * D, dtype=np.float32))
+    v = (1 - 2 * rng.random(Hkv * N * D, dtype=np.float32))
+    m = (1 - 2 * rng.random(N, dtype=np.float32))
+    ref = orc.kernel_test_cpu(q, k, v, m, N, D, H, Hkv, n_threads=8)
+    vt = orc.f32_to_f16_bits(np.ascontiguousarray(v.reshape(Hkv, N, D).transpose(0, 2, 1)))
+    qkv = torch.empty(H * D, dtype=torch.float32, device=dev)
+    fattn.row(_t(q, dev), _t(orc.f32_to_f16_bits(k), dev), _t(vt, dev), _t(orc.f32_to_f16_bits(m), dev), qkv, D, N,
+              H, 1.0 / np.sqrt(np.float32(D)), D * N, H // Hkv)
+    torch.cuda.synchronize()
+    assert attn_rel_err(qkv.cpu().numpy().reshape(H, D), ref.reshape(H, D)) <= RTOL
+
+
+def test_positional_launch_odd_kv(dev):
+    """flash-llama.h:7-32 argument list with an odd ne11: the mask row length
+    comes from nb31 (ggml pads mask rows, GGML_KQ_MASK_PAD), not from ne11."""
+    import torch
+    D, H, Hkv, N = 128, 8, 8, 333
+    p = make_problem(D=D, NQ=1, H=H, Hkv=Hkv, N=N, kv_type="f16", mask="random", seed=17, mask_pad=64)
+    t = upload(p, dev)
+    npad = p.mask_bits.shape[1]
+    ws = torch.zeros(1 << 22, dtype=torch.uint8, device=dev)
+    rc = fattn.lib().fattn_ext_f16_launch(
+        t["q"].data_ptr(), t["k"].data_ptr(), t["v"].data_ptr(), t["mask"].data_ptr(), t["dst"].data_ptr(),
+        p.scale, D, 1, H, 1, D, N, Hkv, 1, p.mask_bits.shape[0], npad * 2, D * 4 * H, D * 4, D * H * 4,
+        D * 2, D * N * 2, D * N * Hkv * 2, D, H, 1, 1, fattn.TYPE_F16, fattn.TYPE_F16, ws.data_ptr(), ws.numel(),
+        torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, fattn.strerror(rc)
+    torch.cuda.synchronize()
+    assert attn_rel_err(t["dst"].cpu().numpy(), p.oracle()) <= RTOL
+
+
+def test_workspace_prefill_then_decode(dev):
+    """One workspace for a masked (causal) prefill and then a multi-chunk
+    decode, as llama.cpp reuses it: the prefill's live-block flags share the
+    front of the workspace with the decode's arrival counters, and every
+    launch must leave it re-armed (include/fattn.h)."""
+    import torch
+    pre = make_problem(D=128, NQ=512, H=8, Hkv=2, N=512, kv_type="q8_0", mask="causal", seed=61)
+    dec = make_problem(D=128, NQ=1, H=32, Hkv=8, N=4096, kv_type="q8_0", mask="random", seed=62)
+    tp, td = upload(pre, dev), upload(dec, dev)
+    fattn.set_option(fattn.OPT_PF, 2)  # the prefill kernel on this small prefill too
+    try:
+        ap = fattn.Attention(*views(pre, tp), tp["dst"], pre.scale)
+        ad = fattn.Attention(*views(dec, td), td["dst"], dec.scale)
+        assert "pf_mask_flags_kernel" in ap.describe(), ap.describe()
+        assert int(ad.describe().split("grid(")[1].split(",")[0]) > 1, ad.describe()  # several chunks
+        need = max(fattn.workspace_size(ap.p), fattn.workspace_size(ad.p))
+        ws = torch.zeros(need, dtype=torch.uint8, device=dev)
+        for a in (ap, ad):
+            a.p.workspace, a.p.workspace_bytes = ws.data_ptr(), ws.numel()
+        ref_dec = dec.oracle()
+        for _ in range(3):
+            ap()
+            ad()
+            torch.cuda.synchronize()
+            assert attn_rel_err(td["dst"].cpu().numpy(), ref_dec) <= RTOL
+        assert attn_rel_err(tp["dst"].cpu().numpy(), pre.oracle()) <= RTOL
+    finally:
+        fattn.set_option(fattn.OPT_PF, 0)
+
+
+# ------------------------------------------------------------------ multi-GPU head shard, one GPU
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_config5_head_shard_slices(dev, world):
+    """BASELINE config 5 (n_q = 64, 32 heads, N = 4096, Q8_0) cut into the
+    per-rank slices bench.py --gpus N runs (fattn.shard.shard_heads +
+    head_views: zero-copy q / k / v views, the GQA map kept inside a slice),
+    each slice run through the HIP kernel on this GPU, the slices assembled
+    into the ggml dst layout exactly as gather_heads does after the RCCL
+    all_gather -- against the oracle of the whole problem."""
+    import torch
+    p = make_problem(D=128, NQ=64, H=32, N=4096, kv_type="q8_0", seed=55)
+    t = upload(p, dev)
+    qv, kv, vv, mv = views(p, t)
+    parts = []
+    for rank in range(world):
+        sh = shard_heads(p.H, p.Hkv, world, rank)
+        qs, ks, vs = head_views(qv, kv, vv, sh)
+        dst = torch.full((1, p.NQ, sh.n_heads, p.D), float("nan"), dtype=torch.float32, device=dev)
+        fattn.Attention(qs, ks, vs, mv, dst, p.scale)()
+        parts.append(dst)
+    torch.cuda.synchronize()
+    full = assemble_heads(torch.stack(parts)).cpu().numpy()
+    assert attn_rel_err(full, p.oracle()) <= RTOL
+
+
+def test_config4_gqa_head_shard_slices(dev):
+    """Config 4 (Q4_0, GQA 32/8) on 8 ranks: one kv head and its 4 q heads each."""
+    import torch
+    p = make_problem(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0", seed=56)
+    t = upload(p, dev)
+    qv, kv, vv, mv = views(p, t)
+    parts = []
+    for rank in range(8):
+        sh = shard_heads(p.H, p.Hkv, 8, rank)
+        assert (sh.n_kv, sh.n_heads) == (1, 4)
+        qs, ks, vs = head_views(qv, kv, vv, sh)
+        dst = torch.empty((1, 1, sh.n_heads, p.D), dtype=torch.float32, device=dev)
+        fattn.Attention(qs, ks, vs, mv, dst, p.scale)()
+        parts.append(dst)
+    torch.cuda.synchronize()
+    assert attn_rel_err(assemble_heads(torch.stack(parts)).cpu().numpy(), p.oracle()) <= RTOL
+
+
+# ------------------------------------------------------------------ loader-wave decode kernel (fattn_dec.h)
+
+@pytest.fixture(params=[4, 8], ids=["4compute", "8compute"])
+def dec_on(request):
+    fattn.set_option(fattn.OPT_DEC, 2)
+    fattn.set_option(fattn.OPT_DEC_COMPUTE, request.param)
+    yield
+    fattn.set_option(fattn.OPT_DEC, 1)
+    fattn.set_option(fattn.OPT_DEC_COMPUTE, 4)
+
+
+DEC_CASES = [
+    dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0"),                 # config 3
+    dict(D=128, NQ=1, H=32, N=2048, kv_type="f16"),                  # config 2
+    dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0"),          # config 4
+    dict(D=128, NQ=1, H=8, N=32768, kv_type="q8_0"),                 # long KV: the LDS ring wraps
+    dict(D=64, NQ=3, H=8, Hkv=2, N=1024, kv_type="q4_0", mask="causal"),
+    dict(D=256, NQ=1, H=4, N=1024, kv_type="q8_0"),
+    dict(D=128, NQ=1, H=4, N=512, kv_type="f16", v_trans=True),
+    dict(D=128, NQ=2, H=4, N=96, kv_type="q8_0", mask="neginf_blocks", S=2),
+]
+
+
+@pytest.mark.parametrize("case", DEC_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_dec_kernel(dev, dec_on, case):
+    p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    t = upload(p, dev)
+    att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+    assert "fattn_dec_kernel" in att.describe() or p.N * p.S < 128, att.describe()
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+# ------------------------------------------------------------------ quantize-on-write (fattn_cpy)
+
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0", "f16"])
+@pytest.mark.parametrize("layout", ["head", "pos"])
+@pytest.mark.parametrize("ntok", [1, 5])
+def test_cpy_into_kv_cache_view(dev, kt, layout, ntok):
+    """GGML_OP_CPY f32 -> cache type into the cache view of `ntok` new tokens at
+    position p: every written row bit-exact with the oracle's ggml
+    quantisation (or f16 RNE), every other byte of the cache untouched."""
+    import torch
+    from problems import TYPES, encode_rows
+    typ = TYPES[kt]
+    D, Hkv, N, p0 = 128, 8, 64, 37
+    rb = fattn.row_size(typ, D)
+    eb = 2 if typ == fattn.TYPE_F16 else fattn.BLOCK_BYTES[typ]
+    rng = np.random.default_rng(ntok * 10 + len(layout))
+    cache0 = rng.integers(0, 256, size=Hkv * N * rb, dtype=np.uint8)
+    cur = (1 - 2 * rng.random((ntok, Hkv, D), dtype=np.float32)) * 3  # K_cur [tok][Hkv][D]
+    cur[0, 1, :32] = 0.0                                                # an all-zero block (d = 0)
+    cache = torch.from_numpy(cache0.copy()).to(dev)
+    src = torch.from_numpy(cur).to(dev)
+    sv = fattn.View(src.data_ptr(), fattn.TYPE_F32, (D, Hkv, ntok, 1), (4, D * 4, Hkv * D * 4, ntok * Hkv * D * 4))
+    if layout == "head":  # [Hkv][N][row]: a token's rows are N rows apart
+        dv = fattn.View(cache.data_ptr() + p0 * rb, typ, (D, Hkv, ntok, 1), (eb, N * rb, rb, N * Hkv * rb))
+    else:                 # [N][Hkv][row]: llama.cpp's cache, a token's rows contiguous
+        dv = fattn.View(cache.data_ptr() + p0 * Hkv * rb, typ, (D, Hkv, ntok, 1), (eb, rb, Hkv * rb, N * Hkv * rb))
+    fattn.cpy(sv, dv)
+    torch.cuda.synchronize()
+    got = cache.cpu().numpy()
+    want = cache0.copy()
+    rows = encode_rows(cur, typ)  # [tok][Hkv][rb]
+    w = want.reshape(Hkv, N, rb) if layout == "head" else want.reshape(N, Hkv, rb)
+    for t in range(ntok):
+        for h in range(Hkv):
+            if layout == "head":
+                w[h, p0 + t] = rows[t, h]
+            else:
+                w[p0 + t, h] = rows[t, h]
+    assert np.array_equal(got, want)

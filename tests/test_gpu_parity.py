@@ -237,22 +237,12 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture(params=[8, 4, "pre", "pipe"], ids=["8waves", "4waves", "predequant", "pipelined"])
-def pf_force(request):
-    """Prefill kernel on every eligible problem, in all its forms: 8 waves x 32
-    rows (fattn_pf.h), 4 waves x 64 rows (fattn_pf4.h), quantised K/V converted
-    to f16 rows first (pf_dequant_rows_kernel + the f16 form), and the f16
-    images through the software-pipelined kernel (fattn_pfp.h)."""
-    prm = request.param
+@pytest.fixture
+def pf_force():
+    """The prefill kernel (fattn_pf.h, 8 waves x 32 rows) on every eligible problem."""
     fattn.set_option(fattn.OPT_PF, 2)
-    fattn.set_option(fattn.OPT_PF_WAVES, prm if isinstance(prm, int) else 8)
-    fattn.set_option(fattn.OPT_PF_DEQUANT, 1 if isinstance(prm, int) else 2)
-    fattn.set_option(fattn.OPT_PF_PIPE, 2 if prm == "pipe" else 1)
     yield
     fattn.set_option(fattn.OPT_PF, 0)
-    fattn.set_option(fattn.OPT_PF_WAVES, 8)
-    fattn.set_option(fattn.OPT_PF_DEQUANT, 0)
-    fattn.set_option(fattn.OPT_PF_PIPE, 0)
 
 
 PF_CASES = [
@@ -278,23 +268,6 @@ def test_pf_sweep(dev, pf_force, case):
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
-@pytest.mark.parametrize("case", [c for c in PF_CASES if c["kv_type"] == "f16"][:2] + PF_CASES[:2],
-                         ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
-def test_pf_images_pipelined(dev, case):
-    """f16 images through the software-pipelined kernel (OPT_PF_PIPE = 2):
-    f16 K/V directly, quantised K/V after the pre-pass."""
-    fattn.set_option(fattn.OPT_PF, 2)
-    fattn.set_option(fattn.OPT_PF_PIPE, 2)
-    fattn.set_option(fattn.OPT_PF_DEQUANT, 2)
-    try:
-        p = make_problem(D=128, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
-        assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
-    finally:
-        fattn.set_option(fattn.OPT_PF, 0)
-        fattn.set_option(fattn.OPT_PF_PIPE, 0)
-        fattn.set_option(fattn.OPT_PF_DEQUANT, 0)
-
-
 @pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
 def test_pf_rescale(dev, pf_force, kt):
     """Large scores and scores rising along the sequence: deferred-max rescales."""
@@ -312,24 +285,6 @@ def test_pf_fully_masked_rows_are_nan(dev, pf_force):
     got, ref = run_gpu(p), p.oracle()
     assert np.isnan(ref[:, 7]).all() and np.isnan(got[:, 7]).all()
     assert attn_rel_err(got, ref) <= RTOL
-
-
-@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
-def test_pf_predequant_bitexact(dev, kt):
-    """Quantised prefill through the f16 pre-pass gives bit-identical output to
-    the in-kernel dequantisation (same f16 operands h(q*d), same kernel math)."""
-    p = make_problem(D=128, NQ=512, H=4, Hkv=2, N=1024, kv_type=kt, mask="random", seed=31)
-    fattn.set_option(fattn.OPT_PF, 2)
-    try:
-        fattn.set_option(fattn.OPT_PF_DEQUANT, 1)
-        a = run_gpu(p)
-        fattn.set_option(fattn.OPT_PF_DEQUANT, 2)
-        b = run_gpu(p)
-    finally:
-        fattn.set_option(fattn.OPT_PF, 0)
-        fattn.set_option(fattn.OPT_PF_DEQUANT, 0)
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
-    assert attn_rel_err(a, p.oracle()) <= RTOL
 
 
 @pytest.mark.parametrize("skip", [0, 1], ids=["range", "noprepass"])
@@ -375,22 +330,13 @@ def test_pf_f16_prefill_full(dev):
     assert attn_rel_err(a, b) <= RTOL
 
 
-@pytest.mark.parametrize("waves", [8, 4, "pre", "pipe"])
-def test_pf_prefill_full_matches_mq(dev, waves):
+def test_pf_prefill_full_matches_mq(dev):
     """The prefill shape at full size (n_q = N = 4096, 32 heads, Q8_0, random mask):
-    the prefill kernel (auto-selected) against the multi-query kernel, and one
-    head of it against the oracle."""
-    import torch
+    the prefill kernel (auto-selected) against the multi-query kernel, and two
+    heads x three query-row blocks (start, middle, end of the sequence)
+    against the oracle."""
     p = make_problem(D=128, NQ=4096, H=32, N=4096, kv_type="q8_0", seed=29)
-    fattn.set_option(fattn.OPT_PF_WAVES, waves if isinstance(waves, int) else 8)
-    fattn.set_option(fattn.OPT_PF_DEQUANT, 1 if isinstance(waves, int) else 2)
-    fattn.set_option(fattn.OPT_PF_PIPE, 2 if waves == "pipe" else 1)
-    try:
-        a = run_gpu(p)
-    finally:
-        fattn.set_option(fattn.OPT_PF_WAVES, 8)
-        fattn.set_option(fattn.OPT_PF_DEQUANT, 0)
-        fattn.set_option(fattn.OPT_PF_PIPE, 0)
+    a = run_gpu(p)
     fattn.set_option(fattn.OPT_PF, 1)
     try:
         b = run_gpu(p)
@@ -398,15 +344,14 @@ def test_pf_prefill_full_matches_mq(dev, waves):
         fattn.set_option(fattn.OPT_PF, 0)
     assert np.isfinite(a).all()
     assert attn_rel_err(a, b) <= RTOL
-    # head 5, query rows 0..255: oracle on the sliced problem
-    sub = make_problem(D=128, NQ=256, H=1, N=4096, kv_type="q8_0", seed=29)
-    sub.q = np.ascontiguousarray(p.q[:, :256, 5:6, :])
-    kb = p.k_bytes.reshape(p.Hkv, -1)[5:6].reshape(-1)
-    vb = p.v_bytes.reshape(p.Hkv, -1)[5:6].reshape(-1)
-    sub.k_bytes, sub.v_bytes = np.ascontiguousarray(kb), np.ascontiguousarray(vb)
-    sub.mask_bits = np.ascontiguousarray(p.mask_bits[:256])
-    ref = sub.oracle()
-    assert attn_rel_err(a[:, :256, 5:6, :], ref) <= RTOL
+    rows = np.r_[0:128, 2048:2176, 3968:4096]
+    for h in (5, 30):
+        sub = make_problem(D=128, NQ=len(rows), H=1, N=4096, kv_type="q8_0", seed=29)
+        sub.q = np.ascontiguousarray(p.q[:, rows, h:h + 1, :])
+        sub.k_bytes = np.ascontiguousarray(p.k_bytes.reshape(p.Hkv, -1)[h:h + 1].reshape(-1))
+        sub.v_bytes = np.ascontiguousarray(p.v_bytes.reshape(p.Hkv, -1)[h:h + 1].reshape(-1))
+        sub.mask_bits = np.ascontiguousarray(p.mask_bits[rows])
+        assert attn_rel_err(a[:, rows, h:h + 1, :], sub.oracle()) <= RTOL
 
 
 # ------------------------------------------------------------------ sweep

@@ -1,0 +1,56 @@
+"""The kernel_test harness (ggml-cuda-experiments_amd/host/kernel_test.cpp, the
+counterpart of src/kernel_test.h:1-249).
+
+CPU: its host-only mode (BASELINE config 1, `--cpu-only`) must reproduce the
+REFERENCE's own CPU output bit for bit -- tests/golden/ holds what
+src/utils.h (compiled from /root/reference, oracle/gen_golden.py) printed for
+the same srand(1) inputs -- which pins the harness's CPU reference
+(kernel_test.cpp cpu_reference) to the reference.
+GPU: both of its branches run and pass their own max-diff check.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "ggml-cuda-experiments_amd", "bin", "kernel_test")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def _need_bin():
+    if not os.path.exists(BIN):
+        pytest.fail(f"{BIN} not built (make harness)")
+
+
+@pytest.mark.parametrize("fixture,args", [
+    ("kernel_test_cfg1.npz", ["--heads", "1", "--kv-heads", "1", "--head-dim", "64", "--kv-size", "128"]),
+    ("kernel_test_default.npz", []),
+])
+def test_cpu_only_matches_reference_bitexact(tmp_path, fixture, args):
+    _need_bin()
+    out = tmp_path / "out.bin"
+    r = subprocess.run([BIN, "--cpu-only", "--dump", str(out)] + args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(out, dtype=np.float32)
+    ref = np.load(os.path.join(GOLDEN, fixture))["out"]
+    assert got.shape == ref.shape
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert "Reference" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    [],                                                    # flash_attn_row + fa_reduce, f16, V transposed
+    ["--no-kv-parallel"],                                  # flash_attn_ext call of kernel_test.h:191-198
+    ["--no-kv-parallel", "--kv-type", "q8_0"],
+    ["--no-kv-parallel", "--kv-type", "q4_0"],
+    ["--kv-size", "4096"],
+    ["--no-kv-parallel", "--kv-type", "q8_0", "--kv-size", "4096", "--kv-heads", "32"],
+], ids=lambda a: "_".join(a) or "default")
+def test_harness_runs_on_gpu(dev, args):
+    _need_bin()
+    r = subprocess.run([BIN, "--iters", "3"] + args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS" in r.stdout

@@ -18,7 +18,7 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "ggml-cuda-experiments_amd"), ROOT]
 
-from fattn.shard import gather_heads, shard_heads  # noqa: E402
+from fattn.shard import assemble_heads, gather_heads, head_views, shard_heads  # noqa: E402
 from tests.problems import make_problem  # noqa: E402
 
 
@@ -42,17 +42,34 @@ def test_shard_heads_rejects(bad):
         shard_heads(H, Hkv, W, 0)
 
 
+def _materialize(base: np.ndarray, view, row_bytes: int) -> np.ndarray:
+    """Bytes of a (possibly narrowed) ggml view whose ptr is a byte offset into
+    `base`: [ne3][ne2][ne1][row_bytes], made contiguous."""
+    ne, nb = view.ne, view.nb
+    arr = np.lib.stride_tricks.as_strided(base[view.ptr:], shape=(ne[3], ne[2], ne[1], row_bytes),
+                                          strides=(nb[3], nb[2], nb[1], 1), writeable=False)
+    return np.ascontiguousarray(arr)
+
+
 def _slice_problem(prob, sh):
-    """The rank's sub-problem: q-heads [h0,h1) and kv-heads [kv0,kv1), head layout."""
+    """The rank's sub-problem through the product's own slicing code
+    (fattn.shard.head_views, as bench.py's sharded mode uses it) applied to
+    byte-offset views of the full problem."""
+    from fattn import View
     from tests.problems import Problem
+    qv = View(0, 0, prob.q_ne, prob.q_nb)
+    kv = View(0, prob.kv_type, prob.kv_ne, prob.k_nb)
+    vv = View(0, prob.kv_type, prob.kv_ne, prob.v_nb)
+    qs, ks, vs = head_views(qv, kv, vv, sh)
     rb = prob.k_nb[1]
-    kb = prob.k_bytes.reshape(prob.Skv, prob.Hkv, prob.N, rb)[:, sh.kv0:sh.kv1]
-    vb = prob.v_bytes.reshape(prob.Skv, prob.Hkv, prob.N, rb)[:, sh.kv0:sh.kv1]
+    qb = _materialize(np.ascontiguousarray(prob.q).view(np.uint8).reshape(-1), qs, prob.D * 4)
+    q = qb.view(np.float32).reshape(prob.S, sh.n_heads, prob.NQ, prob.D).transpose(0, 2, 1, 3)
+    kb = _materialize(prob.k_bytes, ks, rb)  # [Skv][n_kv][N][rb]
+    vb = _materialize(prob.v_bytes, vs, rb)
     nkv = sh.n_kv
     nb = (prob.k_nb[0], rb, rb * prob.N, rb * prob.N * nkv)
     return Problem(prob.D, prob.NQ, sh.n_heads, nkv, prob.N, prob.S, prob.Skv, prob.kv_type, "head", prob.scale,
-                   np.ascontiguousarray(prob.q[:, :, sh.h0:sh.h1]), np.ascontiguousarray(kb).reshape(-1),
-                   np.ascontiguousarray(vb).reshape(-1), nb, nb, prob.mask_bits)
+                   np.ascontiguousarray(q), kb.reshape(-1), vb.reshape(-1), nb, nb, prob.mask_bits)
 
 
 def _worker(rank, world, port, kv_type, q):
@@ -94,3 +111,30 @@ def test_two_rank_gather_equals_single_process(kv_type):
     ref = prob.oracle(n_threads=2)
     assert got.shape == ref.shape
     assert np.array_equal(got, ref)
+
+
+def test_assemble_heads_matches_layout():
+    """assemble_heads puts rank w's heads at [w*Hl, (w+1)*Hl) of the ggml dst
+    [S][n_q][H][D] (src/flash-llama.h:434), for numpy and torch, with and
+    without a leading (rotation) axis."""
+    W, S, NQ, Hl, D = 4, 2, 3, 2, 5
+    full = np.arange(S * NQ * W * Hl * D, dtype=np.float32).reshape(S, NQ, W * Hl, D)
+    parts = np.stack([full[:, :, w * Hl:(w + 1) * Hl] for w in range(W)])
+    assert np.array_equal(assemble_heads(parts), full)
+    assert np.array_equal(assemble_heads(torch.from_numpy(parts)).numpy(), full)
+    lead = np.stack([parts, parts + 1], axis=1)  # [W][R][S][NQ][Hl][D]
+    got = assemble_heads(lead)
+    assert np.array_equal(got[0], full) and np.array_equal(got[1], full + 1)
+
+
+def test_slice_problem_oracle_matches_full_heads():
+    """Single process: every rank's slice (head_views) solved by the oracle
+    equals the full problem's heads -- the same check the GPU slice test makes
+    with the HIP kernel (tests/test_gpu_parity.py::test_config5_head_shard_slices)."""
+    prob = make_problem(D=64, NQ=2, H=8, Hkv=2, N=64, kv_type="q8_0", S=1, layout="head", seed=5)
+    ref = prob.oracle(n_threads=2)
+    parts = []
+    for r in range(2):
+        sh = shard_heads(prob.H, prob.Hkv, 2, r)
+        parts.append(_slice_problem(prob, sh).oracle(n_threads=2))
+    assert np.array_equal(assemble_heads(np.stack(parts)), ref)

@@ -1,7 +1,8 @@
 #!/bin/bash
-# full round: GPU parity suite, default bench (decode + prefill + cpu baseline), rocprof kernel trace
+# round-2 check: whole GPU suite, harness, the sharded bench path rehearsed on one GPU
 source tools/gpu_round.sh
 export TMPDIR=/tmp
-run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
-run bench 300 python bench.py
-run prof_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline
+run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 180 --timeout-method thread
+run rehearse2 300 env FATTN_BENCH_REHEARSE=1 python bench.py --gpus 2 --steps 50 --warmup 5
+cat gpurun_out/rehearse2.log | grep '^{' || true
+run bench1 300 python bench.py --no-prefill --cpu-seconds 4
