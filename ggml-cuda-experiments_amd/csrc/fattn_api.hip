@@ -238,8 +238,10 @@ int size_dec(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t NQ
     }
     const int nlw = 2;  // steps per chunk >= 2 (cs >= min(steps, ncw); one-step chunks: spl 0, rejected below)
     const int step_bytes = G.step_bytes;
-    int nslot = (int)std::min<int64_t>(cs, std::min<int64_t>(kDecMaxSlots, (kLdsPerCU - kDecHdr) / step_bytes));
-    if (nslot < cs) nslot -= nslot % nlw;  // ring: equal rings per loader
+    // equal rings per loader: slot(s) = loader + nlw * ((s / nlw) % (nslot / nlw))
+    const int fit = (int)std::min<int64_t>(kDecMaxSlots, (kLdsPerCU - kDecHdr) / step_bytes);
+    const int whole = (int)((cs + nlw - 1) / nlw * nlw);  // every step its own slot
+    int nslot = whole <= fit ? whole : fit - fit % nlw;
     if (nslot < nlw) return FATTN_ERR_INVALID_ARG;
     a.nbuf = nslot;
     a.split_prio = 0;
@@ -400,6 +402,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
     a.has_mask = has_mask ? 1 : 0;
     a.scale_log2 = p->scale * 1.4426950408889634f;
+    a.scale = p->scale;
 
     // byte spans addressed through the 32-bit buffer descriptors
     const int64_t k_span = (N - 1) * k.nb[1] + (int64_t)rowK;

@@ -39,6 +39,11 @@ constexpr int kStep = 32;   // KV positions per wave step (= one PV k-step)
 constexpr int kRows = 16;   // packed query rows per workgroup (MFMA N)
 constexpr int VT_F16T = 100;  // V f16 stored transposed ([D][N], flash_row_float.h:177)
 constexpr int kCntStride = 64;
+// deferred max (cdna_hip_programming.md T13): the exponentials' reference max
+// moves only when a score exceeds it by more than 2^3 in p, so p <= 8 (and P*d
+// of a V block stays far inside f16 range)
+constexpr float kRescaleLog2 = 3.0f;
+constexpr float kRescaleNat = kRescaleLog2 * 0.6931471805599453f;
 #ifdef FATTN_DMA_NO_NT
 constexpr bool kDecodeNT = false;  // diagnostic build only
 #else
@@ -70,6 +75,7 @@ struct SplitArgs {
     int n_chunks;
     int ncp;            // next power of two >= n_chunks (combine kernel)
     float scale_log2;   // scale * log2(e)
+    float scale;        // the softmax scale (split_step works in natural units)
     int has_mask;
     int nbuf;           // steps in flight per wave (1..4); LDS per wave = wave_bytes
     int wave_bytes;
@@ -344,6 +350,21 @@ __device__ __forceinline__ uint32_t scale_bits(const RowScales<T, D>& s, int b) 
     constexpr int BB = TypeInfo<T>::block_bytes;
     return ((BB * b) & 2) ? (s.w[b] >> 16) : (s.w[b] & 0xffffu);
 }
+// block b's f16 scale in both halves, by one v_perm (b is unrolled)
+template <int T, int D>
+__device__ __forceinline__ uint32_t scale_bcast(const RowScales<T, D>& s, int b) {
+    constexpr int BB = TypeInfo<T>::block_bytes;
+    return perm_b32(s.w[b], s.w[b], ((BB * b) & 2) ? 0x03020302u : 0x01000100u);
+}
+// two 16-bit LDS values -> one dword {lo, hi}: ds_read_u16 + ds_read_u16_d16_hi,
+// no shift / or to pair them
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t lds_u16_pair(const uint8_t* lo, const uint8_t* hi) {
+    u16x2 v;
+    v.x = *(const uint16_t*)lo;
+    v.y = *(const uint16_t*)hi;
+    return __builtin_bit_cast(uint32_t, v);
+}
 // f16 pair {scale of row r0, scale of row r1} for block b
 template <int T, int D>
 __device__ __forceinline__ f16x2 scale_pair(const RowScales<T, D>& s0, const RowScales<T, D>& s1, int b) {
@@ -371,7 +392,7 @@ __device__ __forceinline__ f16x8 k_operand(const uint8_t* kb, int row, int g, in
             case 4: raw = read8_at<4>(kb, base + 2 + 8 * g); break;
             default: raw = read8_at<6>(kb, base + 2 + 8 * g); break;
         }
-        const f16x2 d = bcast_h(dbits);
+        const f16x2 d = as_h2(dbits);
         f16x2 h0, h1, h2, h3;
         i8x4_to_h2x2(raw.x, h0, h1);
         i8x4_to_h2x2(raw.y, h2, h3);
@@ -390,7 +411,7 @@ __device__ __forceinline__ f16x8 k_operand(const uint8_t* kb, int row, int g, in
             default: raw = read8_at<6>(kb, base + 2 + 8 * (g & 1)); break;
         }
         const uint32_t sh = (g >> 1) * 4;
-        const f16x2 d = bcast_h(dbits);
+        const f16x2 d = as_h2(dbits);
         f16x2 h0, h1, h2, h3;
         u4x4_to_h2x2((raw.x >> sh) & 0x0F0F0F0Fu, h0, h1);
         u4x4_to_h2x2((raw.y >> sh) & 0x0F0F0F0Fu, h2, h3);
@@ -619,6 +640,8 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
     if (!active) {  // loader waves (fattn_dec_kernel): no state; they only join the barriers
         if (a.n_chunks > 1 && a.wave_merge && D == 128) return;
     }
+    // split_step keeps the reference max in natural units; the merges work in log2
+    m_run = m_run == kNegInf ? kNegInf : m_run * 1.4426950408889634f;
     const float l_tot = grp4_sum(l_run);
     if constexpr (kVQ) {
         // O^T tiles of block b (columns 32b..32b+31) carry kVOff * sum(P'_b) too
@@ -790,23 +813,27 @@ __device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* bu
             const RowScales<KT, D> ks = row_scales<KT, D>(kb + (16 * t + i16) * C::rowK);
 #pragma unroll
             for (int b = 0; b < NB; b++)
-                st[t] = mfma16(k_operand<KT, D>(kb, 16 * t + i16, g, b, scale_bits(ks, b)), qop[b], st[t]);
+                st[t] = mfma16(k_operand<KT, D>(kb, 16 * t + i16, g, b, scale_bcast(ks, b)), qop[b], st[t]);
         }
     }
 
-    // -- scale + mask (log2 domain); positions past this wave's slice -> -inf
+    // -- u = s * scale + mask in one v_fma_mix per score (the f16 mask converts
+    // inside it); positions past this wave's slice -> -inf
     float sv[8];
 #pragma unroll
     for (int t = 0; t < 2; t++) {
-        float mk[4] = {0.f, 0.f, 0.f, 0.f};
         if constexpr (HM) {
             const uint8_t* mp = mb + (mq < a.QPT ? mq : 0) * (kStep * 2) + (16 * t + 4 * g) * 2;
             const u32x2 mw = *(const u32x2*)mp;
             const f16x2 m01 = as_h2(mw.x), m23 = as_h2(mw.y);
-            mk[0] = (float)m01.x; mk[1] = (float)m01.y; mk[2] = (float)m23.x; mk[3] = (float)m23.y;
-        }
+            sv[4 * t + 0] = __builtin_fmaf(st[t][0], a.scale, (float)m01.x);
+            sv[4 * t + 1] = __builtin_fmaf(st[t][1], a.scale, (float)m01.y);
+            sv[4 * t + 2] = __builtin_fmaf(st[t][2], a.scale, (float)m23.x);
+            sv[4 * t + 3] = __builtin_fmaf(st[t][3], a.scale, (float)m23.y);
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; r++) sv[4 * t + r] = st[t][r] * a.scale_log2 + mk[r] * log2e;
+            for (int r = 0; r < 4; r++) sv[4 * t + r] = st[t][r] * a.scale;
+        }
     }
     if (nvalid < kStep) {  // wave-uniform: only a slice's partial last step
 #pragma unroll
@@ -814,27 +841,31 @@ __device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* bu
             if (16 * (j >> 2) + 4 * g + (j & 3) >= nvalid) sv[j] = kNegInf;
     }
 
-    // -- online softmax for column m (the 4 lanes l, l^16, l^32, l^48 share it)
+    // -- online softmax for column m (the 4 lanes l, l^16, l^32, l^48 share it).
+    // m_run is the reference max the exponentials use (natural units); it
+    // moves only when a score exceeds it by more than kRescaleNat, so p stays
+    // <= 2^kRescaleLog2 and most steps skip the rescale (deferred max).
     float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
                        fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
     tmax = grp4_max(tmax);
-    const float m_new = fmaxf(m_run, tmax);
-    const float m_use = (m_new == kNegInf) ? 0.0f : m_new;
-    // rescale only when a max moved (never at the first step: o, l are still 0)
-    if (!first && __builtin_amdgcn_ballot_w64(m_new != m_run)) {
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
-        l_run *= alpha;
+    if (__builtin_amdgcn_ballot_w64(tmax > m_run + kRescaleNat)) {
+        const float m_new = fmaxf(m_run, tmax);
+        if (!first) {  // o, l are still 0 at a wave's first step
+            const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * log2e);  // m_run = -inf: 0
+            l_run *= alpha;
 #pragma unroll
-        for (int c = 0; c < NC; c++) o[c] *= alpha;
-        if constexpr (kVQ) {
+            for (int c = 0; c < NC; c++) o[c] *= alpha;
+            if constexpr (kVQ) {
 #pragma unroll
-            for (int b = 0; b < NB; b++) corr[b] *= alpha;
+                for (int b = 0; b < NB; b++) corr[b] *= alpha;
+            }
         }
+        m_run = m_new;
     }
-    m_run = m_new;
+    const float m_off = (m_run == kNegInf) ? 0.0f : -m_run * log2e;
     float pv[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) pv[j] = __builtin_amdgcn_exp2f(sv[j] - m_use);
+    for (int j = 0; j < 8; j++) pv[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[j], log2e, m_off));
     l_run += ((pv[0] + pv[1]) + (pv[2] + pv[3])) + ((pv[4] + pv[5]) + (pv[6] + pv[7]));
 
     f16x8 pb;
@@ -853,15 +884,11 @@ __device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* bu
             constexpr int BB = TypeInfo<C::VTT>::block_bytes;
             // block-b scales of this lane's 8 rows (4g..4g+3, 16+4g..16+4g+3):
             // the dword holding each, then f16 pairs {row r, row r+1}
-            uint32_t sw[8];
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                sw[r] = *(const uint32_t*)(vb + (rA + r) * C::rowV + ((BB * b) & ~3));
-                sw[4 + r] = *(const uint32_t*)(vb + (rB + r) * C::rowV + ((BB * b) & ~3));
-            }
-            const uint32_t sel = ((BB * b) & 2) ? 0x07060302u : 0x05040100u;  // b is unrolled
-            const f16x2 d01 = as_h2(perm_b32(sw[1], sw[0], sel)), d23 = as_h2(perm_b32(sw[3], sw[2], sel));
-            const f16x2 d45 = as_h2(perm_b32(sw[5], sw[4], sel)), d67 = as_h2(perm_b32(sw[7], sw[6], sel));
+            const uint8_t* sp = vb + BB * b;
+            const f16x2 d01 = as_h2(lds_u16_pair(sp + (rA + 0) * C::rowV, sp + (rA + 1) * C::rowV));
+            const f16x2 d23 = as_h2(lds_u16_pair(sp + (rA + 2) * C::rowV, sp + (rA + 3) * C::rowV));
+            const f16x2 d45 = as_h2(lds_u16_pair(sp + (rB + 0) * C::rowV, sp + (rB + 1) * C::rowV));
+            const f16x2 d67 = as_h2(lds_u16_pair(sp + (rB + 2) * C::rowV, sp + (rB + 3) * C::rowV));
             // P'_b = P * d_b (element j <-> row of element j of the A operand)
             f16x8 pbd;
             pbd.s01 = pb.s01 * d01;
@@ -876,17 +903,16 @@ __device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* bu
             if constexpr (kVQ8) {
                 // one u16 per row carries columns 2i (-> tile E_b) and 2i+1 (-> tile O_b)
                 const uint8_t* cp = vb + b * BB + 2 + 2 * i16;
-                uint32_t w[8];
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    w[r] = *(const uint16_t*)(cp + (rA + r) * C::rowV);
-                    w[4 + r] = *(const uint16_t*)(cp + (rB + r) * C::rowV);
-                }
+                uint32_t w2[4];  // rows (r, r+1) of this lane's 8: {u16 of row r, u16 of row r+1}
+                w2[0] = lds_u16_pair(cp + (rA + 0) * C::rowV, cp + (rA + 1) * C::rowV);
+                w2[1] = lds_u16_pair(cp + (rA + 2) * C::rowV, cp + (rA + 3) * C::rowV);
+                w2[2] = lds_u16_pair(cp + (rB + 0) * C::rowV, cp + (rB + 1) * C::rowV);
+                w2[3] = lds_u16_pair(cp + (rB + 2) * C::rowV, cp + (rB + 3) * C::rowV);
                 u32x4 ae, ao;  // f16 pairs 1152 + q (exact)
 #pragma unroll
                 for (int pr = 0; pr < 4; pr++) {
                     // bytes [e_r, o_r, e_r+1, o_r+1] -> xor 0x80 -> f16 magic 0x64xx
-                    const uint32_t t2 = (w[2 * pr] | (w[2 * pr + 1] << 16)) ^ 0x80808080u;
+                    const uint32_t t2 = w2[pr] ^ 0x80808080u;
                     ae[pr] = perm_b32(0x64646464u, t2, 0x04020400u);
                     ao[pr] = perm_b32(0x64646464u, t2, 0x04030401u);
                 }
@@ -1021,7 +1047,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
         qop[b] = h;
     }
 
-    float m_run = kNegInf;  // running max (log2 domain) of column m
+    float m_run = kNegInf;  // reference max (natural units) of column m
     float l_run = 0.0f;     // this lane's partial row sum
     f32x4 o[NC];
 #pragma unroll
