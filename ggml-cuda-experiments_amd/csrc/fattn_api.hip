@@ -707,7 +707,7 @@ int fattn_set_option(int option, int value) {
             g_opt_dec_ahead = value;
             return FATTN_OK;
         case FATTN_OPT_DEC_DIAG:
-            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            if (value < 0 || value > 3) return FATTN_ERR_INVALID_ARG;
             g_opt_dec_diag = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:

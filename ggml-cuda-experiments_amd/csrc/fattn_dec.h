@@ -119,7 +119,7 @@ __global__ __launch_bounds__((NCW + NLW) * kWave, 1) void fattn_dec_kernel(const
                 const uint32_t want = (uint32_t)(s - nslot + 1);
                 while (__builtin_amdgcn_readfirstlane(freew[slot]) < want) __builtin_amdgcn_s_sleep(1);
             }
-            if (a.dec_diag != 2)
+            if (a.dec_diag < 2)
                 issue_step<KT, VT, D, 16, HM>(a, rs, c_lo + s * kStep, mrow0, slots + slot * C::stepBytes, lane);
         };
         int ni = 0;
@@ -193,7 +193,7 @@ __global__ __launch_bounds__((NCW + NLW) * kWave, 1) void fattn_dec_kernel(const
         if (first) FATTN_STAMP8(3);
         if (s + NCW >= ns) FATTN_STAMP8(5);
         const int n0 = c_lo + s * kStep;
-        if (a.dec_diag != 1) {
+        if (a.dec_diag != 1 && a.dec_diag != 3) {
             split_step<KT, VT, D, HM>(a, slots + slot * C::stepBytes, qop, mq, g, i16, min(kStep, c_hi - n0), first,
                                       m_run, l_run, o, corr, [] {});
             first = false;

@@ -356,15 +356,6 @@ __device__ __forceinline__ uint32_t scale_bcast(const RowScales<T, D>& s, int b)
     constexpr int BB = TypeInfo<T>::block_bytes;
     return perm_b32(s.w[b], s.w[b], ((BB * b) & 2) ? 0x03020302u : 0x01000100u);
 }
-// two 16-bit LDS values -> one dword {lo, hi}: ds_read_u16 + ds_read_u16_d16_hi,
-// no shift / or to pair them
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t lds_u16_pair(const uint8_t* lo, const uint8_t* hi) {
-    u16x2 v;
-    v.x = *(const uint16_t*)lo;
-    v.y = *(const uint16_t*)hi;
-    return __builtin_bit_cast(uint32_t, v);
-}
 // f16 pair {scale of row r0, scale of row r1} for block b
 template <int T, int D>
 __device__ __forceinline__ f16x2 scale_pair(const RowScales<T, D>& s0, const RowScales<T, D>& s1, int b) {
@@ -560,25 +551,22 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     FATTN_STAMP8(11);
     if (old != (uint32_t)(NP - 1)) return;
     if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // ---- merge: every load issued before one wait (parts past NP: out of range, zeros)
-    const uint32_t obytes = (uint32_t)(NP * D * 4);
-    const i32x4 osrd = make_srd(a.ws_o + tile * NP * D, obytes);
+    // ---- merge: lane half h = lane / 32 takes the parts of parity h, dims
+    // 4 (lane % 32) .. +3, one 16-B load per part (parts past NP fall outside
+    // the descriptor: zeros, no traffic, weight 0); the halves meet by one
+    // permlane32 swap.  Every load of a batch is issued before one wait.
+    const int h = lane >> 5, d4 = 4 * (lane & 31);
+    const i32x4 osrd = make_srd(a.ws_o + tile * NP * D, (uint32_t)(NP * D * 4));
     const i32x4 msrd = make_srd(a.ws_ml + 2 * tile * NP, (uint32_t)(NP * 8));
-    uint32_t v0[kWaveMergeBatch], v1[kWaveMergeBatch];
+    constexpr int kIt = kWaveMergeBatch / 2;  // part pairs per round trip
+    u32x4 v[kIt];
     auto issue = [&](int p0) {
 #pragma unroll
-        for (int p = 0; p < kWaveMergeBatch; p++) {
-            const uint32_t off = p0 + p < NP ? (uint32_t)(((p0 + p) * D + 2 * lane) * 4) : obytes;
-            v0[p] = ld_sc1_buf_b32(osrd, off);
-            v1[p] = ld_sc1_buf_b32(osrd, off + 4);
-        }
+        for (int i = 0; i < kIt; i++) v[i] = ld_sc1_buf(osrd, (uint32_t)(((p0 + 2 * i + h) * D + d4) * 4));
     };
     auto fence = [&] {
 #pragma unroll
-        for (int p = 0; p < kWaveMergeBatch; p++) {
-            reg_fence(v0[p]);
-            reg_fence(v1[p]);
-        }
+        for (int i = 0; i < kIt; i++) reg_fence(v[i]);
     };
     issue(0);
     uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
@@ -592,7 +580,7 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     const float M = seg_reduce<true>(mp, 64);
     const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M);
     const float L = seg_reduce<false>(lane < NP ? w * __builtin_bit_cast(float, mll) : 0.0f, 64);
-    float acc0 = 0.0f, acc1 = 0.0f;
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int p0 = 0; p0 < NP; p0 += kWaveMergeBatch) {  // wave-uniform
         if (p0 > 0) {
             issue(p0);
@@ -600,18 +588,25 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
             fence();
         }
 #pragma unroll
-        for (int p = 0; p < kWaveMergeBatch; p++) {
-            const float wp = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w), p0 + p));
-            acc0 += wp * __builtin_bit_cast(float, v0[p]);
-            acc1 += wp * __builtin_bit_cast(float, v1[p]);
+        for (int i = 0; i < kIt; i++) {
+            const int wi = __builtin_bit_cast(int, w);
+            const float we = __builtin_bit_cast(float, __builtin_amdgcn_readlane(wi, p0 + 2 * i));
+            const float wo = __builtin_bit_cast(float, __builtin_amdgcn_readlane(wi, p0 + 2 * i + 1));
+            const float wp = h ? wo : we;
+            acc += wp * __builtin_bit_cast(f32x4, v[i]);
         }
     }
+    acc.x = xor32_pair(acc.x, false);
+    acc.y = xor32_pair(acc.y, false);
+    acc.z = xor32_pair(acc.z, false);
+    acc.w = xor32_pair(acc.w, false);
+    if (h) return;  // lanes 0..31 store the row, 16 B each
     const int rq = div_R(a, 0);
     const int riq1 = qt * a.QPT + rq;
     const int riq2 = ik2 * a.rk2 + hs * a.R;
-    float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + 2 * lane;
-    const float inv = 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
-    *(f32x2*)out = f32x2{L == 0.0f ? __builtin_nanf("") : acc0 * inv, L == 0.0f ? __builtin_nanf("") : acc1 * inv};
+    float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + d4;
+    const float inv = L == 0.0f ? __builtin_nanf("") : 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
+    *(f32x4*)out = acc * inv;
     FATTN_STAMP8(13);
 }
 
@@ -884,11 +879,15 @@ __device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* bu
             constexpr int BB = TypeInfo<C::VTT>::block_bytes;
             // block-b scales of this lane's 8 rows (4g..4g+3, 16+4g..16+4g+3):
             // the dword holding each, then f16 pairs {row r, row r+1}
-            const uint8_t* sp = vb + BB * b;
-            const f16x2 d01 = as_h2(lds_u16_pair(sp + (rA + 0) * C::rowV, sp + (rA + 1) * C::rowV));
-            const f16x2 d23 = as_h2(lds_u16_pair(sp + (rA + 2) * C::rowV, sp + (rA + 3) * C::rowV));
-            const f16x2 d45 = as_h2(lds_u16_pair(sp + (rB + 0) * C::rowV, sp + (rB + 1) * C::rowV));
-            const f16x2 d67 = as_h2(lds_u16_pair(sp + (rB + 2) * C::rowV, sp + (rB + 3) * C::rowV));
+            uint32_t sw[8];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                sw[r] = *(const uint32_t*)(vb + (rA + r) * C::rowV + ((BB * b) & ~3));
+                sw[4 + r] = *(const uint32_t*)(vb + (rB + r) * C::rowV + ((BB * b) & ~3));
+            }
+            const uint32_t sel = ((BB * b) & 2) ? 0x07060302u : 0x05040100u;  // b is unrolled
+            const f16x2 d01 = as_h2(perm_b32(sw[1], sw[0], sel)), d23 = as_h2(perm_b32(sw[3], sw[2], sel));
+            const f16x2 d45 = as_h2(perm_b32(sw[5], sw[4], sel)), d67 = as_h2(perm_b32(sw[7], sw[6], sel));
             // P'_b = P * d_b (element j <-> row of element j of the A operand)
             f16x8 pbd;
             pbd.s01 = pb.s01 * d01;
@@ -903,16 +902,17 @@ __device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* bu
             if constexpr (kVQ8) {
                 // one u16 per row carries columns 2i (-> tile E_b) and 2i+1 (-> tile O_b)
                 const uint8_t* cp = vb + b * BB + 2 + 2 * i16;
-                uint32_t w2[4];  // rows (r, r+1) of this lane's 8: {u16 of row r, u16 of row r+1}
-                w2[0] = lds_u16_pair(cp + (rA + 0) * C::rowV, cp + (rA + 1) * C::rowV);
-                w2[1] = lds_u16_pair(cp + (rA + 2) * C::rowV, cp + (rA + 3) * C::rowV);
-                w2[2] = lds_u16_pair(cp + (rB + 0) * C::rowV, cp + (rB + 1) * C::rowV);
-                w2[3] = lds_u16_pair(cp + (rB + 2) * C::rowV, cp + (rB + 3) * C::rowV);
+                uint32_t w[8];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    w[r] = *(const uint16_t*)(cp + (rA + r) * C::rowV);
+                    w[4 + r] = *(const uint16_t*)(cp + (rB + r) * C::rowV);
+                }
                 u32x4 ae, ao;  // f16 pairs 1152 + q (exact)
 #pragma unroll
                 for (int pr = 0; pr < 4; pr++) {
                     // bytes [e_r, o_r, e_r+1, o_r+1] -> xor 0x80 -> f16 magic 0x64xx
-                    const uint32_t t2 = w2[pr] ^ 0x80808080u;
+                    const uint32_t t2 = (w[2 * pr] | (w[2 * pr + 1] << 16)) ^ 0x80808080u;
                     ae[pr] = perm_b32(0x64646464u, t2, 0x04020400u);
                     ao[pr] = perm_b32(0x64646464u, t2, 0x04030401u);
                 }

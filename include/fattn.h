@@ -147,7 +147,7 @@ enum {
     FATTN_OPT_DEC_LOADERS = 15,     /* loader waves per fattn_dec_kernel workgroup: 2 (the only value kept) */
     FATTN_OPT_DEC_COMPUTE = 16,     /* compute waves per fattn_dec_kernel workgroup: 4 (default) or 8 */
     FATTN_OPT_DEC_DIAG = 17,        /* diagnostics only: 1 = fattn_dec_kernel skips the compute, 2 = skips the
-                                       K/V DMA (results are garbage) */
+                                       K/V DMA, 3 = both (results are garbage) */
     FATTN_OPT_DEC_AHEAD = 18        /* fattn_dec_kernel: 32-position steps in flight per loader wave (1..8,
                                        default 8; vmcnt caps it at 63 / instructions per step) */
 };
