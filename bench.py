@@ -229,12 +229,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-mq", action="store_true", help="never pick the multi-query kernel (split-KV kernel only)")
     ap.add_argument("--split-prio", type=int, default=0,
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
-    ap.add_argument("--dec", type=int, default=0,
-                    help="split-KV decode: 0 auto (loader-wave kernel), 1 split kernel only, 2 loader kernel")
-    ap.add_argument("--dec-loaders", type=int, default=0, help="loader waves per decode workgroup (1, 2; 0 = default)")
-    ap.add_argument("--dec-compute", type=int, default=0, help="compute waves per decode workgroup (4, 8; 0 = default)")
-    ap.add_argument("--dec-diag", type=int, default=0, help="decode diagnostics: 1 no compute, 2 no DMA")
-    ap.add_argument("--dec-ahead", type=int, default=0, help="decode: steps in flight per loader wave (0 = default)")
+    ap.add_argument("--waves", type=int, default=0, help="split kernel waves per workgroup (4, 8, 16; 0 = planner)")
+    ap.add_argument("--lag", type=int, default=-1, help="split kernel: 1 = issue the next step once the current landed")
     ap.add_argument("--wave-merge", type=int, default=-1, help="split/dec one-row tiles: 0 per-wave merge, 1 LDS merge")
     ap.add_argument("--prefill-causal", action="store_true",
                     help="causal mask on the prefill measurement (fully masked blocks are skipped)")
@@ -253,9 +249,9 @@ def apply_options(args):
     import fattn
     opts = [(args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT), (args.pf, fattn.OPT_PF),
             (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO),
-            (args.dec, fattn.OPT_DEC), (args.dec_loaders, fattn.OPT_DEC_LOADERS),
-            (args.dec_compute, fattn.OPT_DEC_COMPUTE), (args.dec_diag, fattn.OPT_DEC_DIAG),
-            (args.dec_ahead, fattn.OPT_DEC_AHEAD)]
+            (args.waves, fattn.OPT_SPLIT_WAVES)]
+    if args.lag >= 0:
+        fattn.set_option(fattn.OPT_SPLIT_LAG, args.lag)
     for val, opt in opts:
         if val:
             fattn.set_option(opt, val)

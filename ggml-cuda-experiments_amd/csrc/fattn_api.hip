@@ -15,18 +15,13 @@
 #include <cstring>
 #include <type_traits>
 
-#include "fattn_quant.h"
-#include "fattn_mq.h"
-#include "fattn_pf.h"
-#include "fattn_split.h"
-#include "fattn_dec.h"
+#include "fattn_launch.h"
 
 using namespace fattn;
 
 namespace {
 
 constexpr int kCUsDefault = 256;  // MI355X; used when no device can be queried (host-only planning)
-constexpr int kMaxDevices = 64;
 
 // compute units of the current device, queried once per device
 int device_cus() {
@@ -59,31 +54,11 @@ std::atomic<int> g_opt_mq_min_rows{256};  // multi-query kernel from this many p
 std::atomic<int> g_opt_pf_no_skip{0};     // 1: masked prefill without the live-block pre-pass (FATTN_OPT_PF_SKIP)
 std::atomic<int> g_opt_split_prio{0};     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
 std::atomic<int> g_opt_no_wave_merge{0};  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
-std::atomic<int> g_opt_dec{1};         // split-KV decode: 0 auto (loader-wave kernel), 1 split kernel only, 2 loader kernel
-std::atomic<int> g_opt_dec_compute{4}; // compute waves per fattn_dec_kernel workgroup (4 or 8)
-std::atomic<int> g_opt_dec_diag{0};
-std::atomic<int> g_opt_dec_ahead{8};  // steps in flight per loader wave (FATTN_OPT_DEC_AHEAD)    // fattn_dec_kernel diagnostics (1 no compute, 2 no DMA)
+std::atomic<int> g_opt_split_waves{0};
+std::atomic<int> g_opt_split_lag{-1};  // FATTN_OPT_SPLIT_LAG (-1 = planner)  // split kernel waves per workgroup (FATTN_OPT_SPLIT_WAVES; 0 = auto)
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
-
-struct Plan {
-    SplitArgs a;
-    int kt, vt;  // vt may be VT_F16T
-    int D;
-    int gran;
-    dim3 grid;
-    int lds;
-    size_t ws_bytes, cnt_bytes, ml_bytes;
-    int cus;  // compute units of the device the plan is for
-    bool mq;  // multi-query kernel (fattn_mq.h)
-    bool dec; // split-KV decode with loader waves (fattn_dec.h)
-    int nlw;  // its loader waves
-    int ncw;  // its compute waves
-    bool pf;  // prefill kernel (fattn_pf.h)
-    bool pf_flags;          // masked prefill: live-block flags pre-pass (tile-range skipping)
-    int nw;   // its waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
-};
 
 // LDS geometry of one instantiation (type-erased for the planner)
 struct Geom {
@@ -92,7 +67,7 @@ struct Geom {
         const int w = (nbuf * step_bytes + vsc_bytes + 15) / 16 * 16;
         return w > merge_bytes ? w : merge_bytes;
     }
-    int lds_bytes(int nbuf) const { return kSplitWaves * wave_bytes(nbuf); }
+    int lds_bytes(int nbuf, int nwv) const { return nwv * wave_bytes(nbuf); }
 };
 
 template <int KT, int VT, int D>
@@ -123,18 +98,39 @@ bool combine_ok(int64_t nch, int rv, int D) {
     return nch <= 64 && ncp * rv <= 256;
 }
 
-// Split-KV sizing for 256 CUs.  Every wave streams `spw` steps of 32 positions;
-// the grid is sized so that all (Y x S x chunks) workgroups are co-resident
-// (one wave per step when the problem is small: maximum memory-level
-// parallelism, no tail), limited by LDS (steps in flight) and registers.
+// Split-KV sizing.  A workgroup has nwv waves (4, 8 or 16); every wave streams
+// `spw` steps of 32 positions.  Waves per workgroup follow the steps each CU
+// gets: 16 from 12 steps per CU up, 8 from 6 (the register budget and one step
+// in flight per wave in LDS permitting), else 4.  The grid is sized so that
+// all (Y x S x chunks) workgroups are co-resident, limited by LDS (steps in
+// flight) and registers.
 int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t NQ) {
     SplitArgs& a = pl.a;
     const Geom G = geom(pl.kt, pl.vt, pl.D);
-    const int quantum = kStep * kSplitWaves;
     const int64_t steps = (N + kStep - 1) / kStep;
-    const int vgpr_wgs = (pl.kt == FATTN_TYPE_F16 || pl.gran == 4 || pl.D == 256) ? 2 : 4;  // __launch_bounds__ waves/SIMD
+    const int wps = (pl.kt == FATTN_TYPE_F16 || pl.gran == 4 || pl.D == 256) ? 2 : 4;  // __launch_bounds__ waves/SIMD
     const int rv_max = std::min<int64_t>(kRows, (int64_t)a.R * std::min<int64_t>(a.QPT, NQ));
-    int spw = 1, nbuf = 1;
+    const int64_t total = steps * Y * S;
+    int nwv = 4;
+    if (pl.gran == 16) {
+        if (g_opt_split_waves > 0) {
+            nwv = g_opt_split_waves;
+        } else if (kv_chunk <= 0) {
+            const int64_t per_cu = total / pl.cus;
+            nwv = per_cu >= 12 ? 16 : per_cu >= 6 ? 8 : 4;
+        }
+        nwv = std::min(nwv, 4 * wps);
+        while (nwv > 4 && G.lds_bytes(1, nwv) > kLdsPerCU) nwv /= 2;
+    }
+    const int quantum = kStep * nwv;
+    // steps in flight per wave: 2 with 4 waves (the measured optimum of the
+    // 4-wave form); with more waves as many as LDS holds, up to 4
+    auto inflight = [&](int spw_) {
+        int nb = std::min(spw_, nwv == 4 ? 2 : 4);
+        while (nb > 1 && G.lds_bytes(nb, nwv) > kLdsPerCU) nb--;
+        return nb;
+    };
+    int spw = 1;
     if (kv_chunk > 0) {
         spw = (int)((kv_chunk + quantum - 1) / quantum);
         for (;;) {  // a forced chunk is a lower bound: grow it until the combine fits
@@ -143,41 +139,31 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
             spw++;
         }
     } else {
-        // About one 4-wave workgroup per CU, each wave streaming its slice with
-        // two steps in flight -- the measured optimum on the decode shapes
-        // (config 3: 4 steps per wave, config 4: 2, config 2 (f16): 2 -- 10.3
-        // vs 11.9 us at one step), which also keeps the chunk count per tile
-        // (the cross-workgroup merge) small.  Fewer in flight where LDS is short.
-        {
-            const int64_t total = steps * Y * S;
-            spw = (int)std::max<int64_t>(1, (total + (int64_t)pl.cus * kSplitWaves / 2) / ((int64_t)pl.cus * kSplitWaves));
-            spw = (int)std::min<int64_t>(spw, (steps + kSplitWaves - 1) / kSplitWaves);
-        }
+        spw = (int)std::max<int64_t>(1, (total + (int64_t)pl.cus * nwv / 2) / ((int64_t)pl.cus * nwv));
+        spw = (int)std::min<int64_t>(spw, (steps + nwv - 1) / nwv);
         for (;;) {
-            nbuf = spw == 1 ? 1 : 2;
-            while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
-            const int wgs_cu = std::max(1, std::min(vgpr_wgs, kLdsPerCU / G.lds_bytes(nbuf)));
-            const int64_t slots = (int64_t)pl.cus * wgs_cu * kSplitWaves;
+            const int nb = inflight(spw);
+            const int wgs_cu = std::max(1, std::min(4 * wps / nwv, kLdsPerCU / G.lds_bytes(nb, nwv)));
+            const int64_t slots = (int64_t)pl.cus * wgs_cu * nwv;
             const int64_t need = (int64_t)((steps + spw - 1) / spw) * Y * S;  // waves at this spw
             const int64_t nch = (N + (int64_t)spw * quantum - 1) / ((int64_t)spw * quantum);
             const bool reducer_ok = nch == 1 || combine_ok(nch, rv_max, pl.D);
             if ((need <= slots && reducer_ok) || nch == 1) break;
             spw++;
         }
+        if (g_opt_split_spw > 0) {
+            spw = (int)std::min<int64_t>(g_opt_split_spw, (steps + nwv - 1) / nwv);
+            const int64_t nch = (N + (int64_t)spw * quantum - 1) / ((int64_t)spw * quantum);
+            if (nch > 1 && !combine_ok(nch, rv_max, pl.D)) return FATTN_ERR_INVALID_ARG;
+        }
     }
-    nbuf = std::min(spw, 2);
-    while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
-    if (kv_chunk <= 0 && g_opt_split_spw > 0) {
-        spw = (int)std::min<int64_t>(g_opt_split_spw, (steps + kSplitWaves - 1) / kSplitWaves);
-        nbuf = std::min(spw, 2);
-        while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
-        const int64_t nch = (N + (int64_t)spw * quantum - 1) / ((int64_t)spw * quantum);
-        if (nch > 1 && !combine_ok(nch, rv_max, pl.D)) return FATTN_ERR_INVALID_ARG;
-    }
+    int nbuf = inflight(spw);
     if (g_opt_split_nbuf > 0) {
         nbuf = std::min(spw, (int)g_opt_split_nbuf);
-        while (nbuf > 1 && G.lds_bytes(nbuf) > kLdsPerCU) nbuf--;
+        while (nbuf > 1 && G.lds_bytes(nbuf, nwv) > kLdsPerCU) nbuf--;
     }
+    pl.nwv = nwv;
+    a.issue_lag = g_opt_split_lag >= 0 ? (int)g_opt_split_lag : 0;
     a.nbuf = nbuf;
     a.split_prio = g_opt_split_prio;
     a.wave_bytes = G.wave_bytes(nbuf);
@@ -186,85 +172,26 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     a.ncp = 1;
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     if (a.n_chunks > 1 && !combine_ok(a.n_chunks, rv_max, pl.D)) return FATTN_ERR_INVALID_ARG;
-    // one-row tiles with few parts: per-wave partials, merged by the last wave
-    a.wave_merge = a.n_chunks > 1 && rv_max == 1 && pl.D == 128 && !g_opt_no_wave_merge &&
-                   a.n_chunks * kSplitWaves <= kWaveMergeParts;
-    pl.lds = G.lds_bytes(nbuf);
+    // epilogue: one-row tiles with few parts publish per wave and the last wave
+    // merges (4-wave form, D = 128); other one-row tiles merge their waves in
+    // LDS and publish one row per workgroup; multi-row tiles: combine_tile
+    a.wave_merge = 0;
+    if (rv_max == 1 && !g_opt_no_wave_merge) {
+        if (nwv == 4 && a.n_chunks > 1 && pl.D == 128 && a.n_chunks * nwv <= kWaveMergeParts) a.wave_merge = 1;
+        else if (nwv > 4 || a.n_chunks > 1) a.wave_merge = 2;
+    }
+    pl.lds = G.lds_bytes(nbuf, nwv);
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     if (a.n_chunks > 1 && a.wave_merge) {
-        // [arrival counters][(m, l) per part][row-0 O per part], parts = waves
-        const size_t parts = (size_t)S * Y * a.n_chunks * kSplitWaves;
+        // [arrival counters][(m, l) per part][row-0 O per part]; parts = waves
+        // (wave_merge 1) or workgroups (2)
+        const size_t parts = (size_t)S * Y * a.n_chunks * (a.wave_merge == 1 ? nwv : 1);
         pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
         pl.ml_bytes = (parts * 2 * sizeof(float) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + parts * pl.D * 4;
     } else if (a.n_chunks > 1) {
         // [arrival counters, one 256-B line per tile][(m, l) pairs][O partials];
         // zero-filled once per allocation: each launch re-arms the counters
-        pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
-        pl.ml_bytes = ((size_t)S * Y * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
-        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + (size_t)S * Y * a.n_chunks * kRows * pl.D * 4;
-    } else {
-        pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
-    }
-    return FATTN_OK;
-}
-
-// Loader-wave decode sizing (fattn_dec_kernel): about one workgroup per CU,
-// each chunk at least one step per compute wave; the chunk's steps get an LDS
-// ring of as many step images as fit (all of them on the decode shapes, so
-// every byte is requested at kernel start).
-int size_dec(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t NQ) {
-    SplitArgs& a = pl.a;
-    const Geom G = geom(pl.kt, pl.vt, pl.D);
-    const int64_t steps = (N + kStep - 1) / kStep;
-    const int64_t tiles = Y * S;
-    const int rv_max = std::min<int64_t>(kRows, (int64_t)a.R * std::min<int64_t>(a.QPT, NQ));
-    const bool wm_ok = rv_max == 1 && pl.D == 128 && !g_opt_no_wave_merge;
-    const int ncw = g_opt_dec_compute;
-    int64_t cs;  // steps per chunk
-    if (kv_chunk > 0) {
-        cs = (kv_chunk + kStep - 1) / kStep;
-    } else {
-        const int64_t nch = std::max<int64_t>(1, (pl.cus + tiles / 2) / tiles);
-        cs = (steps + nch - 1) / nch;
-        cs = std::max<int64_t>(cs, std::min<int64_t>(steps, ncw));
-    }
-    int64_t nch;
-    for (;;) {
-        nch = (steps + cs - 1) / cs;
-        const bool ok = nch == 1 || (wm_ok && nch * ncw <= kWaveMergeParts) || combine_ok(nch, rv_max, pl.D);
-        if (ok) break;
-        cs++;
-    }
-    const int nlw = 2;  // steps per chunk >= 2 (cs >= min(steps, ncw); one-step chunks: spl 0, rejected below)
-    const int step_bytes = G.step_bytes;
-    // equal rings per loader: slot(s) = loader + nlw * ((s / nlw) % (nslot / nlw))
-    const int fit = (int)std::min<int64_t>(kDecMaxSlots, (kLdsPerCU - kDecHdr) / step_bytes);
-    const int whole = (int)((cs + nlw - 1) / nlw * nlw);  // every step its own slot
-    int nslot = whole <= fit ? whole : fit - fit % nlw;
-    if (nslot < nlw) return FATTN_ERR_INVALID_ARG;
-    a.nbuf = nslot;
-    a.split_prio = 0;
-    a.wave_bytes = 0;
-    a.chunk_len = (int)(cs * kStep);
-    a.n_chunks = (int)nch;
-    a.ncp = 1;
-    while (a.ncp < a.n_chunks) a.ncp <<= 1;
-    a.wave_merge = a.n_chunks > 1 && wm_ok && a.n_chunks * ncw <= kWaveMergeParts;
-    a.dec_diag = g_opt_dec_diag;
-    a.dec_ahead = g_opt_dec_ahead;
-    const int combine_bytes = kRows * pl.D * 4 + kRows * 64 * 4 + kRows * 4;
-    pl.lds = std::max({kDecHdr + nslot * step_bytes, ncw * G.merge_bytes, combine_bytes});
-    pl.dec = true;
-    pl.nlw = nlw;
-    pl.ncw = ncw;
-    pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
-    if (a.n_chunks > 1 && a.wave_merge) {
-        const size_t parts = (size_t)S * Y * a.n_chunks * ncw;
-        pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
-        pl.ml_bytes = (parts * 2 * sizeof(float) + 255) / 256 * 256;
-        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + parts * pl.D * 4;
-    } else if (a.n_chunks > 1) {
         pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
         pl.ml_bytes = ((size_t)S * Y * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + (size_t)S * Y * a.n_chunks * kRows * pl.D * 4;
@@ -476,156 +403,8 @@ int make_plan(const fattn_params* p, Plan& pl) {
         pl.ws_bytes = pl.cnt_bytes;
         return FATTN_OK;
     }
-    pl.dec = false;
-    const bool dec_ok = g16 && g_opt_dec != 1;
-    int rc = FATTN_ERR_INVALID_ARG;
-    if (pl.mq) rc = size_mq(pl, p->kv_chunk, Y, S, N);
-    else if (dec_ok) rc = size_dec(pl, p->kv_chunk, Y, S, N, NQ);
-    if (!pl.mq && rc != FATTN_OK) {  // not the loader kernel, or a shape it does not take (one-step chunks)
-        pl.dec = false;
-        rc = size_split(pl, p->kv_chunk, Y, S, N, NQ);
-    }
-    if (rc != FATTN_OK) return rc;
-    return FATTN_OK;
-}
-
-struct Events {
-    hipEvent_t begin = nullptr, end = nullptr;
-};
-
-// Launch with errors attributed to this launch only: a pending error left on
-// the thread by other code is cleared first; FATTN_DEBUG=1 names a failure.
-template <typename F>
-int launch_kernel(const void* kern, const Plan& pl, hipStream_t st, const Events& ev, F&& go) {
-    (void)hipGetLastError();
-    // large dynamic LDS must be allowed per kernel and per device: cached per
-    // (launch site = F's instantiation, device); a lost race only repeats the call
-    static std::atomic<int> lds_set[kMaxDevices];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
-    if (pl.lds > 65536 && pl.lds > lds_set[dev].load(std::memory_order_relaxed)) {
-        // the query loads the code object (HIP loads kernels lazily; setting an
-        // attribute of a kernel whose module is not loaded yet fails)
-        hipFuncAttributes fa;
-        (void)hipFuncGetAttributes(&fa, kern);
-        if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, pl.lds) == hipSuccess) {
-            lds_set[dev].store(pl.lds, std::memory_order_relaxed);
-        } else if (std::getenv("FATTN_DEBUG")) {
-            std::fprintf(stderr, "fattn: hipFuncSetAttribute(%d B LDS) failed; launching anyway\n", pl.lds);
-        }
-        (void)hipGetLastError();
-    }
-    if (ev.begin) (void)hipEventRecord(ev.begin, st);
-    go();
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        if (std::getenv("FATTN_DEBUG"))
-            std::fprintf(stderr, "fattn: launch grid (%u,%u,%u) lds %d failed: %s\n", pl.grid.x, pl.grid.y, pl.grid.z,
-                         pl.lds, hipGetErrorString(e));
-        return FATTN_ERR_LAUNCH;
-    }
-    if (ev.end) (void)hipEventRecord(ev.end, st);
-    return FATTN_OK;
-}
-
-template <int KT, int VT, int D, int GRAN, bool HM>
-int launch_split_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    auto kern = fattn_split_kernel<KT, VT, D, GRAN, HM>;
-    return launch_kernel((const void*)kern, pl, st, ev, [&] {
-        hipLaunchKernelGGL(kern, pl.grid, dim3(kSplitWaves * kWave), pl.lds, st, pl.a);
-    });
-}
-
-template <int KT, int VT, int D, int GRAN>
-int launch_split(const Plan& pl, hipStream_t st, const Events& ev) {
-    return pl.a.has_mask ? launch_split_hm<KT, VT, D, GRAN, true>(pl, st, ev)
-                         : launch_split_hm<KT, VT, D, GRAN, false>(pl, st, ev);
-}
-
-template <int KT, int VT, int D, bool HM, int NLW, int NCW>
-int launch_dec_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    auto kern = fattn_dec_kernel<KT, VT, D, HM, NLW, NCW>;
-    return launch_kernel((const void*)kern, pl, st, ev, [&] {
-        hipLaunchKernelGGL(kern, pl.grid, dim3((NCW + NLW) * kWave), pl.lds, st, pl.a);
-    });
-}
-
-template <int KT, int VT, int D, int NCW>
-int launch_dec_w(const Plan& pl, hipStream_t st, const Events& ev) {
-    // two loader waves (one loader measured 20 us on config 3 against 15.7)
-    return pl.a.has_mask ? launch_dec_hm<KT, VT, D, true, 2, NCW>(pl, st, ev)
-                         : launch_dec_hm<KT, VT, D, false, 2, NCW>(pl, st, ev);
-}
-
-template <int KT, int VT, int D>
-int launch_dec(const Plan& pl, hipStream_t st, const Events& ev) {
-    return pl.ncw == 8 ? launch_dec_w<KT, VT, D, 8>(pl, st, ev) : launch_dec_w<KT, VT, D, 4>(pl, st, ev);
-}
-
-template <int KT, int VT, int D>
-int launch_gran(const Plan& pl, hipStream_t st, const Events& ev) {
-    if (pl.dec) return launch_dec<KT, VT, D>(pl, st, ev);
-    if constexpr (VT == VT_F16T) {
-        return launch_split<KT, VT, D, 16>(pl, st, ev);
-    } else {
-        return pl.gran == 16 ? launch_split<KT, VT, D, 16>(pl, st, ev) : launch_split<KT, VT, D, 4>(pl, st, ev);
-    }
-}
-
-template <int KT, int D, int NW, bool HM>
-int launch_mq_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    auto kern = fattn_mq_kernel<KT, D, NW, HM>;
-    return launch_kernel((const void*)kern, pl, st, ev, [&] {
-        hipLaunchKernelGGL(kern, pl.grid, dim3(NW * kWave), pl.lds, st, pl.a);
-    });
-}
-
-template <int KT, int D>
-int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
-    if (pl.nw == 8)
-        return pl.a.has_mask ? launch_mq_hm<KT, D, 8, true>(pl, st, ev) : launch_mq_hm<KT, D, 8, false>(pl, st, ev);
-    return pl.a.has_mask ? launch_mq_hm<KT, D, 4, true>(pl, st, ev) : launch_mq_hm<KT, D, 4, false>(pl, st, ev);
-}
-
-template <int KT, bool HM>
-int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    auto kern = fattn_pf_kernel<KT, 128, HM>;
-    return launch_kernel((const void*)kern, pl, st, ev, [&] {
-        if (HM && pl.a.pf_flags)
-            hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,
-                               pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
-        hipLaunchKernelGGL(kern, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
-        if (HM && pl.a.pf_flags) (void)hipMemsetAsync((void*)pl.a.pf_flags, 0, pl.cnt_bytes, st);
-    });
-}
-
-template <int KT>
-int launch_pf(const Plan& pl, hipStream_t st, const Events& ev) {
-    return pl.a.has_mask ? launch_pf_hm<KT, true>(pl, st, ev) : launch_pf_hm<KT, false>(pl, st, ev);
-}
-
-template <int D>
-int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
-    if constexpr (D == 128) {
-        if (pl.pf) {
-            if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_pf<FATTN_TYPE_F16>(pl, st, ev);
-            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0>(pl, st, ev);
-            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0>(pl, st, ev);
-            return FATTN_ERR_UNSUPPORTED_TYPE;
-        }
-    }
-    if constexpr (D <= 128) {
-        if (pl.mq) {
-            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_mq<FATTN_TYPE_Q8_0, D>(pl, st, ev);
-            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_mq<FATTN_TYPE_Q4_0, D>(pl, st, ev);
-            return FATTN_ERR_UNSUPPORTED_TYPE;
-        }
-    }
-    if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_gran<FATTN_TYPE_Q8_0, FATTN_TYPE_Q8_0, D>(pl, st, ev);
-    if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_gran<FATTN_TYPE_Q4_0, FATTN_TYPE_Q4_0, D>(pl, st, ev);
-    if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_gran<FATTN_TYPE_F16, FATTN_TYPE_F16, D>(pl, st, ev);
-    if (pl.kt == FATTN_TYPE_F16 && pl.vt == VT_F16T) return launch_gran<FATTN_TYPE_F16, VT_F16T, D>(pl, st, ev);
-    return FATTN_ERR_UNSUPPORTED_TYPE;
+    pl.nwv = 4;
+    return pl.mq ? size_mq(pl, p->kv_chunk, Y, S, N) : size_split(pl, p->kv_chunk, Y, S, N, NQ);
 }
 
 }  // namespace
@@ -634,8 +413,11 @@ extern "C" {
 
 #ifdef FATTN_STAMPS
 // diagnostic build only: where the split kernel writes its phase stamps
+int fattn_debug_set_stamps_d64(void*);
+int fattn_debug_set_stamps_d128(void*);
+int fattn_debug_set_stamps_d256(void*);
 int fattn_debug_set_stamps(void* dev_ptr) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(void*)) == hipSuccess ? 0 : -1;
+    return fattn_debug_set_stamps_d64(dev_ptr) | fattn_debug_set_stamps_d128(dev_ptr) | fattn_debug_set_stamps_d256(dev_ptr);
 }
 // grid of the plan: out[0..2] = chunks, Y, S
 int fattn_debug_plan(const fattn_params* p, int* out) {
@@ -692,23 +474,20 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;
             g_opt_split_spw = value;
             return FATTN_OK;
-        case FATTN_OPT_DEC:
-            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
-            g_opt_dec = value;
-            return FATTN_OK;
+        case FATTN_OPT_DEC:  // the loader-wave decode kernel was removed (slower)
+            return value == 0 || value == 1 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_DEC_LOADERS:
-            return value == 2 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_DEC_COMPUTE:
-            if (value != 4 && value != 8) return FATTN_ERR_INVALID_ARG;
-            g_opt_dec_compute = value;
-            return FATTN_OK;
         case FATTN_OPT_DEC_AHEAD:
-            if (value < 1 || value > 8) return FATTN_ERR_INVALID_ARG;
-            g_opt_dec_ahead = value;
-            return FATTN_OK;
         case FATTN_OPT_DEC_DIAG:
-            if (value < 0 || value > 3) return FATTN_ERR_INVALID_ARG;
-            g_opt_dec_diag = value;
+            return value == 0 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
+        case FATTN_OPT_SPLIT_LAG:
+            if (value < -1 || value > 1) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_lag = value;
+            return FATTN_OK;
+        case FATTN_OPT_SPLIT_WAVES:
+            if (value != 0 && value != 4 && value != 8 && value != 16) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_waves = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:
             if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
@@ -771,12 +550,9 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
                       tn(pl.kt), pl.D, hm);
     else if (pl.mq)
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>", tn(pl.kt), pl.D, pl.nw, hm);
-    else if (pl.dec)
-        std::snprintf(kern, sizeof kern, "fattn_dec_kernel<%s,%s,D%d,%s,%dloaders,%dcompute>", tn(pl.kt), tn(pl.vt),
-                      pl.D, hm, pl.nlw, pl.ncw);
     else
-        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s>", tn(pl.kt), tn(pl.vt), pl.D,
-                      pl.gran, hm);
+        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>", tn(pl.kt), tn(pl.vt), pl.D,
+                      pl.gran, hm, pl.nwv);
     const int n = std::snprintf(out, cap, "%s grid(%u,%u,%u) lds %d chunk %d steps/slots %d ws %zu", kern, pl.grid.x,
                                 pl.grid.y, pl.grid.z, pl.lds, pl.a.chunk_len, pl.a.nbuf, pl.ws_bytes);
     return n < 0 || (size_t)n >= cap ? FATTN_ERR_INVALID_ARG : FATTN_OK;

@@ -1,0 +1,192 @@
+// fattn_launch.h -- the launch plan and the kernel launchers, shared by the
+// planner / C ABI (fattn_api.hip) and the per-head-dim translation units
+// (fattn_launch_d*.hip: each instantiates launch_types<D>, so the kernels of
+// the head dims compile in parallel).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+
+#include "fattn_quant.h"
+#include "fattn_mq.h"
+#include "fattn_pf.h"
+#include "fattn_split.h"
+
+namespace fattn {
+
+constexpr int kMaxDevices = 64;
+
+struct Plan {
+    SplitArgs a;
+    int kt, vt;  // vt may be VT_F16T
+    int D;
+    int gran;
+    dim3 grid;
+    int lds;
+    size_t ws_bytes, cnt_bytes, ml_bytes;
+    int cus;  // compute units of the device the plan is for
+    int nwv;  // split kernel: waves per workgroup (4, 8, 16)
+    bool mq;  // multi-query kernel (fattn_mq.h)
+    bool pf;  // prefill kernel (fattn_pf.h)
+    bool pf_flags;          // masked prefill: live-block flags pre-pass (tile-range skipping)
+    int nw;   // mq kernel: waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
+};
+
+struct Events {
+    hipEvent_t begin = nullptr, end = nullptr;
+};
+
+// Launch with errors attributed to this launch only: a pending error left on
+// the thread by other code is cleared first; FATTN_DEBUG=1 names a failure.
+template <typename F>
+int launch_kernel(const void* kern, const Plan& pl, hipStream_t st, const Events& ev, F&& go) {
+    (void)hipGetLastError();
+    // large dynamic LDS must be allowed per kernel and per device: cached per
+    // (launch site = F's instantiation, device); a lost race only repeats the call
+    static std::atomic<int> lds_set[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
+    if (pl.lds > 65536 && pl.lds > lds_set[dev].load(std::memory_order_relaxed)) {
+        // the query loads the code object (HIP loads kernels lazily; setting an
+        // attribute of a kernel whose module is not loaded yet fails)
+        hipFuncAttributes fa;
+        (void)hipFuncGetAttributes(&fa, kern);
+        if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, pl.lds) == hipSuccess) {
+            lds_set[dev].store(pl.lds, std::memory_order_relaxed);
+        } else if (std::getenv("FATTN_DEBUG")) {
+            std::fprintf(stderr, "fattn: hipFuncSetAttribute(%d B LDS) failed; launching anyway\n", pl.lds);
+        }
+        (void)hipGetLastError();
+    }
+    if (ev.begin) (void)hipEventRecord(ev.begin, st);
+    go();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        if (std::getenv("FATTN_DEBUG"))
+            std::fprintf(stderr, "fattn: launch grid (%u,%u,%u) lds %d failed: %s\n", pl.grid.x, pl.grid.y, pl.grid.z,
+                         pl.lds, hipGetErrorString(e));
+        return FATTN_ERR_LAUNCH;
+    }
+    if (ev.end) (void)hipEventRecord(ev.end, st);
+    return FATTN_OK;
+}
+
+template <int KT, int VT, int D, int GRAN, bool HM, int NWV, int EPI>
+int launch_split_e(const Plan& pl, hipStream_t st, const Events& ev) {
+    auto kern = fattn_split_kernel<KT, VT, D, GRAN, HM, NWV, EPI>;
+    return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        hipLaunchKernelGGL(kern, pl.grid, dim3(NWV * kWave), pl.lds, st, pl.a);
+    });
+}
+
+// the plan's epilogue (a.wave_merge): 1 only for 4 waves at D = 128
+template <int KT, int VT, int D, int GRAN, bool HM, int NWV>
+int launch_split_w(const Plan& pl, hipStream_t st, const Events& ev) {
+    if constexpr (NWV == 4 && D == 128) {
+        if (pl.a.wave_merge == 1) return launch_split_e<KT, VT, D, GRAN, HM, NWV, 1>(pl, st, ev);
+    }
+    if (pl.a.wave_merge == 2) return launch_split_e<KT, VT, D, GRAN, HM, NWV, 2>(pl, st, ev);
+    if (pl.a.wave_merge != 0) return FATTN_ERR_INVALID_ARG;
+    return launch_split_e<KT, VT, D, GRAN, HM, NWV, 0>(pl, st, ev);
+}
+
+// 8 / 16 waves per workgroup: the 16-B path only; 16 needs the 4-waves-per-SIMD
+// register budget (split_waves_per_simd); the planner never asks otherwise
+template <int KT, int VT, int D, int GRAN, bool HM>
+int launch_split_hm(const Plan& pl, hipStream_t st, const Events& ev) {
+    if constexpr (GRAN == 16) {
+        if (pl.nwv == 8) return launch_split_w<KT, VT, D, GRAN, HM, 8>(pl, st, ev);
+        if constexpr (split_waves_per_simd<KT, D, GRAN>() == 4) {
+            if (pl.nwv == 16) return launch_split_w<KT, VT, D, GRAN, HM, 16>(pl, st, ev);
+        }
+    }
+    if (pl.nwv != 4) return FATTN_ERR_INVALID_ARG;
+    return launch_split_w<KT, VT, D, GRAN, HM, 4>(pl, st, ev);
+}
+
+template <int KT, int VT, int D, int GRAN>
+int launch_split(const Plan& pl, hipStream_t st, const Events& ev) {
+    return pl.a.has_mask ? launch_split_hm<KT, VT, D, GRAN, true>(pl, st, ev)
+                         : launch_split_hm<KT, VT, D, GRAN, false>(pl, st, ev);
+}
+
+template <int KT, int VT, int D>
+int launch_gran(const Plan& pl, hipStream_t st, const Events& ev) {
+    if constexpr (VT == VT_F16T) {
+        return launch_split<KT, VT, D, 16>(pl, st, ev);
+    } else {
+        return pl.gran == 16 ? launch_split<KT, VT, D, 16>(pl, st, ev) : launch_split<KT, VT, D, 4>(pl, st, ev);
+    }
+}
+
+template <int KT, int D, int NW, bool HM>
+int launch_mq_hm(const Plan& pl, hipStream_t st, const Events& ev) {
+    auto kern = fattn_mq_kernel<KT, D, NW, HM>;
+    return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        hipLaunchKernelGGL(kern, pl.grid, dim3(NW * kWave), pl.lds, st, pl.a);
+    });
+}
+
+template <int KT, int D>
+int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
+    if (pl.nw == 8)
+        return pl.a.has_mask ? launch_mq_hm<KT, D, 8, true>(pl, st, ev) : launch_mq_hm<KT, D, 8, false>(pl, st, ev);
+    return pl.a.has_mask ? launch_mq_hm<KT, D, 4, true>(pl, st, ev) : launch_mq_hm<KT, D, 4, false>(pl, st, ev);
+}
+
+template <int KT, bool HM>
+int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
+    auto kern = fattn_pf_kernel<KT, 128, HM>;
+    return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        if (HM && pl.a.pf_flags)
+            hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,
+                               pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
+        hipLaunchKernelGGL(kern, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
+        if (HM && pl.a.pf_flags) (void)hipMemsetAsync((void*)pl.a.pf_flags, 0, pl.cnt_bytes, st);
+    });
+}
+
+template <int KT>
+int launch_pf(const Plan& pl, hipStream_t st, const Events& ev) {
+    return pl.a.has_mask ? launch_pf_hm<KT, true>(pl, st, ev) : launch_pf_hm<KT, false>(pl, st, ev);
+}
+
+// every kernel of head dim D (defined here, instantiated once per D in
+// fattn_launch_d<D>.hip)
+template <int D>
+int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
+    if constexpr (D == 128) {
+        if (pl.pf) {
+            if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_pf<FATTN_TYPE_F16>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0>(pl, st, ev);
+            return FATTN_ERR_UNSUPPORTED_TYPE;
+        }
+    }
+    if constexpr (D == 64 || D == 128) {
+        if (pl.mq) {
+            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_mq<FATTN_TYPE_Q8_0, D>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_mq<FATTN_TYPE_Q4_0, D>(pl, st, ev);
+            return FATTN_ERR_UNSUPPORTED_TYPE;
+        }
+    }
+    if (pl.pf || pl.mq) return FATTN_ERR_UNSUPPORTED_HEAD_DIM;
+    if constexpr (D % QK == 0) {
+        if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0)
+            return launch_gran<FATTN_TYPE_Q8_0, FATTN_TYPE_Q8_0, D>(pl, st, ev);
+        if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0)
+            return launch_gran<FATTN_TYPE_Q4_0, FATTN_TYPE_Q4_0, D>(pl, st, ev);
+    }
+    if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_gran<FATTN_TYPE_F16, FATTN_TYPE_F16, D>(pl, st, ev);
+    if (pl.kt == FATTN_TYPE_F16 && pl.vt == VT_F16T) return launch_gran<FATTN_TYPE_F16, VT_F16T, D>(pl, st, ev);
+    return FATTN_ERR_UNSUPPORTED_TYPE;
+}
+
+extern template int launch_types<64>(const Plan&, hipStream_t, const Events&);
+extern template int launch_types<128>(const Plan&, hipStream_t, const Events&);
+extern template int launch_types<256>(const Plan&, hipStream_t, const Events&);
+
+}  // namespace fattn

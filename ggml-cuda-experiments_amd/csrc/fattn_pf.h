@@ -631,7 +631,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
 // QPT mask rows has a key above -inf (f16 0xFC00) in KV tile s.  One workgroup
 // per (query tile, KV tile) block; every flag is written on every launch, so
 // the array needs no initialisation.  Reads the mask once (f16 [NQ][N]).
-__global__ __launch_bounds__(256) void pf_mask_flags_kernel(const uint8_t* __restrict__ mask, int64_t m_nb1, int NQ,
+static __global__ __launch_bounds__(256) void pf_mask_flags_kernel(const uint8_t* __restrict__ mask, int64_t m_nb1, int NQ,
                                                             int QPT, int ntiles, uint8_t* __restrict__ flags) {
     const int s = blockIdx.x, qt = blockIdx.y;
     // thread -> (row qt*QPT + r, 16-B piece pc of the tile's 128 B): 8 pieces per row

@@ -25,7 +25,7 @@ __device__ __forceinline__ float opaque(float x) {
     return x;
 }
 
-__global__ __launch_bounds__(256) void dequant_q8_0_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst,
+static __global__ __launch_bounds__(256) void dequant_q8_0_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst,
                                                            int64_t nblocks) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nblocks) return;
@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void dequant_q8_0_kernel(const uint8_t* __rest
     }
 }
 
-__global__ __launch_bounds__(256) void dequant_q4_0_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst,
+static __global__ __launch_bounds__(256) void dequant_q4_0_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst,
                                                            int64_t nblocks) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nblocks) return;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void dequant_q4_0_kernel(const uint8_t* __rest
     }
 }
 
-__global__ __launch_bounds__(256) void dequant_f16_kernel(const uint16_t* __restrict__ src, float* __restrict__ dst,
+static __global__ __launch_bounds__(256) void dequant_f16_kernel(const uint16_t* __restrict__ src, float* __restrict__ dst,
                                                           int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;

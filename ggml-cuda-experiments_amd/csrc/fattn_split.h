@@ -82,10 +82,13 @@ struct SplitArgs {
     int pf_stagger;     // prefill kernel: SIMD partner waves run their phases staggered
     const uint8_t* pf_flags;  // prefill: [n_qt][N/64] live-block flags (pf_mask_flags_kernel), or null
     int split_prio;     // split kernel wave priorities: 0 staggered 3/2/1/0, 1 none, 2 staggered while issuing
-    int wave_merge;     // split kernel, one-row tiles: every wave publishes its own partial and
-                        // the last-arriving WAVE merges them (no LDS merge, no barriers)
-    int dec_diag;       // fattn_dec_kernel diagnostics: 1 = no compute, 2 = no DMA (never in the product path)
-    int dec_ahead;      // fattn_dec_kernel: steps in flight per loader wave (capped by vmcnt)
+    int wave_merge;     // split kernel epilogue: 0 = LDS merge of the waves + combine_tile;
+                        // 1 = one-row tiles: every wave publishes its own partial and the
+                        // last-arriving WAVE merges them (no LDS merge, no barriers);
+                        // 2 = one-row tiles: LDS merge, then one partial per workgroup
+                        // (wg_row_merge)
+    int issue_lag;      // split kernel: 1 = issue step s + nbuf - 1 once step s has landed (one step in
+                        // flight beside the compute), 0 = refill a buffer once its step is computed
 };
 
 template <int KT, int VT, int D>
@@ -459,20 +462,21 @@ __device__ __forceinline__ int tile_rows(const SplitArgs& a, int qt, int hs) {
 }
 
 // ---------------------------------------------------------------- diagnostics
-// Diagnostic build only (-DFATTN_STAMPS, libfattn_stamps.so): lane 0 of every
-// wave records s_memrealtime (100 MHz) at phase boundaries into g_stamps
-// [block][wave][16]: 0 start, 1 first steps issued, 2+s data of step s in LDS
-// (s < 8), 10 loop done, 11 4-wave merge done, 12 partial published (or output
-// stored), 13 tile merge done (last workgroup).  No stamp executes in
-// the product library.
+// Diagnostic build only (-DFATTN_STAMPS, libfattn_stamps.so, tools/stamps.py):
+// lane 0 of every wave records s_memrealtime (100 MHz) at phase boundaries into
+// g_stamps[block][16 wave slots][16]: 0 start, 1 first steps issued, 2+s data of
+// step s in LDS (s < 8), 10 loop done, 11 waves merged (LDS), 12 partial
+// published and drained, 14 arrival atomic returned, 15 merger's loads in,
+// 13 tile merged and stored (merging wave).  No stamp executes in the product
+// library.
 #ifdef FATTN_STAMPS
-__device__ unsigned long long* g_stamps;
+static __device__ unsigned long long* g_stamps;  // one per translation unit (fattn_launch_d*.hip)
 #define FATTN_STAMP(k)                                                                          \
     do {                                                                                        \
         if (lane == 0 && g_stamps) {                                                            \
             const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                     \
             const int64_t blk_ = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
-            g_stamps[(blk_ * kSplitWaves + wave) * 16 + (k)] = t_;                                \
+            g_stamps[(blk_ * 16 + wave) * 16 + (k)] = t_;                                \
         }                                                                                       \
     } while (0)
 // any lane: slot k of wave 0's record = max(slot, v)
@@ -480,22 +484,12 @@ __device__ unsigned long long* g_stamps;
     do {                                                                                        \
         if (g_stamps) {                                                                         \
             const int64_t blk_ = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
-            atomicMax(&g_stamps[blk_ * kSplitWaves * 16 + (k)], (unsigned long long)(v));      \
-        }                                                                                       \
-    } while (0)
-// fattn_dec_kernel: [block][8 waves][16] (tools/dec_stamps.py)
-#define FATTN_STAMP8(k)                                                                         \
-    do {                                                                                        \
-        if (lane == 0 && g_stamps) {                                                            \
-            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                     \
-            const int64_t blk_ = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
-            g_stamps[(blk_ * 8 + wave) * 16 + (k)] = t_;                                        \
+            atomicMax(&g_stamps[blk_ * 16 * 16 + (k)], (unsigned long long)(v));      \
         }                                                                                       \
     } while (0)
 #else
 #define FATTN_STAMP(k) do { } while (0)
 #define FATTN_STAMP_MAX(k, v) do { } while (0)
-#define FATTN_STAMP8(k) do { } while (0)
 #endif
 
 // ---------------------------------------------------------------- kernel
@@ -543,12 +537,12 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
         if (g == 0) st_sc1_x2(a.ws_ml + 2 * (tile * NP + part), u32x2{bits(m_run), bits(l_tot)});
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FATTN_STAMP8(10);
+    FATTN_STAMP(12);
     uint32_t* cnt = a.ws_cnt + tile * kCntStride;
     uint32_t old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __builtin_amdgcn_readfirstlane(old);
-    FATTN_STAMP8(11);
+    FATTN_STAMP(14);
     if (old != (uint32_t)(NP - 1)) return;
     if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---- merge: lane half h = lane / 32 takes the parts of parity h, dims
@@ -572,7 +566,7 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
     uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8 + 4));  //          l of part p
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FATTN_STAMP8(12);
+    FATTN_STAMP(15);
     reg_fence(mlm);
     reg_fence(mll);
     fence();
@@ -607,17 +601,202 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + d4;
     const float inv = L == 0.0f ? __builtin_nanf("") : 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
     *(f32x4*)out = acc * inv;
-    FATTN_STAMP8(13);
+    FATTN_STAMP(13);
 }
 
-// Tail of a split-KV workgroup: the compute waves' (O, m, l) states merge --
-// through the last-arriving wave (one-row tiles, wave_merge) or through LDS
-// (wave w's image at smem + w * region) and then across the tile's chunks via
-// the last-arriving workgroup (combine_tile).  `active`: this wave holds a
-// state (fattn_dec_kernel's loader waves do not, and only join the barriers;
-// waves >= NW must be inactive).  `sync_first`: the images alias
-// step buffers, so wait for every wave before writing them.
-template <int KT, int VT, int D, int NW = kSplitWaves>
+// Log-sum-exp merge of NP <= 64 one-row partials of a tile: O rows [NP][D]
+// f32 and (m in log2 units, l) pairs [NP][2], written write-through by other
+// workgroups of this launch (sc1 loads: first row of the hand-off table,
+// MI355X_MICROARCH.md).  One wave: lane (h, dl) = (lane / (D/4), lane % (D/4))
+// loads 16 B of every part p = h (mod 64 / (D/4)); every load of a batch is
+// issued before one wait; the lane groups meet by permlane swaps.  Fixed
+// order (deterministic).  `out` = the tile's dst row.  fa_reduce math,
+// src/flash_row_float.h:415-472, in fp32.
+template <int D>
+__device__ __forceinline__ void merge_row_parts(const float* parts_o, const float* parts_ml, int NP, float* out,
+                                                int lane) {
+    constexpr float kNegInf = -__builtin_inff();
+    constexpr int LPP = D / 4;     // lanes per part
+    constexpr int PPR = 64 / LPP;  // parts per lane row (1, 2, 4)
+    constexpr int kIt = 16;        // loads per lane per round trip
+    const int h = lane / LPP, d4 = 4 * (lane % LPP);
+    const i32x4 osrd = make_srd(parts_o, (uint32_t)(NP * D * 4));
+    const i32x4 msrd = make_srd(parts_ml, (uint32_t)(NP * 8));
+    u32x4 v[kIt];
+    auto issue = [&](int p0) {
+#pragma unroll
+        for (int i = 0; i < kIt; i++) v[i] = ld_sc1_buf(osrd, (uint32_t)(((p0 + PPR * i + h) * D + d4) * 4));
+    };
+    auto fence = [&] {
+#pragma unroll
+        for (int i = 0; i < kIt; i++) reg_fence(v[i]);
+    };
+    issue(0);
+    uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
+    uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8 + 4));  //          l of part p
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    reg_fence(mlm);
+    reg_fence(mll);
+    fence();
+    const float mp = lane < NP ? __builtin_bit_cast(float, mlm) : kNegInf;
+    const float M = seg_reduce<true>(mp, 64);
+    const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M);
+    const float L = seg_reduce<false>(lane < NP ? w * __builtin_bit_cast(float, mll) : 0.0f, 64);
+    const int wi = __builtin_bit_cast(int, w);
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int p0 = 0; p0 < NP; p0 += kIt * PPR) {  // wave-uniform
+        if (p0 > 0) {
+            issue(p0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            fence();
+        }
+#pragma unroll
+        for (int i = 0; i < kIt; i++) {
+            float wp = 0.0f;
+#pragma unroll
+            for (int j = 0; j < PPR; j++) {
+                const float wj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(wi, (p0 + PPR * i + j) & 63));
+                wp = (h == j) ? wj : wp;
+            }
+            acc += wp * __builtin_bit_cast(f32x4, v[i]);
+        }
+    }
+    if constexpr (PPR == 4) {
+        acc.x = xor16_pair(acc.x, false);
+        acc.y = xor16_pair(acc.y, false);
+        acc.z = xor16_pair(acc.z, false);
+        acc.w = xor16_pair(acc.w, false);
+    }
+    if constexpr (PPR >= 2) {
+        acc.x = xor32_pair(acc.x, false);
+        acc.y = xor32_pair(acc.y, false);
+        acc.z = xor32_pair(acc.z, false);
+        acc.w = xor32_pair(acc.w, false);
+    }
+    if (h) return;
+    const float inv = L == 0.0f ? __builtin_nanf("") : 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
+    *(f32x4*)(out + d4) = acc * inv;
+}
+
+// One-row tiles, NW waves per workgroup: every wave writes its row-0 state
+// (O, m, l) into its own LDS region (its steps have all landed), one barrier,
+// then wave 0 merges the NW states (lane (h, dl): states p = h mod PPR, dims
+// 4dl..4dl+3, one ds_read_b128 each).  With one chunk it writes dst; with
+// several it publishes the workgroup's row write-through, drains, counts the
+// workgroup on the tile's arrival word, and the last workgroup's wave 0 merges
+// the chunks (merge_row_parts).  The cross-workgroup hand-off carries one row
+// per workgroup instead of one per wave.
+template <int D, bool VQ8, int NW>
+__device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o)[D / 16], float m_run, float l_tot,
+                                             int chunk, int wave, int lane, int qt, int hs, int ik2, int iq3,
+                                             uint8_t* smem, int region) {
+    constexpr int NB = D / QK;
+    constexpr int NC = D / 16;
+    constexpr float kNegInf = -__builtin_inff();
+    constexpr int LPP = D / 4;
+    constexpr int PPR = 64 / LPP;
+    const int g = lane >> 4, m = lane & 15;
+    float* so = (float*)(smem + wave * region);  // [D] O row, then (m, l)
+    if (m == 0) {  // column 0 = the tile's row; its dims sit on lanes 0, 16, 32, 48
+        if constexpr (VQ8) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                const f32x4 e = o[2 * b], od = o[2 * b + 1];
+                *(f32x4*)(so + 32 * b + 8 * g) = f32x4{e.x, od.x, e.y, od.y};
+                *(f32x4*)(so + 32 * b + 8 * g + 4) = f32x4{e.z, od.z, e.w, od.w};
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < NC; c++) *(f32x4*)(so + 16 * c + 4 * g) = o[c];
+        }
+        if (g == 0) *(f32x2*)(so + D) = f32x2{m_run, l_tot};
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    FATTN_STAMP(11);
+    // ---- wave 0: merge the NW states
+    const int h = lane / LPP, d4 = 4 * (lane % LPP);
+    const f32x2 ml = lane < NW ? *(const f32x2*)((const float*)(smem + lane * region) + D) : f32x2{kNegInf, 0.0f};
+    const float M = seg_reduce<true>(ml.x, 64);
+    const float w = (ml.x == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(ml.x - M);
+    const float L = seg_reduce<false>(w * ml.y, 64);
+    const int wi = __builtin_bit_cast(int, w);
+    constexpr int NI = (NW + PPR - 1) / PPR;
+    f32x4 part[NI];
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        const int p = PPR * i + h;
+        part[i] = p < NW ? *(const f32x4*)((const float*)(smem + p * region) + d4) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        float wp = 0.0f;
+#pragma unroll
+        for (int j = 0; j < PPR; j++) {
+            const float wj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(wi, (PPR * i + j) & 63));
+            wp = (h == j && PPR * i + j < NW) ? wj : wp;
+        }
+        acc += wp * part[i];
+    }
+    if constexpr (PPR == 4) {
+        acc.x = xor16_pair(acc.x, false);
+        acc.y = xor16_pair(acc.y, false);
+        acc.z = xor16_pair(acc.z, false);
+        acc.w = xor16_pair(acc.w, false);
+    }
+    if constexpr (PPR >= 2) {
+        acc.x = xor32_pair(acc.x, false);
+        acc.y = xor32_pair(acc.y, false);
+        acc.z = xor32_pair(acc.z, false);
+        acc.w = xor32_pair(acc.w, false);
+    }
+    const int riq1 = qt * a.QPT;
+    const int riq2 = ik2 * a.rk2 + hs * a.R;
+    float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D;
+    if (a.n_chunks == 1) {
+        if (h == 0) {
+            const float inv = L == 0.0f ? __builtin_nanf("") : 1.0f / L;
+            *(f32x4*)(out + d4) = acc * inv;
+        }
+        return;
+    }
+#ifdef FATTN_DIAG_NOPUBLISH
+    if (acc.x == 12345.0f) a.dst[0] = L;  // diagnostic build only: stop after the workgroup merge
+    return;
+#endif
+    const int64_t tile = (int64_t)iq3 * gridDim.y + blockIdx.y;
+    float* po = a.ws_o + (tile * a.n_chunks + chunk) * D;
+    auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
+    if (h == 0) st_sc1(po + d4, u32x4{bits(acc.x), bits(acc.y), bits(acc.z), bits(acc.w)});
+    if (lane == 0) st_sc1_x2(a.ws_ml + 2 * (tile * a.n_chunks + chunk), u32x2{bits(M), bits(L)});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FATTN_STAMP(12);
+#ifdef FATTN_DIAG_NOATOMIC
+    return;  // diagnostic build only: stop after the published row drained
+#endif
+    uint32_t* cnt = a.ws_cnt + tile * kCntStride;
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    FATTN_STAMP(14);
+    if (old != (uint32_t)(a.n_chunks - 1)) return;
+    if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    merge_row_parts<D>(a.ws_o + tile * a.n_chunks * D, a.ws_ml + 2 * tile * a.n_chunks, a.n_chunks, out, lane);
+    FATTN_STAMP(13);
+}
+
+// Tail of a split-KV workgroup: the waves' (O, m, l) states merge.  EPI (the
+// plan's a.wave_merge, a template parameter so that each kernel carries only
+// its own epilogue's registers -- combine_tile's in-flight loads made the
+// whole kernel spill): 0 = through LDS (wave w's image at smem + w * region)
+// and then across the tile's chunks via the last-arriving workgroup
+// (combine_tile); 1 = one-row tiles, every wave publishes and the
+// last-arriving wave merges (wave_merge_epilogue); 2 = one-row tiles, LDS
+// merge and one published row per workgroup (wg_row_merge).  `active`: this
+// wave holds a state (waves >= NW must be inactive).  `sync_first`: the images
+// alias step buffers, so wait for every wave before writing them.
+template <int KT, int VT, int D, int NW, int EPI>
 __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D / 16], float m_run, float l_run,
                                                float (&corr)[D / QK], int wave, int lane, int qt, int hs, int ik2,
                                                int iq3, int y, int chunk, uint8_t* smem, int region, bool active,
@@ -631,10 +810,6 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
     constexpr float kVOff = kVQ8 ? 1152.0f : 1032.0f;
     const int g = lane >> 4;
     const int m = lane & 15;
-    // ---- per-wave state -> LDS (this wave's own region), then merge the 4 waves
-    if (!active) {  // loader waves (fattn_dec_kernel): no state; they only join the barriers
-        if (a.n_chunks > 1 && a.wave_merge && D == 128) return;
-    }
     // split_step keeps the reference max in natural units; the merges work in log2
     m_run = m_run == kNegInf ? kNegInf : m_run * 1.4426950408889634f;
     const float l_tot = grp4_sum(l_run);
@@ -647,11 +822,13 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
             o[2 * b + 1] -= cb;
         }
     }
-    if constexpr (D == 128) {
-        if (a.wave_merge) {
-            wave_merge_epilogue<D, kVQ8, NW>(a, o, m_run, l_tot, chunk, wave, lane, qt, hs, ik2, iq3);
-            return;
-        }
+    if constexpr (EPI == 1) {
+        static_assert(D == 128, "per-wave merge: lane i <-> dims 2i, 2i+1");
+        wave_merge_epilogue<D, kVQ8, NW>(a, o, m_run, l_tot, chunk, wave, lane, qt, hs, ik2, iq3);
+        return;
+    } else if constexpr (EPI == 2) {
+        wg_row_merge<D, kVQ8, NW>(a, o, m_run, l_tot, chunk, wave, lane, qt, hs, ik2, iq3, smem, region);
+        return;
     }
     constexpr int MS = C::kMergeStride;
     // the merge images alias step buffers other waves may still be reading
@@ -941,8 +1118,19 @@ __device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* bu
 
 }
 
-template <int KT, int VT, int D, int GRAN, bool HM>
-__global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || D == 256) ? 2 : 4) void fattn_split_kernel(
+// waves per SIMD the split kernel's register budget allows (__launch_bounds__)
+template <int KT, int D, int GRAN>
+constexpr int split_waves_per_simd() {
+    return (KT == FATTN_TYPE_F16 || GRAN == 4 || D == 256) ? 2 : 4;
+}
+
+// NWV waves per workgroup (4, 8 or 16), each streaming its own slice of the
+// chunk.  More waves per CU put more LDS-DMA instructions in flight from more
+// issuing waves (tools/hbm_probe: a 35.7 MB read takes 8.3 us from 256 4-wave
+// workgroups, 6.4 us from 16 waves per CU) and let the SIMDs interleave the
+// steps' dependent LDS -> VALU -> MFMA chains.
+template <int KT, int VT, int D, int GRAN, bool HM, int NWV, int EPI>
+__global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || D == 256) ? 2 : 4) void fattn_split_kernel(
     const SplitArgs a) {
     using C = SplitCfg<KT, VT, D>;
     using P = StepPlan<KT, VT, D, GRAN>;
@@ -984,7 +1172,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     const bool row_ok = (m < a.QPT * a.R) && (iq1 < a.NQ) && (mh < a.rk2);
 
     // ---- this wave's KV slice
-    const int wl = a.chunk_len / kSplitWaves;
+    const int wl = a.chunk_len / NWV;
     const int c_hi = min(a.N, (chunk + 1) * a.chunk_len);
     const int w_lo = chunk * a.chunk_len + wave * wl;
     const int w_hi = min(c_hi, w_lo + wl);
@@ -1003,8 +1191,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     // all compute starts late; by priority the first waves' steps land first
     // and their compute overlaps the rest of the stream.
     // (split_prio 1: no priorities; 2: staggered only while the first steps issue)
+    // (NWV > 4: by the wave's rank among the waves of its SIMD, wave / 4)
     if (a.split_prio != 1) {
-        switch (__builtin_amdgcn_readfirstlane(wave)) {
+        switch (__builtin_amdgcn_readfirstlane(NWV == 4 ? wave : wave >> 2)) {
             case 0: __builtin_amdgcn_s_setprio(3); break;
             case 1: __builtin_amdgcn_s_setprio(2); break;
             case 2: __builtin_amdgcn_s_setprio(1); break;
@@ -1028,13 +1217,17 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
             qraw[b][1] = ld_buf(qs, qoff + 128 * b + 16);
         }
     }
-    for (int s = 0; s < nbuf && s < nsteps; s++) {
+    // issue_lag: the next step is issued when the current one has landed (one
+    // step in flight beside the compute) instead of when its buffer is free
+    const int lag = (a.issue_lag && nbuf > 1) ? 1 : 0;
+    const int pro = min(nbuf - lag, nsteps);  // steps issued before the loop
+    for (int s = 0; s < pro; s++) {
         issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + s * kStep, mrow0, wbuf + s * C::stepBytes, lane);
     }
 
     FATTN_STAMP(1);
     if (a.split_prio == 2) __builtin_amdgcn_s_setprio(0);
-    wait_steps<NI>(min(nbuf, nsteps));  // Q landed (the steps issued after it may fly on)
+    wait_steps<NI>(pro);  // Q landed (the steps issued after it may fly on)
     f16x8 qop[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) {
@@ -1058,14 +1251,22 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
 
     int cur = 0;  // buffer of step s
     for (int s = 0; s < nsteps; s++) {
-        const int ahead = min(nbuf - 1, nsteps - 1 - s);  // steps issued after step s
+        int ahead = min(nbuf - 1 - lag, nsteps - 1 - s);  // steps issued after step s
         // K and mask of step s landed (its V and the later steps may fly on)
         wait_steps_plus<NI, P::NIV>(ahead);
         if (s < 8) FATTN_STAMP(2 + s);
+        if (lag && s + nbuf - 1 < nsteps) {
+            // the buffer of step s - 1 (its LDS reads retired) takes step s + nbuf - 1
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const int nb = cur == 0 ? nbuf - 1 : cur - 1;
+            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf - 1) * kStep, mrow0, wbuf + nb * C::stepBytes,
+                                            lane);
+            ahead++;
+        }
 #ifdef FATTN_DIAG_NOCOMPUTE
         // diagnostic build only: memory-side ceiling of this access pattern
         wait_steps<NI>(ahead);
-        if (s + nbuf < nsteps) {
+        if (!lag && s + nbuf < nsteps) {
             issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf) * kStep, mrow0,
                                             wbuf + cur * C::stepBytes, lane);
         }
@@ -1077,7 +1278,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
                                   l_run, o, corr, [&] { wait_steps<NI>(ahead); });
 
         // -- refill this buffer with step s + nbuf
-        if (s + nbuf < nsteps) {
+        if (!lag && s + nbuf < nsteps) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf) * kStep, mrow0,
                                             wbuf + cur * C::stepBytes, lane);
@@ -1096,8 +1297,8 @@ __global__ __launch_bounds__(kSplitWaves * kWave, (KT == FATTN_TYPE_F16 || GRAN 
     return;
 #endif
     FATTN_STAMP(10);
-    split_epilogue<KT, VT, D>(a, o, m_run, l_run, corr, wave, lane, qt, hs, ik2, iq3, y, chunk, smem, a.wave_bytes, true,
-                              false);
+    split_epilogue<KT, VT, D, NWV, EPI>(a, o, m_run, l_run, corr, wave, lane, qt, hs, ik2, iq3, y, chunk, smem, a.wave_bytes,
+                                   true, false);
 }
 
 // ---------------------------------------------------------------- combine

@@ -54,6 +54,8 @@ OPT_DEC_LOADERS = 15
 OPT_DEC_COMPUTE = 16
 OPT_DEC_DIAG = 17
 OPT_DEC_AHEAD = 18
+OPT_SPLIT_WAVES = 19
+OPT_SPLIT_LAG = 20
 
 
 class FattnError(RuntimeError):

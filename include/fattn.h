@@ -142,14 +142,17 @@ enum {
                                        1 = no pre-pass (every tile fetched; all -inf wave blocks still skipped) */,
     FATTN_OPT_MQ_MIN_ROWS = 13,     /* multi-query kernel only from this many packed (query x head) rows per kv
                                        head (default 256, minimum 32); fewer rows take the split-KV kernel */
-    FATTN_OPT_DEC = 14,             /* split-KV decode: 0 = auto, 1 = fattn_split_kernel (default), 2 = the
-                                       loader-wave kernel fattn_dec_kernel where the 16-B row layout allows */
-    FATTN_OPT_DEC_LOADERS = 15,     /* loader waves per fattn_dec_kernel workgroup: 2 (the only value kept) */
-    FATTN_OPT_DEC_COMPUTE = 16,     /* compute waves per fattn_dec_kernel workgroup: 4 (default) or 8 */
-    FATTN_OPT_DEC_DIAG = 17,        /* diagnostics only: 1 = fattn_dec_kernel skips the compute, 2 = skips the
-                                       K/V DMA, 3 = both (results are garbage) */
-    FATTN_OPT_DEC_AHEAD = 18        /* fattn_dec_kernel: 32-position steps in flight per loader wave (1..8,
-                                       default 8; vmcnt caps it at 63 / instructions per step) */
+    FATTN_OPT_DEC = 14,             /* removed (the loader-wave decode kernel measured slower than the split
+                                       kernel); accepted with 0 or 1 only */
+    FATTN_OPT_DEC_LOADERS = 15,     /* removed; accepted with 0 only */
+    FATTN_OPT_DEC_COMPUTE = 16,     /* removed; accepted with 0 only */
+    FATTN_OPT_DEC_DIAG = 17,        /* removed; accepted with 0 only */
+    FATTN_OPT_DEC_AHEAD = 18,       /* removed; accepted with 0 only */
+    FATTN_OPT_SPLIT_WAVES = 19,     /* split kernel waves per workgroup: 0 = auto, 4, 8 or 16 (16-B row path;
+                                       16 needs the Q8_0/Q4_0 register budget, else clamped to 8) */
+    FATTN_OPT_SPLIT_LAG = 20        /* split kernel issue order: -1 = planner, 0 = a buffer is refilled once its
+                                       step is computed, 1 = the next step is issued once the current one has
+                                       landed (with >= 2 buffers: one step in flight beside the compute) */
 };
 int fattn_set_option(int option, int value);
 

@@ -1,7 +1,7 @@
 """GPU parity, round 2: the reference's own fixtures and call sites through the
 HIP path, the head-sharded multi-GPU slices on one GPU, one workspace shared
 by a prefill and a decode, fattn_row at the reference's default GQA shape,
-and the loader-wave decode kernel (fattn_dec.h) on the BASELINE configs.
+and the split kernel at 4, 8 and 16 waves per workgroup on the BASELINE configs.
 
 Bar as in test_gpu_parity.py: attention within 1e-3 normwise relative error
 per output row against the oracle -- here mostly against outputs the
@@ -232,35 +232,41 @@ def test_config4_gqa_head_shard_slices(dev):
     assert attn_rel_err(assemble_heads(torch.stack(parts)).cpu().numpy(), p.oracle()) <= RTOL
 
 
-# ------------------------------------------------------------------ loader-wave decode kernel (fattn_dec.h)
+# ------------------------------------------------------------------ split kernel, 4 / 8 / 16 waves per workgroup
 
-@pytest.fixture(params=[4, 8], ids=["4compute", "8compute"])
-def dec_on(request):
-    fattn.set_option(fattn.OPT_DEC, 2)
-    fattn.set_option(fattn.OPT_DEC_COMPUTE, request.param)
-    yield
-    fattn.set_option(fattn.OPT_DEC, 1)
-    fattn.set_option(fattn.OPT_DEC_COMPUTE, 4)
+@pytest.fixture(params=[(4, 0), (8, 0), (16, 0), (4, 1), (8, 1)], ids=["4waves", "8waves", "16waves", "4waves-lag",
+                                                                       "8waves-lag"])
+def split_waves(request):
+    waves, lag = request.param
+    fattn.set_option(fattn.OPT_SPLIT_WAVES, waves)
+    fattn.set_option(fattn.OPT_SPLIT_LAG, lag)
+    yield request.param
+    fattn.set_option(fattn.OPT_SPLIT_WAVES, 0)
+    fattn.set_option(fattn.OPT_SPLIT_LAG, -1)
 
 
 DEC_CASES = [
     dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0"),                 # config 3
     dict(D=128, NQ=1, H=32, N=2048, kv_type="f16"),                  # config 2
     dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0"),          # config 4
-    dict(D=128, NQ=1, H=8, N=32768, kv_type="q8_0"),                 # long KV: the LDS ring wraps
+    dict(D=128, NQ=1, H=8, N=32768, kv_type="q8_0"),                 # long KV: several steps per wave
+    dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0"),                 # config 5, one GPU's shard
     dict(D=64, NQ=3, H=8, Hkv=2, N=1024, kv_type="q4_0", mask="causal"),
+    dict(D=64, NQ=1, H=16, N=2048, kv_type="q8_0"),
     dict(D=256, NQ=1, H=4, N=1024, kv_type="q8_0"),
+    dict(D=256, NQ=1, H=16, N=2048, kv_type="f16"),
     dict(D=128, NQ=1, H=4, N=512, kv_type="f16", v_trans=True),
     dict(D=128, NQ=2, H=4, N=96, kv_type="q8_0", mask="neginf_blocks", S=2),
+    dict(D=128, NQ=1, H=8, N=1000, kv_type="q8_0", layout="pos"),    # generic-stride path: always 4 waves
 ]
 
 
 @pytest.mark.parametrize("case", DEC_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
-def test_dec_kernel(dev, dec_on, case):
+def test_split_waves(dev, split_waves, case):
     p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
     t = upload(p, dev)
     att = fattn.Attention(*views(p, t), t["dst"], p.scale)
-    assert "fattn_dec_kernel" in att.describe() or p.N * p.S < 128, att.describe()
+    assert "fattn_split_kernel" in att.describe(), att.describe()
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 

@@ -67,6 +67,28 @@ __global__ __launch_bounds__(256) void dma_read(const unsigned char* __restrict_
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// NW waves per workgroup, U pieces (1 KiB) in flight per wave before each wait
+template <int NW, int U>
+__global__ __launch_bounds__(NW * 64) void dma_read_w(const unsigned char* __restrict__ src, size_t per_wg, unsigned* sink) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned char* p = src + blockIdx.x * per_wg;
+    const size_t pieces = per_wg / 1024;
+    unsigned char* wb = lds + wave * U * 1024;
+    unsigned acc = 0;
+    for (size_t i = wave; i < pieces; i += NW * U) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const size_t pc = i + (size_t)u * NW;
+            const size_t off = (pc < pieces ? pc : i) * 1024 + lane * 16;
+            __builtin_amdgcn_global_load_lds((const void*)(p + off), (void*)(wb + u * 1024), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        acc ^= *(const unsigned*)(wb + lane * 4);
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 template <typename K>
 static float time_it(K launch, int L) {
     hipEvent_t a, b;
@@ -111,6 +133,26 @@ int main(int argc, char** argv) {
                "dma U4 %6.2f us %6.0f GB/s | dma U8 %6.2f us %6.0f GB/s | dma U16 %6.2f us %6.0f GB/s\n",
                wgs, per, t_v4, bytes / t_v4 * 1e-3, t_v8, bytes / t_v8 * 1e-3, t_d4, bytes / t_d4 * 1e-3, t_d8,
                bytes / t_d8 * 1e-3, t_d16, bytes / t_d16 * 1e-3);
+    }
+    // 256 workgroups of NW waves (one per CU): U pieces in flight per wave
+    {
+        const int wgs = 256;
+        const size_t per = (B / wgs) / 1024 * 1024;
+        const double bytes = (double)per * wgs;
+        auto w16u2 = [&](int i) { hipLaunchKernelGGL((dma_read_w<16, 2>), dim3(wgs), dim3(1024), 16 * 2 * 1024, 0, bufs[i % R], per, sink); };
+        auto w16u4 = [&](int i) { hipLaunchKernelGGL((dma_read_w<16, 4>), dim3(wgs), dim3(1024), 16 * 4 * 1024, 0, bufs[i % R], per, sink); };
+        auto w16u9 = [&](int i) { hipLaunchKernelGGL((dma_read_w<16, 9>), dim3(wgs), dim3(1024), 16 * 9 * 1024, 0, bufs[i % R], per, sink); };
+        auto w8u4 = [&](int i) { hipLaunchKernelGGL((dma_read_w<8, 4>), dim3(wgs), dim3(512), 8 * 4 * 1024, 0, bufs[i % R], per, sink); };
+        auto w8u8 = [&](int i) { hipLaunchKernelGGL((dma_read_w<8, 8>), dim3(wgs), dim3(512), 8 * 8 * 1024, 0, bufs[i % R], per, sink); };
+        auto w8u17 = [&](int i) { hipLaunchKernelGGL((dma_read_w<8, 17>), dim3(wgs), dim3(512), 8 * 17 * 1024, 0, bufs[i % R], per, sink); };
+        CHECK(hipFuncSetAttribute((const void*)dma_read_w<16, 9>, hipFuncAttributeMaxDynamicSharedMemorySize, 16 * 9 * 1024));
+        CHECK(hipFuncSetAttribute((const void*)dma_read_w<8, 17>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 17 * 1024));
+        const float a1 = time_it(w16u2, L), a2 = time_it(w16u4, L), a3 = time_it(w16u9, L);
+        const float b1 = time_it(w8u4, L), b2 = time_it(w8u8, L), b3 = time_it(w8u17, L);
+        printf("wgs 256 x 16 waves per_wg %zu B | U2 %6.2f us %6.0f GB/s | U4 %6.2f us %6.0f GB/s | U9 (all) %6.2f us %6.0f GB/s\n",
+               per, a1, bytes / a1 * 1e-3, a2, bytes / a2 * 1e-3, a3, bytes / a3 * 1e-3);
+        printf("wgs 256 x  8 waves per_wg %zu B | U4 %6.2f us %6.0f GB/s | U8 %6.2f us %6.0f GB/s | U17 (all) %6.2f us %6.0f GB/s\n",
+               per, b1, bytes / b1 * 1e-3, b2, bytes / b2 * 1e-3, b3, bytes / b3 * 1e-3);
     }
     // empty-kernel launch floor
     auto e = [&](int i) { hipLaunchKernelGGL(vgpr_read<1>, dim3(1024), dim3(256), 0, 0, (const u32x4*)bufs[i % R], 0, sink); };
