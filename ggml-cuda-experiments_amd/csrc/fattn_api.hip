@@ -84,8 +84,14 @@ Geom geom(int kt, int vt, int D) {
         if (vt == VT_F16T) return geom_of<FATTN_TYPE_F16, VT_F16T, DD>();
         return geom_of<FATTN_TYPE_F16, FATTN_TYPE_F16, DD>();
     };
-    if (D == 256) return pick(std::integral_constant<int, 256>());
-    return D == 128 ? pick(std::integral_constant<int, 128>()) : pick(std::integral_constant<int, 64>());
+    switch (D) {
+        case 64: return pick(std::integral_constant<int, 64>());
+        case 80:  // f16 only (80 is not a whole number of 32-element ggml blocks)
+            return vt == VT_F16T ? geom_of<FATTN_TYPE_F16, VT_F16T, 80>() : geom_of<FATTN_TYPE_F16, FATTN_TYPE_F16, 80>();
+        case 96: return pick(std::integral_constant<int, 96>());
+        case 128: return pick(std::integral_constant<int, 128>());
+        default: return pick(std::integral_constant<int, 256>());
+    }
 }
 
 constexpr int kLdsPerCU = 163840;
@@ -99,9 +105,12 @@ bool combine_ok(int64_t nch, int rv, int D) {
 }
 
 // Split-KV sizing.  A workgroup has nwv waves (4, 8 or 16); every wave streams
-// `spw` steps of 32 positions.  Waves per workgroup follow the steps each CU
-// gets: 16 from 12 steps per CU up, 8 from 6 (the register budget and one step
-// in flight per wave in LDS permitting), else 4.  The grid is sized so that
+// `spw` steps of 32 positions.  One-row tiles (decode without GQA packing) with
+// at least 6 steps per CU take 8 waves per workgroup, one step in flight each
+// (config 3: 8 waves x 2 steps, 11.3 us against 11.8 with 16 waves x 1 step
+// all requested at once, 12.4 with both steps of the 8 waves in flight, 12.6
+// for the 4-wave form; config 2: 8 x 1); multi-row tiles keep 4 waves (config
+// 4: 10.8 vs 11.3 us, config 5 shard 14.6 vs 15.7).  The grid is sized so that
 // all (Y x S x chunks) workgroups are co-resident, limited by LDS (steps in
 // flight) and registers.
 int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t NQ) {
@@ -117,16 +126,16 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
             nwv = g_opt_split_waves;
         } else if (kv_chunk <= 0) {
             const int64_t per_cu = total / pl.cus;
-            nwv = per_cu >= 12 ? 16 : per_cu >= 6 ? 8 : 4;
+            nwv = (rv_max == 1 && per_cu >= 6) ? 8 : 4;
         }
         nwv = std::min(nwv, 4 * wps);
         while (nwv > 4 && G.lds_bytes(1, nwv) > kLdsPerCU) nwv /= 2;
     }
     const int quantum = kStep * nwv;
-    // steps in flight per wave: 2 with 4 waves (the measured optimum of the
-    // 4-wave form); with more waves as many as LDS holds, up to 4
+    // steps in flight per wave: 2 with 4 waves, 1 with more (the measured
+    // optima; more bytes requested at once land later for every wave)
     auto inflight = [&](int spw_) {
-        int nb = std::min(spw_, nwv == 4 ? 2 : 4);
+        int nb = std::min(spw_, nwv == 4 ? 2 : 1);
         while (nb > 1 && G.lds_bytes(nb, nwv) > kLdsPerCU) nb--;
         return nb;
     };
@@ -257,7 +266,8 @@ int make_plan(const fattn_params* p, Plan& pl) {
     const fattn_tensor &q = p->q, &k = p->k, &v = p->v, &mk = p->mask;
     if (q.type != FATTN_TYPE_F32 || q.nb[0] != 4) return FATTN_ERR_UNSUPPORTED_TYPE;
     const int64_t D = q.ne[0];
-    if (D != 64 && D != 128 && D != 256) return FATTN_ERR_UNSUPPORTED_HEAD_DIM;
+    if (D != 64 && D != 80 && D != 96 && D != 128 && D != 256) return FATTN_ERR_UNSUPPORTED_HEAD_DIM;
+    if (D % QK && (k.type != FATTN_TYPE_F16 || v.type != FATTN_TYPE_F16)) return FATTN_ERR_UNSUPPORTED_HEAD_DIM;
     if (k.ne[0] != D || v.ne[0] != D) return FATTN_ERR_INVALID_ARG;
     const int64_t NQ = q.ne[1], H = q.ne[2], S = q.ne[3];
     const int64_t N = k.ne[1], Hkv = k.ne[2], Skv = k.ne[3];
@@ -281,9 +291,8 @@ int make_plan(const fattn_params* p, Plan& pl) {
         if (N % kStep || v.nb[0] % 16 || (uintptr_t)v.data % 16) return FATTN_ERR_BAD_STRIDE;
     }
     if (is_quant(v.type) && v.nb[0] != (int64_t)fattn_row_size(v.type, 32)) return FATTN_ERR_BAD_STRIDE;
-    if (k.nb[1] % 4 || k.nb[2] % 4 || k.nb[3] % 4 || (uintptr_t)k.data % 4) return FATTN_ERR_ALIGNMENT;
+    if (k.nb[1] % 2 || k.nb[2] % 4 || k.nb[3] % 4 || (uintptr_t)k.data % 4) return FATTN_ERR_ALIGNMENT;
     if (v.nb[1] % 2 || v.nb[2] % 4 || v.nb[3] % 4 || (uintptr_t)v.data % 4) return FATTN_ERR_ALIGNMENT;
-    if (!v_trans && v.nb[1] % 4) return FATTN_ERR_ALIGNMENT;
 
     const bool has_mask = mk.data != nullptr;
     if (has_mask) {
@@ -307,6 +316,9 @@ int make_plan(const fattn_params* p, Plan& pl) {
     }
     if (has_mask) g16 = g16 && (uintptr_t)mk.data % 16 == 0 && mk.nb[1] % 16 == 0 && N % kStep == 0;
     if (!g16 && v_trans) return FATTN_ERR_BAD_STRIDE;
+    // the dword-granular path needs dword rows (D = 96 Q8_0 / Q4_0 rows are 102 / 54 B:
+    // contiguous 16-B-aligned caches only)
+    if (!g16 && (k.nb[1] % 4 || (!v_trans && v.nb[1] % 4))) return FATTN_ERR_ALIGNMENT;
 
     SplitArgs& a = pl.a;
     std::memset(&a, 0, sizeof(a));
@@ -352,7 +364,8 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // are packed (R = rk2, a power of two <= 64).
     // (below 256 packed rows per kv head the split kernel measures faster:
     // config 5, 64 rows, 15.5 vs 37.6 us at 4 heads; FATTN_OPT_MQ_MIN_ROWS)
-    const bool mq_ok = !g_opt_mq_disable && is_quant(k.type) && g16 && D <= 128 && NQ * a.rk2 >= 32 && a.rk2 <= 64 &&
+    const bool mq_ok = !g_opt_mq_disable && is_quant(k.type) && g16 && (D == 64 || D == 128) && NQ * a.rk2 >= 32 &&
+                       a.rk2 <= 64 &&
                        (a.rk2 & (a.rk2 - 1)) == 0;
     pl.mq = mq_ok && NQ * a.rk2 >= g_opt_mq_min_rows;
     if (pl.mq) {
@@ -414,10 +427,13 @@ extern "C" {
 #ifdef FATTN_STAMPS
 // diagnostic build only: where the split kernel writes its phase stamps
 int fattn_debug_set_stamps_d64(void*);
+int fattn_debug_set_stamps_d80(void*);
+int fattn_debug_set_stamps_d96(void*);
 int fattn_debug_set_stamps_d128(void*);
 int fattn_debug_set_stamps_d256(void*);
 int fattn_debug_set_stamps(void* dev_ptr) {
-    return fattn_debug_set_stamps_d64(dev_ptr) | fattn_debug_set_stamps_d128(dev_ptr) | fattn_debug_set_stamps_d256(dev_ptr);
+    return fattn_debug_set_stamps_d64(dev_ptr) | fattn_debug_set_stamps_d80(dev_ptr) | fattn_debug_set_stamps_d96(dev_ptr) |
+           fattn_debug_set_stamps_d128(dev_ptr) | fattn_debug_set_stamps_d256(dev_ptr);
 }
 // grid of the plan: out[0..2] = chunks, Y, S
 int fattn_debug_plan(const fattn_params* p, int* out) {
@@ -504,7 +520,7 @@ const char* fattn_strerror(int s) {
         case FATTN_OK: return "ok";
         case FATTN_ERR_INVALID_ARG: return "invalid argument";
         case FATTN_ERR_UNSUPPORTED_TYPE: return "unsupported tensor type";
-        case FATTN_ERR_UNSUPPORTED_HEAD_DIM: return "unsupported head dim (64, 128, 256)";
+        case FATTN_ERR_UNSUPPORTED_HEAD_DIM: return "unsupported head dim (64, 80 (f16 K/V), 96, 128, 256)";
         case FATTN_ERR_BAD_STRIDE: return "unsupported strides / layout";
         case FATTN_ERR_WORKSPACE: return "workspace too small";
         case FATTN_ERR_LAUNCH: return "HIP launch failed";
@@ -576,8 +592,13 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
     Events ev;
     ev.begin = (hipEvent_t)ev_begin;
     ev.end = (hipEvent_t)ev_end;
-    if (pl.D == 256) return launch_types<256>(pl, st, ev);
-    return pl.D == 128 ? launch_types<128>(pl, st, ev) : launch_types<64>(pl, st, ev);
+    switch (pl.D) {
+        case 64: return launch_types<64>(pl, st, ev);
+        case 80: return launch_types<80>(pl, st, ev);
+        case 96: return launch_types<96>(pl, st, ev);
+        case 128: return launch_types<128>(pl, st, ev);
+        default: return launch_types<256>(pl, st, ev);
+    }
 }
 
 int fattn_ext_f16_launch(const void* q, const void* k, const void* v, const void* mask, float* dst, float scale,

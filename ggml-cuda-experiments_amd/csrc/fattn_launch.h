@@ -186,6 +186,8 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
 }
 
 extern template int launch_types<64>(const Plan&, hipStream_t, const Events&);
+extern template int launch_types<80>(const Plan&, hipStream_t, const Events&);
+extern template int launch_types<96>(const Plan&, hipStream_t, const Events&);
 extern template int launch_types<128>(const Plan&, hipStream_t, const Events&);
 extern template int launch_types<256>(const Plan&, hipStream_t, const Events&);
 

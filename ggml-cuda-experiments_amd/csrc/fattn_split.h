@@ -91,6 +91,17 @@ struct SplitArgs {
                         // flight beside the compute), 0 = refill a buffer once its step is computed
 };
 
+// XOR mask of the 16-B chunk swizzle of an LDS row of `cpr` chunks: the largest
+// power of two dividing cpr, minus one, so that chunk ^ (x & mask) stays a
+// bijection on [0, cpr) (cpr = 16 / 8 for D = 128 / 64 f16 rows; 12 and 10 for
+// the D = 96 / 80 rows, whose swizzle works within groups of 4 / 2 chunks)
+__host__ __device__ constexpr int swz_mask(int cpr) { return (cpr & -cpr) - 1; }
+
+// epilogue outputs per thread (16 threads per row): D / 16 where that is a
+// multiple of 4 (D = 64, 128, 256), else 8 with D / 8 threads of the 16 active
+template <int D>
+constexpr int epi_ept() { return (D / 16) % 4 == 0 ? D / 16 : 8; }
+
 template <int KT, int VT, int D>
 struct SplitCfg {
     static constexpr int KTT = KT;
@@ -279,9 +290,9 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs
         uint32_t off;
         if constexpr (KT == FATTN_TYPE_F16) {
             // f16 rows: 16-B chunks XOR-swizzled by row (conflict-free ds_read_b128)
-            constexpr int CPR = C::rowK / 16;
+            constexpr int SW = swz_mask(C::rowK / 16);
             const int row = byte / C::rowK;
-            const int chunk = ((byte % C::rowK) / 16) ^ (row & (CPR - 1));
+            const int chunk = ((byte % C::rowK) / 16) ^ (row & SW);
             off = (uint32_t)(n0 + row) * kn1 + chunk * 16 + (byte & 15);
         } else if constexpr (GRAN == 16) {
             off = (uint32_t)n0 * C::rowK + byte;
@@ -318,9 +329,9 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs
             const int d = byte / (kStep * 2);
             off = (uint32_t)d * (uint32_t)a.v_nb0 + (uint32_t)n0 * 2 + (byte % (kStep * 2));
         } else if constexpr (VT == FATTN_TYPE_F16) {
-            constexpr int CPR = C::rowV / 16;
+            constexpr int SW = swz_mask(C::rowV / 16);
             const int row = byte / C::rowV;
-            const int chunk = ((byte % C::rowV) / 16) ^ (((row & 7) << 1) & (CPR - 1));
+            const int chunk = ((byte % C::rowV) / 16) ^ (((row & 7) << 1) & SW);
             off = (uint32_t)(n0 + row) * vn1 + chunk * 16 + (byte & 15);
         } else if constexpr (GRAN == 16) {
             off = (uint32_t)n0 * C::rowV + byte;
@@ -340,24 +351,31 @@ template <int T, int D>
 struct RowScales {
     uint32_t w[D / QK];
 };
+// whether block b's scale sits in the high half of its dword (rows that are a
+// whole number of dwords); rows that are not (D = 96) read each scale as a u16
+template <int T, int D>
+__host__ __device__ constexpr bool scale_hi(int b) {
+    return row_bytes<T, D>() % 4 == 0 && ((TypeInfo<T>::block_bytes * b) & 2) != 0;
+}
 template <int T, int D>
 __device__ __forceinline__ RowScales<T, D> row_scales(const uint8_t* row) {
     constexpr int BB = TypeInfo<T>::block_bytes;
     RowScales<T, D> s;
 #pragma unroll
-    for (int b = 0; b < D / QK; b++) s.w[b] = *(const uint32_t*)(row + ((BB * b) & ~3));
+    for (int b = 0; b < D / QK; b++) {
+        if constexpr (row_bytes<T, D>() % 4 != 0) s.w[b] = *(const uint16_t*)(row + BB * b);
+        else s.w[b] = *(const uint32_t*)(row + ((BB * b) & ~3));
+    }
     return s;
 }
 template <int T, int D>
 __device__ __forceinline__ uint32_t scale_bits(const RowScales<T, D>& s, int b) {
-    constexpr int BB = TypeInfo<T>::block_bytes;
-    return ((BB * b) & 2) ? (s.w[b] >> 16) : (s.w[b] & 0xffffu);
+    return scale_hi<T, D>(b) ? (s.w[b] >> 16) : (s.w[b] & 0xffffu);
 }
 // block b's f16 scale in both halves, by one v_perm (b is unrolled)
 template <int T, int D>
 __device__ __forceinline__ uint32_t scale_bcast(const RowScales<T, D>& s, int b) {
-    constexpr int BB = TypeInfo<T>::block_bytes;
-    return perm_b32(s.w[b], s.w[b], ((BB * b) & 2) ? 0x03020302u : 0x01000100u);
+    return perm_b32(s.w[b], s.w[b], scale_hi<T, D>(b) ? 0x03020302u : 0x01000100u);
 }
 // f16 pair {scale of row r0, scale of row r1} for block b
 template <int T, int D>
@@ -367,6 +385,20 @@ __device__ __forceinline__ f16x2 scale_pair(const RowScales<T, D>& s0, const Row
     return as_h2(((BB * b) & 2) ? perm_b32(s1.w[b], s0.w[b], 0x07060302u) : perm_b32(s1.w[b], s0.w[b], 0x05040100u));
 }
 
+// 8 bytes at a 2-byte-aligned LDS offset whose alignment is known only at run
+// time (Q8_0 / Q4_0 rows of D = 96: 102 / 54 B, so odd rows start 2 B off a
+// dword): three dword reads and two v_alignbyte with the shift in a VGPR
+__device__ __forceinline__ u32x2 read8_any(const uint8_t* smem, uint32_t off) {
+    const uint32_t base = off & ~3u, sh = off & 3u;
+    const uint32_t w0 = *(const uint32_t*)(smem + base);
+    const uint32_t w1 = *(const uint32_t*)(smem + base + 4);
+    const uint32_t w2 = *(const uint32_t*)(smem + base + 8);
+    u32x2 r;
+    r.x = alignbyte(w1, w0, sh);
+    r.y = alignbyte(w2, w1, sh);
+    return r;
+}
+
 // ---------------------------------------------------------------- operands
 // K operand (A of S^T = K.Q^T) for tile t (16 rows), block/k-step b:
 // lane l -> row 16t + (l&15), elements d = 32b + 8(l>>4) + j.
@@ -374,13 +406,19 @@ template <int KT, int D>
 __device__ __forceinline__ f16x8 k_operand(const uint8_t* kb, int row, int g, int b, uint32_t dbits) {
     if constexpr (KT == FATTN_TYPE_F16) {
         constexpr int CPR = D * 2 / 16;
-        const int chunk = (4 * b + g) ^ (row & (CPR - 1));
-        return *(const f16x8*)(kb + row * (D * 2) + chunk * 16);
+        const int chunk = (4 * b + g) ^ (row & swz_mask(CPR));
+        const f16x8 r = *(const f16x8*)(kb + row * (D * 2) + chunk * 16);
+        if constexpr (D % QK != 0) {  // D = 80: the last k-step's dims past D read as zero
+            if (b == D / QK && 4 * b + g >= CPR) return f16x8{};
+        }
+        return r;
     } else if constexpr (KT == FATTN_TYPE_Q8_0) {
         constexpr int RB = row_bytes<KT, D>();
         const uint32_t base = row * RB + kQ8Bytes * b;
         u32x2 raw;
-        switch ((kQ8Bytes * b + 2) & 7) {  // b is a compile-time constant after unrolling
+        if constexpr (RB % 4 != 0) {
+            raw = read8_any(kb, base + 2 + 8 * g);
+        } else switch ((kQ8Bytes * b + 2) & 7) {  // b is a compile-time constant after unrolling
             case 0: raw = read8_at<0>(kb, base + 2 + 8 * g); break;
             case 2: raw = read8_at<2>(kb, base + 2 + 8 * g); break;
             case 4: raw = read8_at<4>(kb, base + 2 + 8 * g); break;
@@ -398,7 +436,9 @@ __device__ __forceinline__ f16x8 k_operand(const uint8_t* kb, int row, int g, in
         constexpr int RB = row_bytes<KT, D>();
         const uint32_t base = row * RB + kQ4Bytes * b;
         u32x2 raw;
-        switch ((kQ4Bytes * b + 2) & 7) {
+        if constexpr (RB % 4 != 0) {
+            raw = read8_any(kb, base + 2 + 8 * (g & 1));
+        } else switch ((kQ4Bytes * b + 2) & 7) {
             case 0: raw = read8_at<0>(kb, base + 2 + 8 * (g & 1)); break;
             case 2: raw = read8_at<2>(kb, base + 2 + 8 * (g & 1)); break;
             case 4: raw = read8_at<4>(kb, base + 2 + 8 * (g & 1)); break;
@@ -438,8 +478,8 @@ __device__ __forceinline__ f16x8 v_operand_f16(const uint8_t* vb, int c, int g, 
         const int q = i >> 2, p = i & 3;
         const int chunk = 2 * c + (p >> 1);
         const int r0 = 4 * g + q, r1 = 16 + 4 * g + q;
-        const int a0 = r0 * RB + ((chunk ^ (((r0 & 7) << 1) & (CPR - 1))) * 16) + (p & 1) * 8;
-        const int a1 = r1 * RB + ((chunk ^ (((r1 & 7) << 1) & (CPR - 1))) * 16) + (p & 1) * 8;
+        const int a0 = r0 * RB + ((chunk ^ (((r0 & 7) << 1) & swz_mask(CPR))) * 16) + (p & 1) * 8;
+        const int a1 = r1 * RB + ((chunk ^ (((r1 & 7) << 1) & swz_mask(CPR))) * 16) + (p & 1) * 8;
         typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + a0));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + a1));
@@ -616,8 +656,8 @@ template <int D>
 __device__ __forceinline__ void merge_row_parts(const float* parts_o, const float* parts_ml, int NP, float* out,
                                                 int lane) {
     constexpr float kNegInf = -__builtin_inff();
-    constexpr int LPP = D / 4;     // lanes per part
-    constexpr int PPR = 64 / LPP;  // parts per lane row (1, 2, 4)
+    constexpr int LPP = D / 4;                         // lanes per part
+    constexpr int PPR = 64 % LPP == 0 ? 64 / LPP : 1;  // parts per lane row (4, 2, 1; D = 80 / 96: 1)
     constexpr int kIt = 16;        // loads per lane per round trip
     const int h = lane / LPP, d4 = 4 * (lane % LPP);
     const i32x4 osrd = make_srd(parts_o, (uint32_t)(NP * D * 4));
@@ -694,7 +734,7 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
     constexpr int NC = D / 16;
     constexpr float kNegInf = -__builtin_inff();
     constexpr int LPP = D / 4;
-    constexpr int PPR = 64 / LPP;
+    constexpr int PPR = 64 % LPP == 0 ? 64 / LPP : 1;  // (D = 80 / 96: one part per lane row)
     const int g = lane >> 4, m = lane & 15;
     float* so = (float*)(smem + wave * region);  // [D] O row, then (m, l)
     if (m == 0) {  // column 0 = the tile's row; its dims sit on lanes 0, 16, 32, 48
@@ -798,7 +838,7 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
 // alias step buffers, so wait for every wave before writing them.
 template <int KT, int VT, int D, int NW, int EPI>
 __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D / 16], float m_run, float l_run,
-                                               float (&corr)[D / QK], int wave, int lane, int qt, int hs, int ik2,
+                                               float (&corr)[(D + QK - 1) / QK], int wave, int lane, int qt, int hs, int ik2,
                                                int iq3, int y, int chunk, uint8_t* smem, int region, bool active,
                                                bool sync_first) {
     using C = SplitCfg<KT, VT, D>;
@@ -858,10 +898,11 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
     __syncthreads();
     FATTN_STAMP(11);
 
-    constexpr int EPT = D / 16;  // outputs per thread: 16 rows x D over 256 threads
+    constexpr int EPT = epi_ept<D>();  // outputs per thread: 16 rows x D over 256 threads
     const int tm = threadIdx.x / 16;
     const int tj = threadIdx.x % 16;
     const int d0 = tj * EPT;
+    const bool dok = d0 < D;  // (D = 80 / 96: the last threads of a row hold no dims)
     float M = kNegInf;
     float mw[NW], lw[NW];
 #pragma unroll
@@ -880,7 +921,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
         for (int w = 0; w < NW; w++) {
             const float wt = (mw[w] == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mw[w] - M);
             L += wt * lw[w];
-            const float* ow = (const float*)(smem + w * region) + tm * MS + d0;
+            const float* ow = (const float*)(smem + w * region) + tm * MS + (dok ? d0 : 0);
 #pragma unroll
             for (int e = 0; e < EPT; e++) acc[e] += wt * ow[e];
         }
@@ -892,7 +933,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
         return a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D;
     };
     if (a.n_chunks == 1) {
-        if (tm < rv) {
+        if (tm < rv && dok) {
             float* out = dst_row(tm) + d0;
             const float inv = 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
 #pragma unroll
@@ -925,9 +966,12 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
     if (tm < rv) {
         const int64_t slot = (tile * a.n_chunks + chunk) * kRows + tm;
         auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
+        if (dok) {
 #pragma unroll
-        for (int e = 0; e < EPT; e += 4)
-            st_sc1(a.ws_o + slot * D + d0 + e, u32x4{bits(acc[e]), bits(acc[e + 1]), bits(acc[e + 2]), bits(acc[e + 3])});
+            for (int e = 0; e < EPT; e += 4)
+                st_sc1(a.ws_o + slot * D + d0 + e,
+                       u32x4{bits(acc[e]), bits(acc[e + 1]), bits(acc[e + 2]), bits(acc[e + 3])});
+        }
         if (tj == 0) st_sc1_x2(a.ws_ml + 2 * slot, u32x2{bits(M), bits(L)});
     }
     // every storing wave drains: the merging workgroup reads its own partial back too
@@ -959,11 +1003,11 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
 // for the step's V, which it issues last).  `first`: o, l are still zero.
 // Shared by fattn_split_kernel and fattn_dec_kernel (fattn_dec.h).
 template <int KT, int VT, int D, bool HM, typename WaitV>
-__device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* buf, const f16x8 (&qop)[D / QK], int mq,
+__device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* buf, const f16x8 (&qop)[(D + QK - 1) / QK], int mq,
                                            int g, int i16, int nvalid, bool first, float& m_run, float& l_run,
-                                           f32x4 (&o)[D / 16], float (&corr)[D / QK], WaitV&& wait_v) {
+                                           f32x4 (&o)[D / 16], float (&corr)[(D + QK - 1) / QK], WaitV&& wait_v) {
     using C = SplitCfg<KT, VT, D>;
-    constexpr int NB = D / QK;
+    constexpr int NB = (D + QK - 1) / QK;  // k-steps of S^T (D = 80: the last one half zero)
     constexpr int NC = D / 16;
     constexpr float kNegInf = -__builtin_inff();
     constexpr bool kVQ8 = C::VTT == FATTN_TYPE_Q8_0;
@@ -1059,10 +1103,15 @@ __device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* bu
             uint32_t sw[8];
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                sw[r] = *(const uint32_t*)(vb + (rA + r) * C::rowV + ((BB * b) & ~3));
-                sw[4 + r] = *(const uint32_t*)(vb + (rB + r) * C::rowV + ((BB * b) & ~3));
+                if constexpr (C::rowV % 4 != 0) {  // D = 96: rows not a whole number of dwords
+                    sw[r] = *(const uint16_t*)(vb + (rA + r) * C::rowV + BB * b);
+                    sw[4 + r] = *(const uint16_t*)(vb + (rB + r) * C::rowV + BB * b);
+                } else {
+                    sw[r] = *(const uint32_t*)(vb + (rA + r) * C::rowV + ((BB * b) & ~3));
+                    sw[4 + r] = *(const uint32_t*)(vb + (rB + r) * C::rowV + ((BB * b) & ~3));
+                }
             }
-            const uint32_t sel = ((BB * b) & 2) ? 0x07060302u : 0x05040100u;  // b is unrolled
+            const uint32_t sel = scale_hi<C::VTT, D>(b) ? 0x07060302u : 0x05040100u;  // b is unrolled
             const f16x2 d01 = as_h2(perm_b32(sw[1], sw[0], sel)), d23 = as_h2(perm_b32(sw[3], sw[2], sel));
             const f16x2 d45 = as_h2(perm_b32(sw[5], sw[4], sel)), d67 = as_h2(perm_b32(sw[7], sw[6], sel));
             // P'_b = P * d_b (element j <-> row of element j of the A operand)
@@ -1136,7 +1185,7 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     using P = StepPlan<KT, VT, D, GRAN>;
     constexpr int NI = P::NIKV + (HM ? P::NIM : 0);  // VMEM instructions per step
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int NB = D / QK;   // 32-wide k-steps of QK^T (= ggml blocks per row)
+    constexpr int NB = (D + QK - 1) / QK;  // 32-wide k-steps of QK^T (= ggml blocks per row; D = 80: 3)
     constexpr int NC = D / 16;   // 16-wide output column groups (MFMA tiles of O^T)
     constexpr float kNegInf = -__builtin_inff();
     // quantised V: the A operand is the exact integer code plus the magic-number
@@ -1213,8 +1262,10 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
                                      : a.q_span;
 #pragma unroll
         for (int b = 0; b < NB; b++) {
-            qraw[b][0] = ld_buf(qs, qoff + 128 * b);
-            qraw[b][1] = ld_buf(qs, qoff + 128 * b + 16);
+            // (D = 80: dims past D come from past the descriptor, as zeros)
+            const uint32_t qb = (D % QK == 0 || 32 * b + 8 * g < D) ? qoff + 128 * b : a.q_span;
+            qraw[b][0] = ld_buf(qs, qb);
+            qraw[b][1] = ld_buf(qs, qb + 16);
         }
     }
     // issue_lag: the next step is issued when the current one has landed (one
@@ -1317,7 +1368,7 @@ template <int D, int CB>
 __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, int qt, int hs, int ik2, int iq3,
                                              int rv, int row_base, uint8_t* smem) {
     constexpr float kNegInf = -__builtin_inff();
-    constexpr int EPT = D / 16;
+    constexpr int EPT = epi_ept<D>();
     // CB = chunks per load batch: with 8 (the split kernel at D = 128) every
     // thread's partials come in ONE memory round trip up to 8 chunks per thread
     // (config 4: 32 chunks x 4 rows); batch slots past the thread's chunks
@@ -1330,7 +1381,7 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
     const int grp = threadIdx.x / 16, tj = threadIdx.x % 16, d0 = tj * EPT;
     const int64_t sb = tile * NCH;
     const int r = grp / G, cg = grp % G;
-    const bool active = grp < rv * G;
+    const bool active = grp < rv * G && d0 < D;  // (D = 80 / 96: threads past the row's dims idle)
     const int kmax = active ? (NCH - cg + G - 1) / G : 0;
     auto fl = [](uint32_t x) { return __builtin_bit_cast(float, x); };
     // partial loads of chunks cg + (k0 + kk) * G through a buffer descriptor

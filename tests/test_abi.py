@@ -68,13 +68,36 @@ def test_single_chunk_needs_no_workspace():
 
 
 @pytest.mark.parametrize("bad", [
-    dict(D=96), dict(D=80), dict(D=512), dict(H=30, Hkv=8), dict(N=0), dict(kt=fattn.TYPE_F32), dict(kt=5),
+    dict(D=80), dict(D=72, kt=fattn.TYPE_F16), dict(D=112, kt=fattn.TYPE_F16), dict(D=512), dict(H=30, Hkv=8),
+    dict(N=0), dict(kt=fattn.TYPE_F32), dict(kt=5),
 ])
 def test_rejects_invalid(bad):
     p = _params(**bad)
     assert fattn.workspace_size(p) == 0
     with pytest.raises(fattn.FattnError):
         fattn.flash_attn_ext(p, stream=0)
+
+
+@pytest.mark.parametrize("ok", [dict(D=96), dict(D=96, kt=fattn.TYPE_Q4_0), dict(D=96, kt=fattn.TYPE_F16),
+                                dict(D=80, kt=fattn.TYPE_F16)])
+def test_accepts_head_dims_80_96(ok):
+    """D = 96 for every K/V type, D = 80 for f16 K/V (80 is not
+    a whole number of 32-element ggml blocks, so the Q8_0 row above is rejected)."""
+    assert fattn.workspace_size(_params(**ok)) > 0
+
+
+def test_d96_quant_needs_dword_rows():
+    """D = 96 Q8_0 rows are 102 B: a [N][Hkv][row] cache (rows Hkv * 102 B apart,
+    heads 102 B apart) cannot be moved in dwords -> FATTN_ERR_ALIGNMENT."""
+    D, N, Hkv, ptr = 96, 256, 3, 1 << 20
+    rb = fattn.row_size(fattn.TYPE_Q8_0, D)
+    q = fattn.View(ptr, fattn.TYPE_F32, (D, 1, Hkv, 1), (4, Hkv * D * 4, D * 4, Hkv * D * 4))
+    k = fattn.View(ptr, fattn.TYPE_Q8_0, (D, N, Hkv, 1), (34, rb * Hkv, rb, rb * Hkv * N))
+    p = fattn.ext_params(q, k, k, None, ptr, 0.1)
+    assert fattn.workspace_size(p) == 0
+    with pytest.raises(fattn.FattnError) as e:
+        fattn.flash_attn_ext(p, stream=0)
+    assert e.value.code == -7
 
 
 def test_rejects_missing_workspace():
@@ -100,7 +123,8 @@ def test_rejects_null():
 
 def test_row_workspace_size():
     assert fattn.lib().fattn_row_workspace_size(128, 4096, 32) > 0
-    assert fattn.lib().fattn_row_workspace_size(96, 4096, 32) == 0
+    assert fattn.lib().fattn_row_workspace_size(96, 4096, 32) > 0   # head dims 80 / 96 (f16 rows)
+    assert fattn.lib().fattn_row_workspace_size(72, 4096, 32) == 0
 
 
 def test_cpy_rejects_bad_views():

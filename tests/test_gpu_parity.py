@@ -375,6 +375,24 @@ for kt in ("f16", "q8_0", "q4_0"):
     CASES.append(dict(D=256, kv_type=kt, layout="head", NQ=1, H=2, Hkv=2, N=4096, mask="random"))  # chunk merge
 
 
+# head_dims 80 (f16 only) and 96 (the reference's mem_copy
+# experiment pads 80 -> 128, src/flash-matrix.cu:18-65): split-KV kernel, padded-free rows
+# (Q8_0 / Q4_0 rows of D = 96 are 102 / 54 B, not whole dwords: those caches
+# need the contiguous [Hkv][N][row] layout and N % 32 == 0 -- test_abi checks
+# the rejection of the others)
+for D, kts in ((96, ("f16", "q8_0", "q4_0")), (80, ("f16",))):
+    for kt in kts:
+        f16 = kt == "f16"
+        for layout in (("head", "pos") if f16 else ("head",)):
+            CASES.append(dict(D=D, kv_type=kt, layout=layout, NQ=1, H=4, Hkv=4, N=256, mask="random"))
+        CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=1, H=32, Hkv=32, N=4096, mask="random"))  # chunk merge
+        CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=1, H=32, Hkv=8, N=4096, mask="random"))   # GQA tiles
+        CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=9, H=8, Hkv=2, N=300 if f16 else 320, mask="causal"))
+        CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=64, H=4, Hkv=4, N=1024, mask="random"))
+        CASES.append(dict(D=D, kv_type=kt, layout="head", NQ=4, H=2, Hkv=2, N=33 if f16 else 64, mask="random", S=3))
+    CASES.append(dict(D=D, kv_type="f16", layout="head", NQ=1, H=4, Hkv=4, N=512, mask="random", v_trans=True))
+
+
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_sweep(dev, case):
     p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
