@@ -226,7 +226,6 @@ def parse_args(argv=None):
     ap.add_argument("--no-mask", action="store_true", help="no mask tensor (diagnostics; the metric uses a mask)")
     ap.add_argument("--pf-stagger", type=int, default=2)
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
-    ap.add_argument("--pf-pipe", type=int, default=0, help="quantised prefill: 0 auto, 1 lockstep, 2 ping-pong")
     ap.add_argument("--no-mq", action="store_true", help="never pick the multi-query kernel (split-KV kernel only)")
     ap.add_argument("--split-prio", type=int, default=0,
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
@@ -249,7 +248,6 @@ def parse_args(argv=None):
 def apply_options(args):
     import fattn
     opts = [(args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT), (args.pf, fattn.OPT_PF),
-            (args.pf_pipe, fattn.OPT_PF_PIPE),
             (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO),
             (args.waves, fattn.OPT_SPLIT_WAVES)]
     if args.lag >= 0:

@@ -50,7 +50,6 @@ std::atomic<int> g_opt_split_spw{0};
 std::atomic<int> g_opt_split_nbuf{0};
 std::atomic<int> g_opt_pf{0};  // 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_pf_stagger{2};
-std::atomic<int> g_opt_pf_pipe{0};  // FATTN_OPT_PF_PIPE: 0 auto (lockstep), 1 lockstep kernel, 2 ping-pong kernel
 std::atomic<int> g_opt_mq_min_rows{256};  // multi-query kernel from this many packed rows per kv head (>= 32)
 std::atomic<int> g_opt_pf_no_skip{0};     // 1: masked prefill without the live-block pre-pass (FATTN_OPT_PF_SKIP)
 std::atomic<int> g_opt_split_prio{0};     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
@@ -413,7 +412,6 @@ int make_plan(const fattn_params* p, Plan& pl) {
         // re-zeroes them behind the prefill kernel (workspace contract,
         // include/fattn.h: every launch leaves the workspace re-armed).
         pl.pf_flags = has_mask && !g_opt_pf_no_skip;
-        pl.pf2 = is_quant(pl.kt) && g_opt_pf_pipe == 2;  // (measured even with the lockstep kernel so far)
         if (pl.pf_flags) pl.cnt_bytes = ((size_t)a.n_qt * (N / kPfKeys) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes;
         return FATTN_OK;
@@ -486,10 +484,8 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
             g_opt_no_wave_merge = value;
             return FATTN_OK;
-        case FATTN_OPT_PF_PIPE:
-            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
-            g_opt_pf_pipe = value;
-            return FATTN_OK;
+        case FATTN_OPT_PF_PIPE:  // removed experiments: only the lockstep kernel remains
+            return value == 0 || value == 1 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_SPLIT_STEPS:
             if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;
             g_opt_split_spw = value;
@@ -566,8 +562,8 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
     char kern[160];
     const char* hm = pl.a.has_mask ? "mask" : "nomask";
     if (pl.pf)
-        std::snprintf(kern, sizeof kern, "%s%s<%s,D%d,%s>", pl.pf_flags ? "pf_mask_flags_kernel + " : "",
-                      pl.pf2 ? "fattn_pf2_kernel" : "fattn_pf_kernel", tn(pl.kt), pl.D, hm);
+        std::snprintf(kern, sizeof kern, "%sfattn_pf_kernel<%s,D%d,%s>", pl.pf_flags ? "pf_mask_flags_kernel + " : "",
+                      tn(pl.kt), pl.D, hm);
     else if (pl.mq)
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>", tn(pl.kt), pl.D, pl.nw, hm);
     else

@@ -13,7 +13,6 @@
 #include "fattn_quant.h"
 #include "fattn_mq.h"
 #include "fattn_pf.h"
-#include "fattn_pf2.h"
 #include "fattn_split.h"
 
 namespace fattn {
@@ -33,7 +32,6 @@ struct Plan {
     bool mq;  // multi-query kernel (fattn_mq.h)
     bool pf;  // prefill kernel (fattn_pf.h)
     bool pf_flags;          // masked prefill: live-block flags pre-pass (tile-range skipping)
-    bool pf2;               // quantised prefill: SIMD-partner ping-pong schedule (fattn_pf2.h)
     int nw;   // mq kernel: waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
 };
 
@@ -142,9 +140,6 @@ int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
 template <int KT, bool HM>
 int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     auto kern = fattn_pf_kernel<KT, 128, HM>;
-    if constexpr (KT != FATTN_TYPE_F16) {
-        if (pl.pf2) kern = fattn_pf2_kernel<KT, 128, HM>;
-    }
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         if (HM && pl.a.pf_flags)
             hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,

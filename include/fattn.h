@@ -129,9 +129,8 @@ enum {
     FATTN_OPT_PF_DEQUANT = 8        /* quantised prefill: 0 = auto, 1 = dequantise inside the kernel, 2 = convert K/V
                                        to f16 rows in the workspace first (fattn_workspace_size grows by
                                        2 * Skv * Hkv * N * D * 2 bytes; 8 waves only) */,
-    FATTN_OPT_PF_PIPE = 9           /* quantised prefill schedule: 0 = auto, 1 = fattn_pf_kernel (all waves in
-                                       lockstep, one barrier per tile), 2 = fattn_pf2_kernel (SIMD partners
-                                       alternate matrix and vector half-phases) */,
+    FATTN_OPT_PF_PIPE = 9           /* removed prefill schedule experiments (software-pipelined, SIMD-partner
+                                       ping-pong: parity-green, not faster); accepts 0 or 1 only */,
     FATTN_OPT_SPLIT_WAVE_MERGE = 10 /* split kernel, one-row tiles with <= 32 wave partials: 0 = every wave
                                        publishes and the last-arriving wave merges (default), 1 = the
                                        workgroup-level merge used for all other tiles */,

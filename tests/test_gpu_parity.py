@@ -237,16 +237,12 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture(params=[1, 2], ids=["lockstep", "pingpong"])
-def pf_force(request):
-    """The prefill kernel (8 waves x 32 rows) on every eligible problem, in both
-    schedules: fattn_pf_kernel (lockstep) and, for Q8_0 / Q4_0, fattn_pf2_kernel
-    (SIMD-partner ping-pong, fattn_pf2.h)."""
+@pytest.fixture
+def pf_force():
+    """The prefill kernel (fattn_pf.h, 8 waves x 32 rows) on every eligible problem."""
     fattn.set_option(fattn.OPT_PF, 2)
-    fattn.set_option(fattn.OPT_PF_PIPE, request.param)
     yield
     fattn.set_option(fattn.OPT_PF, 0)
-    fattn.set_option(fattn.OPT_PF_PIPE, 0)
 
 
 PF_CASES = [

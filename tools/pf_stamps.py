@@ -20,10 +20,7 @@ ap.add_argument("--n-q", type=int, default=4096)
 ap.add_argument("--kv-len", type=int, default=4096)
 ap.add_argument("--heads", type=int, default=32)
 ap.add_argument("--kv-type", default="q8_0")
-ap.add_argument("--pipe", type=int, default=0, help="FATTN_OPT_PF_PIPE: 1 lockstep, 2 ping-pong")
 args = ap.parse_args()
-if args.pipe:
-    fattn.set_option(fattn.OPT_PF_PIPE, args.pipe)
 dev = torch.device("cuda:0")
 D, H, N, NQ = 128, args.heads, args.kv_len, args.n_q
 typ = fattn.TYPE_NAMES[args.kv_type]
@@ -54,8 +51,7 @@ L.fattn_debug_set_stamps(None)
 s = st.cpu().numpy().reshape(-1, 8, 16)
 s = s[s[:, 0, 8] > 0]
 nt = s[:, :, 8].astype(np.float64)
-names = (["wait+barrier", "dma issue", "dequant", "X: P.V+S^T", "Y: softmax", "-", "-", "-"] if "pf2" in att.describe()
-         else ["wait+barrier", "dma issue", "dequant", "S^T mfma", "softmax", "O^T mfma", "-", "loop tail"])
+names = ["wait+barrier", "dma issue", "dequant", "S^T mfma", "softmax", "O^T mfma", "-", "loop tail"]
 print(att.describe())
 print(f"workgroups {len(s)}  event {e0.elapsed_time(e1) * 1e3:.1f} us  (cycles per tile, mean)")
 for half, sl in (("waves 0-3", slice(0, 4)), ("waves 4-7", slice(4, 8))):
