@@ -230,7 +230,9 @@ def parse_args(argv=None):
     ap.add_argument("--split-prio", type=int, default=0,
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
     ap.add_argument("--waves", type=int, default=0, help="split kernel waves per workgroup (4, 8, 16; 0 = planner)")
-    ap.add_argument("--lag", type=int, default=-1, help="split kernel: 1 = issue the next step once the current landed")
+    ap.add_argument("--no-step-skip", action="store_true", help="split kernel: load and compute every step")
+    ap.add_argument("--mask-live", type=float, default=1.0,
+                    help="diagnostics: mask positions from this fraction of N on to -inf (a padded cache)")
     ap.add_argument("--wave-merge", type=int, default=-1, help="split/dec one-row tiles: 0 per-wave merge, 1 LDS merge")
     ap.add_argument("--prefill-causal", action="store_true",
                     help="causal mask on the prefill measurement (fully masked blocks are skipped)")
@@ -250,8 +252,7 @@ def apply_options(args):
     opts = [(args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT), (args.pf, fattn.OPT_PF),
             (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO),
             (args.waves, fattn.OPT_SPLIT_WAVES)]
-    if args.lag >= 0:
-        fattn.set_option(fattn.OPT_SPLIT_LAG, args.lag)
+    fattn.set_option(fattn.OPT_SPLIT_SKIP, 1 if args.no_step_skip else 0)
     for val, opt in opts:
         if val:
             fattn.set_option(opt, val)
@@ -314,6 +315,8 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
     q = torch.rand((1, NQ, H, D), generator=g, device=dev) * 2 - 1
     npad = (N + 63) // 64 * 64
     mask = (torch.rand((NQ, npad), generator=g, device=dev) * 2 - 1).to(torch.float16)
+    if args.mask_live < 1.0:  # diagnostics: a padded cache, positions past the live fraction -inf
+        mask[:, int(args.mask_live * N):] = float("-inf")
     Hl = sh.n_heads
     outs = torch.empty((R, 1, NQ, Hl, D), dtype=torch.float32, device=dev)
 

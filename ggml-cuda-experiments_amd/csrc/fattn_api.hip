@@ -55,7 +55,7 @@ std::atomic<int> g_opt_pf_no_skip{0};     // 1: masked prefill without the live-
 std::atomic<int> g_opt_split_prio{0};     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
 std::atomic<int> g_opt_no_wave_merge{0};  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
 std::atomic<int> g_opt_split_waves{0};
-std::atomic<int> g_opt_split_lag{-1};  // FATTN_OPT_SPLIT_LAG (-1 = planner)  // split kernel waves per workgroup (FATTN_OPT_SPLIT_WAVES; 0 = auto)
+std::atomic<int> g_opt_split_no_skip{0};  // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -172,7 +172,7 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
         while (nbuf > 1 && G.lds_bytes(nbuf, nwv) > kLdsPerCU) nbuf--;
     }
     pl.nwv = nwv;
-    a.issue_lag = g_opt_split_lag >= 0 ? (int)g_opt_split_lag : 0;
+    a.step_skip = g_opt_split_no_skip ? 0 : 1;
     a.nbuf = nbuf;
     a.split_prio = g_opt_split_prio;
     a.wave_bytes = G.wave_bytes(nbuf);
@@ -497,9 +497,9 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_DEC_AHEAD:
         case FATTN_OPT_DEC_DIAG:
             return value == 0 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
-        case FATTN_OPT_SPLIT_LAG:
-            if (value < -1 || value > 1) return FATTN_ERR_INVALID_ARG;
-            g_opt_split_lag = value;
+        case FATTN_OPT_SPLIT_SKIP:
+            if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_no_skip = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_WAVES:
             if (value != 0 && value != 4 && value != 8 && value != 16) return FATTN_ERR_INVALID_ARG;

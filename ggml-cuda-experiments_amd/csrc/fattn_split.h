@@ -87,7 +87,7 @@ struct SplitArgs {
                         // last-arriving WAVE merges them (no LDS merge, no barriers);
                         // 2 = one-row tiles: LDS merge, then one partial per workgroup
                         // (wg_row_merge)
-    int issue_lag;      // split kernel: 1 = issue step s + nbuf - 1 once step s has landed (one step in
+    int step_skip;      // split kernel: 1 = skip steps whose mask is all -inf for the tile (FATTN_OPT_SPLIT_SKIP)
                         // flight beside the compute), 0 = refill a buffer once its step is computed
 };
 
@@ -1001,7 +1001,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
 // O^T += V^T.P^T.  `buf` is the step's LDS image [K rows | V rows | mask rows];
 // `wait_v()` runs between the softmax and P.V (the split kernel waits there
 // for the step's V, which it issues last).  `first`: o, l are still zero.
-// Shared by fattn_split_kernel and fattn_dec_kernel (fattn_dec.h).
+// Used by fattn_split_kernel.
 template <int KT, int VT, int D, bool HM, typename WaitV>
 __device__ __forceinline__ void split_step(const SplitArgs& a, const uint8_t* buf, const f16x8 (&qop)[(D + QK - 1) / QK], int mq,
                                            int g, int i16, int nvalid, bool first, float& m_run, float& l_run,
@@ -1268,17 +1268,30 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
             qraw[b][1] = ld_buf(qs, qb + 16);
         }
     }
-    // issue_lag: the next step is issued when the current one has landed (one
-    // step in flight beside the compute) instead of when its buffer is free
-    const int lag = (a.issue_lag && nbuf > 1) ? 1 : 0;
-    const int pro = min(nbuf - lag, nsteps);  // steps issued before the loop
+    // ---- -inf step skipping (src/flash-llama.h:275-278), lifted to the DMA:
+    // a step whose mask is -inf for every key of every query row of the tile
+    // adds exp(-inf) = 0 to o and l, so it is neither loaded nor computed.
+    // The mask words of the wave's steps are read here beside Q (their wait is
+    // Q's): one (row, step) pair of 64 B per lane, when the tile's rows x
+    // steps fit the wave.  The prologue's steps are issued regardless.
+    const int pro = min(nbuf, nsteps);  // steps issued before the loop
+    const int n_rows = HM ? min(a.QPT, a.NQ - mrow0) : 0;
+    const bool pre = HM && a.step_skip && nsteps > pro && n_rows * nsteps <= kWave;
+    u32x4 mraw[4] = {};
+    if (pre) {
+        const int r = lane / nsteps, st = lane - r * nsteps;
+        const uint32_t moff = r < n_rows ? (uint32_t)(mrow0 + r) * (uint32_t)a.m_nb1 + (uint32_t)(w_lo + st * kStep) * 2
+                                         : a.m_span;  // past the descriptor: no traffic
+#pragma unroll
+        for (int j = 0; j < 4; j++) mraw[j] = ld_buf(rs.m, moff + 16 * j);
+    }
     for (int s = 0; s < pro; s++) {
         issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + s * kStep, mrow0, wbuf + s * C::stepBytes, lane);
     }
 
     FATTN_STAMP(1);
     if (a.split_prio == 2) __builtin_amdgcn_s_setprio(0);
-    wait_steps<NI>(pro);  // Q landed (the steps issued after it may fly on)
+    wait_steps<NI>(pro);  // Q and the mask words landed (the steps issued after them may fly on)
     f16x8 qop[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) {
@@ -1290,6 +1303,41 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
         h.s4 = (f16)x1.x; h.s5 = (f16)x1.y; h.s6 = (f16)x1.z; h.s7 = (f16)x1.w;
         qop[b] = h;
     }
+    // Steps after the prologue, in issue (= compute) order: the live ones of
+    // steps [pro, 64) as a bit set, then every step from 64 on (not prefetched).
+    uint64_t todo = 0;
+    {
+        const int nb64 = min(nsteps, 64);
+        const uint64_t upto = nb64 == 64 ? ~0ull : (1ull << nb64) - 1;
+        todo = upto & ~((1ull << pro) - 1);
+        if (pre) {
+            constexpr uint32_t kNegInf2 = 0xFC00FC00u;  // two f16 -inf
+            bool lv = false;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                reg_fence(mraw[j]);
+                lv |= (mraw[j].x != kNegInf2) | (mraw[j].y != kNegInf2) | (mraw[j].z != kNegInf2) |
+                      (mraw[j].w != kNegInf2);
+            }
+            const uint64_t bl = __builtin_amdgcn_ballot_w64(lv && lane < n_rows * nsteps);
+            uint64_t live = 0;
+            for (int r = 0; r < n_rows; r++) live |= bl >> (r * nsteps);
+            todo &= live;
+        }
+    }
+    const int n_iter = pro + __builtin_popcountll(todo) + max(0, nsteps - 64);
+    uint64_t i_rem = todo;  // issue side
+    int i_dense = 64;
+    auto next_issue = [&]() -> int {
+        if (i_rem) {
+            const int st = __builtin_ctzll(i_rem);
+            i_rem &= i_rem - 1;
+            return st;
+        }
+        return i_dense++;
+    };
+    uint64_t c_rem = todo;  // compute side (the same sequence, nbuf behind)
+    int c_dense = 64;
 
     float m_run = kNegInf;  // reference max (natural units) of column m
     float l_run = 0.0f;     // this lane's partial row sum
@@ -1300,39 +1348,40 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
 #pragma unroll
     for (int b = 0; b < NB; b++) corr[b] = 0.0f;
 
-    int cur = 0;  // buffer of step s
-    for (int s = 0; s < nsteps; s++) {
-        int ahead = min(nbuf - 1 - lag, nsteps - 1 - s);  // steps issued after step s
-        // K and mask of step s landed (its V and the later steps may fly on)
-        wait_steps_plus<NI, P::NIV>(ahead);
-        if (s < 8) FATTN_STAMP(2 + s);
-        if (lag && s + nbuf - 1 < nsteps) {
-            // the buffer of step s - 1 (its LDS reads retired) takes step s + nbuf - 1
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const int nb = cur == 0 ? nbuf - 1 : cur - 1;
-            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf - 1) * kStep, mrow0, wbuf + nb * C::stepBytes,
-                                            lane);
-            ahead++;
+    int cur = 0;  // buffer of iteration i
+    for (int i = 0; i < n_iter; i++) {
+        int st = i;  // the step of iteration i
+        if (i >= pro) {
+            if (c_rem) {
+                st = __builtin_ctzll(c_rem);
+                c_rem &= c_rem - 1;
+            } else {
+                st = c_dense++;
+            }
         }
+        const int ahead = min(nbuf - 1, n_iter - 1 - i);  // steps issued after this one
+        // K and mask of this step landed (its V and the later steps may fly on)
+        wait_steps_plus<NI, P::NIV>(ahead);
+        if (i < 8) FATTN_STAMP(2 + i);
 #ifdef FATTN_DIAG_NOCOMPUTE
         // diagnostic build only: memory-side ceiling of this access pattern
         wait_steps<NI>(ahead);
-        if (!lag && s + nbuf < nsteps) {
-            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf) * kStep, mrow0,
-                                            wbuf + cur * C::stepBytes, lane);
+        if (i + nbuf < n_iter) {
+            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + next_issue() * kStep, mrow0, wbuf + cur * C::stepBytes,
+                                            lane);
         }
         cur = (cur + 1 == nbuf) ? 0 : cur + 1;
         continue;
 #endif
-        const int n0 = w_lo + s * kStep;
-        split_step<KT, VT, D, HM>(a, wbuf + cur * C::stepBytes, qop, mq, g, i16, min(kStep, w_hi - n0), s == 0, m_run,
+        const int n0 = w_lo + st * kStep;
+        split_step<KT, VT, D, HM>(a, wbuf + cur * C::stepBytes, qop, mq, g, i16, min(kStep, w_hi - n0), i == 0, m_run,
                                   l_run, o, corr, [&] { wait_steps<NI>(ahead); });
 
-        // -- refill this buffer with step s + nbuf
-        if (!lag && s + nbuf < nsteps) {
+        // -- refill this buffer with the step nbuf iterations on
+        if (i + nbuf < n_iter) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf) * kStep, mrow0,
-                                            wbuf + cur * C::stepBytes, lane);
+            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + next_issue() * kStep, mrow0, wbuf + cur * C::stepBytes,
+                                            lane);
         }
         cur = (cur + 1 == nbuf) ? 0 : cur + 1;
     }

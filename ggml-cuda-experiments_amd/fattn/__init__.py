@@ -55,7 +55,7 @@ OPT_DEC_COMPUTE = 16
 OPT_DEC_DIAG = 17
 OPT_DEC_AHEAD = 18
 OPT_SPLIT_WAVES = 19
-OPT_SPLIT_LAG = 20
+OPT_SPLIT_SKIP = 20
 
 
 class FattnError(RuntimeError):

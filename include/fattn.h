@@ -150,9 +150,9 @@ enum {
     FATTN_OPT_DEC_AHEAD = 18,       /* removed; accepted with 0 only */
     FATTN_OPT_SPLIT_WAVES = 19,     /* split kernel waves per workgroup: 0 = auto, 4, 8 or 16 (16-B row path;
                                        16 needs the Q8_0/Q4_0 register budget, else clamped to 8) */
-    FATTN_OPT_SPLIT_LAG = 20        /* split kernel issue order: -1 = planner, 0 = a buffer is refilled once its
-                                       step is computed, 1 = the next step is issued once the current one has
-                                       landed (with >= 2 buffers: one step in flight beside the compute) */
+    FATTN_OPT_SPLIT_SKIP = 20       /* split kernel, masked: 0 = steps whose mask is -inf for every key and row
+                                       of the tile are neither loaded nor computed (default; the mask words are
+                                       read beside Q), 1 = every step loaded and computed */
 };
 int fattn_set_option(int option, int value);
 

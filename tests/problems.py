@@ -102,7 +102,8 @@ def make_problem(D=128, NQ=1, H=32, Hkv=None, N=4096, kv_type="q8_0", S=1, Skv=N
                  ramp=0.0) -> Problem:
     """Random problem.  mask: "none" | "random" (U[-1,1], like kernel_test.h:48) |
     "zero" | "causal" (query i sees positions <= N - NQ + i) | "neginf_blocks"
-    (some 32-position blocks fully -inf for every row)."""
+    (some 32-position blocks fully -inf for every row) | "tail" (a padded cache:
+    -inf from ~3N/8 on, so whole chunks of the split are masked)."""
     typ = TYPES[kv_type] if isinstance(kv_type, str) else kv_type
     Hkv = H if Hkv is None else Hkv
     Skv = S if Skv is None else Skv
@@ -164,6 +165,10 @@ def make_problem(D=128, NQ=1, H=32, Hkv=None, N=4096, kv_type="q8_0", S=1, Skv=N
             m = np.zeros((rows, npad), dtype=np.float32)
             for i in range(rows):
                 m[i, N - NQ + i + 1:] = -np.inf
+        elif mask == "tail":
+            # a padded KV cache: positions from ~3/8 of N on are unused (-inf)
+            m = u(rows, npad)
+            m[:, max(1, 3 * N // 8 + 5):] = -np.inf
         elif mask == "neginf_blocks":
             m = u(rows, npad)
             for b in range(1, N // 32, 3):

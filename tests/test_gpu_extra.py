@@ -234,15 +234,15 @@ def test_config4_gqa_head_shard_slices(dev):
 
 # ------------------------------------------------------------------ split kernel, 4 / 8 / 16 waves per workgroup
 
-@pytest.fixture(params=[(4, 0), (8, 0), (16, 0), (4, 1), (8, 1)], ids=["4waves", "8waves", "16waves", "4waves-lag",
-                                                                       "8waves-lag"])
+@pytest.fixture(params=[(4, 0), (8, 0), (16, 0), (4, 1), (8, 1)], ids=["4waves", "8waves", "16waves", "4waves-noskip",
+                                                                       "8waves-noskip"])
 def split_waves(request):
-    waves, lag = request.param
+    waves, no_skip = request.param
     fattn.set_option(fattn.OPT_SPLIT_WAVES, waves)
-    fattn.set_option(fattn.OPT_SPLIT_LAG, lag)
+    fattn.set_option(fattn.OPT_SPLIT_SKIP, no_skip)
     yield request.param
     fattn.set_option(fattn.OPT_SPLIT_WAVES, 0)
-    fattn.set_option(fattn.OPT_SPLIT_LAG, -1)
+    fattn.set_option(fattn.OPT_SPLIT_SKIP, 0)
 
 
 DEC_CASES = [
@@ -258,6 +258,10 @@ DEC_CASES = [
     dict(D=128, NQ=1, H=4, N=512, kv_type="f16", v_trans=True),
     dict(D=128, NQ=2, H=4, N=96, kv_type="q8_0", mask="neginf_blocks", S=2),
     dict(D=128, NQ=1, H=8, N=1000, kv_type="q8_0", layout="pos"),    # generic-stride path: always 4 waves
+    # padded caches: whole steps, slices and chunks -inf (step skipping, empty partials)
+    dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", mask="tail"),
+    dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0", mask="tail"),
+    dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0", mask="tail"),
 ]
 
 
