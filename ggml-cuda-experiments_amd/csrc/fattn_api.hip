@@ -55,7 +55,9 @@ std::atomic<int> g_opt_pf_no_skip{0};     // 1: masked prefill without the live-
 std::atomic<int> g_opt_split_prio{0};     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
 std::atomic<int> g_opt_no_wave_merge{0};  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
 std::atomic<int> g_opt_split_waves{0};
-std::atomic<int> g_opt_split_no_skip{0};  // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
+std::atomic<int> g_opt_split_no_skip{0};
+// launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
+std::atomic<uint32_t> g_epoch{0};  // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -584,6 +586,9 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
         if (!p->workspace || p->workspace_bytes < pl.ws_bytes || (uintptr_t)p->workspace % 16) return FATTN_ERR_WORKSPACE;
         uint8_t* w = (uint8_t*)p->workspace;
         pl.a.ws_cnt = (uint32_t*)w;
+        uint32_t e = g_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
+        if (e == 0) e = g_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
+        pl.a.arrival_stamp = kArrivalTag | (uint64_t)e << 16;
         pl.a.ws_ml = (float*)(w + pl.cnt_bytes);
         pl.a.ws_o = (float*)(w + pl.cnt_bytes + pl.ml_bytes);  // (prefill pre-pass: the f16 rows)
         if (pl.pf && pl.pf_flags) pl.a.pf_flags = w;

@@ -416,6 +416,9 @@ __global__ __launch_bounds__(NW * kWave, NW == 8 ? 1 : 2) void fattn_mq_kernel(c
     // of the tile merges the subtiles (same hand-off as fattn_split_kernel)
     constexpr int SUBS = NW * NG;
     const int64_t tile = (int64_t)iq3 * gridDim.y + y;
+    // this launch's stamp on the tile's arrival word (arrival_begin,
+    // fattn_split.h): ahead of the publish, so the drain below covers it
+    if (tid == 0) arrival_begin(a, tile);
     {
         auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
 #pragma unroll
@@ -432,13 +435,7 @@ __global__ __launch_bounds__(NW * kWave, NW == 8 ? 1 : 2) void fattn_mq_kernel(c
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* last_flag = (int*)smem;
-    if (tid == 0) {
-        uint32_t* cnt = a.ws_cnt + tile * kCntStride;
-        const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == (uint32_t)(a.n_chunks - 1);
-        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *last_flag = last;
-    }
+    if (tid == 0) *last_flag = arrive_last(a, tile, a.n_chunks);
     __syncthreads();
     if (!*last_flag) return;
     __syncthreads();  // the flag word is reused by the merge's LDS

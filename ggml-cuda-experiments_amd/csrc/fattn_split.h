@@ -56,7 +56,7 @@ struct SplitArgs {
     const uint8_t* v;
     const uint8_t* mask;
     float* dst;
-    uint32_t* ws_cnt;   // [S][Y] chunk arrival counters, one per 256-B line (zero between launches)
+    uint32_t* ws_cnt;   // [S][Y] chunk arrival words (64-bit), one per 256-B line (arrival_begin/arrive_last)
     float* ws_o;        // [S][Y][C][16][D] chunk partials
     float* ws_ml;       // [S][Y][C][16][2]
     int64_t q_nb1, q_nb2, q_nb3;
@@ -87,6 +87,7 @@ struct SplitArgs {
                         // last-arriving WAVE merges them (no LDS merge, no barriers);
                         // 2 = one-row tiles: LDS merge, then one partial per workgroup
                         // (wg_row_merge)
+    uint64_t arrival_stamp;  // kArrivalTag | launch epoch << 16 (arrival_begin)
     int step_skip;      // split kernel: 1 = skip steps whose mask is all -inf for the tile (FATTN_OPT_SPLIT_SKIP)
                         // flight beside the compute), 0 = refill a buffer once its step is computed
 };
@@ -271,18 +272,54 @@ struct StepSrc {
     i32x4 k, v, m;
 };
 
+// ---------------------------------------------------------------- arrivals
+// The chunks of a tile meet through one 64-bit arrival word per tile,
+// [0xFFFF | launch epoch : 32 | arrivals : 16].  Each arriving lane first
+// stamps the word with its launch's tag and epoch (atomic max, no return;
+// the split kernel issues it right after its prologue's DMA, off every
+// critical path): a word left by an earlier launch
+// (re-armed or, after an aborted launch, mid-count) or never zeroed (top 16
+// bits not all ones) is superseded and the count restarts at 0.  The last
+// arriver re-arms the word (count 0, same epoch), so a replayed graph finds
+// it clean.  Launches sharing one workspace must be stream-ordered.
+constexpr uint64_t kArrivalTag = 0xFFFFull << 48;
+
+__device__ __forceinline__ uint64_t* arrival_word(const SplitArgs& a, int64_t tile) {
+    return (uint64_t*)(a.ws_cnt + tile * kCntStride);
+}
+
+// by the lane that later calls arrive_last, before it (same-lane order)
+__device__ __forceinline__ void arrival_begin(const SplitArgs& a, int64_t tile) {
+    (void)__hip_atomic_fetch_max(arrival_word(a, tile), a.arrival_stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one lane: count this arrival; true for the tile's n-th (last) arriver,
+// which re-arms the word
+__device__ __forceinline__ bool arrive_last(const SplitArgs& a, int64_t tile, int n) {
+    uint64_t* w = arrival_word(a, tile);
+    const uint64_t old = __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = (old & 0xFFFF) == (uint64_t)(n - 1);
+    if (last) __hip_atomic_store(w, old & ~0xFFFFull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return last;
+}
+
 // One step = [K rows | V rows | mask rows] for positions [n0, n0+32), copied
 // as raw bytes.  GRAN = 16: 16-B pieces (quantised rows contiguous, f16 rows
 // 16-B aligned); GRAN = 4: dword pieces for any ggml row stride.
 template <int KT, int VT, int D, int GRAN, bool HM>
 __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs, int n0, int mrow0, uint8_t* buf,
-                                           int lane) {
+                                           int lane, bool kv_live = true) {
 #ifdef FATTN_DIAG_NOMEM
     return;  // diagnostic build only: compute on whatever LDS holds (compute latency)
 #endif
     using C = SplitCfg<KT, VT, D>;
     using P = StepPlan<KT, VT, D, GRAN>;
     const uint32_t kn1 = (uint32_t)a.k_nb1, vn1 = (uint32_t)a.v_nb1;
+    // a step that is -inf for the whole tile: K and V through empty
+    // descriptors (every load out of range: zeros, no traffic)
+    i32x4 ksrd = rs.k, vsrd = rs.v;
+    ksrd.z = __builtin_amdgcn_readfirstlane(kv_live ? rs.k.z : 0);
+    vsrd.z = __builtin_amdgcn_readfirstlane(kv_live ? rs.v.z : 0);
 #pragma unroll
     for (int i = 0; i < P::NIK; i++) {
         const int p = i * kWave + lane;
@@ -300,7 +337,7 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs
             const int row = byte / C::rowK;
             off = (uint32_t)(n0 + row) * kn1 + (byte % C::rowK);
         }
-        if (P::PK % kWave == 0 || p < P::PK) dma<GRAN, kDecodeNT>(rs.k, lds_addr(buf + i * kWave * GRAN), off);
+        if (P::PK % kWave == 0 || p < P::PK) dma<GRAN, kDecodeNT>(ksrd, lds_addr(buf + i * kWave * GRAN), off);
     }
     // K, then the mask, then V: a step's S^T and softmax start once K and the
     // mask have landed, while V is still in flight
@@ -339,7 +376,7 @@ __device__ __forceinline__ void issue_step(const SplitArgs& a, const StepSrc& rs
             const int row = byte / C::rowV;
             off = (uint32_t)(n0 + row) * vn1 + (byte % C::rowV);
         }
-        if (P::PV % kWave == 0 || p < P::PV) dma<GRAN, kDecodeNT>(rs.v, lds_addr(vbuf + i * kWave * GRAN), off);
+        if (P::PV % kWave == 0 || p < P::PV) dma<GRAN, kDecodeNT>(vsrd, lds_addr(vbuf + i * kWave * GRAN), off);
     }
 }
 
@@ -578,13 +615,11 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     FATTN_STAMP(12);
-    uint32_t* cnt = a.ws_cnt + tile * kCntStride;
-    uint32_t old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __builtin_amdgcn_readfirstlane(old);
+    int last = 0;
+    if (lane == 0) last = arrive_last(a, tile, NP);
+    last = __builtin_amdgcn_readfirstlane(last);
     FATTN_STAMP(14);
-    if (old != (uint32_t)(NP - 1)) return;
-    if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!last) return;
     // ---- merge: lane half h = lane / 32 takes the parts of parity h, dims
     // 4 (lane % 32) .. +3, one 16-B load per part (parts past NP fall outside
     // the descriptor: zeros, no traffic, weight 0); the halves meet by one
@@ -815,13 +850,11 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
 #ifdef FATTN_DIAG_NOATOMIC
     return;  // diagnostic build only: stop after the published row drained
 #endif
-    uint32_t* cnt = a.ws_cnt + tile * kCntStride;
-    uint32_t old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __builtin_amdgcn_readfirstlane(old);
+    int last = 0;
+    if (lane == 0) last = arrive_last(a, tile, a.n_chunks);
+    last = __builtin_amdgcn_readfirstlane(last);
     FATTN_STAMP(14);
-    if (old != (uint32_t)(a.n_chunks - 1)) return;
-    if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!last) return;
     merge_row_parts<D>(a.ws_o + tile * a.n_chunks * D, a.ws_ml + 2 * tile * a.n_chunks, a.n_chunks, out, lane);
     FATTN_STAMP(13);
 }
@@ -981,14 +1014,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
 #endif
     __syncthreads();  // every storing wave has drained; every wave is done reading the merge image
     int* last_flag = (int*)smem;
-    if (threadIdx.x == 0) {
-        uint32_t* cnt = a.ws_cnt + tile * kCntStride;
-        const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == (uint32_t)(a.n_chunks - 1);
-        // every chunk has arrived: re-arm the counter for the next launch
-        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *last_flag = last;
-    }
+    if (threadIdx.x == 0) *last_flag = arrive_last(a, tile, a.n_chunks);
     __syncthreads();
     FATTN_STAMP(12);
     if (!*last_flag) return;
@@ -1268,15 +1294,23 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
             qraw[b][1] = ld_buf(qs, qb + 16);
         }
     }
-    // ---- -inf step skipping (src/flash-llama.h:275-278), lifted to the DMA:
-    // a step whose mask is -inf for every key of every query row of the tile
-    // adds exp(-inf) = 0 to o and l, so it is neither loaded nor computed.
-    // The mask words of the wave's steps are read here beside Q (their wait is
-    // Q's): one (row, step) pair of 64 B per lane, when the tile's rows x
-    // steps fit the wave.  The prologue's steps are issued regardless.
+    // ---- -inf steps (src/flash-llama.h:275-278 skips their compute): a step
+    // whose mask is -inf for every key of every query row of the tile adds
+    // exp(-inf) = 0 to o and l.  Its K and V are not fetched: their DMA goes
+    // through empty descriptors (no HBM traffic, zeros in LDS; the mask still
+    // lands, so every score is -inf and the step's compute adds exactly 0).
+    // Loop and vmcnt accounting are unchanged.  The mask words of the wave's
+    // steps are read here beside Q (their wait is Q's): one (row, step) pair
+    // of 64 B per lane, when the tile's rows x steps fit the wave and the
+    // wave has at least 4 steps; the prologue's steps are fetched regardless.
+    // Measured (profiles/r02_skip): config 3 (2 steps per wave, no prefetch)
+    // unchanged; 8 heads x N = 32768 with 70 % of the cache masked 16.1 vs
+    // 17.1-17.5 us; the same unmasked 17.6-18.2 vs 16.9-17.5 us (the loads
+    // ahead of the first wait).  Reading the words after step 0 instead, or
+    // skipping by control flow in the loop, measured slower everywhere.
     const int pro = min(nbuf, nsteps);  // steps issued before the loop
     const int n_rows = HM ? min(a.QPT, a.NQ - mrow0) : 0;
-    const bool pre = HM && a.step_skip && nsteps > pro && n_rows * nsteps <= kWave;
+    const bool pre = HM && a.step_skip && nsteps >= 4 && n_rows * nsteps <= kWave;
     u32x4 mraw[4] = {};
     if (pre) {
         const int r = lane / nsteps, st = lane - r * nsteps;
@@ -1288,6 +1322,10 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     for (int s = 0; s < pro; s++) {
         issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + s * kStep, mrow0, wbuf + s * C::stepBytes, lane);
     }
+    // this launch's stamp on the tile's arrival word, by each lane that will
+    // count an arrival: issued after the prologue's DMA, so no wait is spent
+    // on it (at most one DMA instruction's worth in the counted waits below)
+    if (a.n_chunks > 1 && lane == 0 && (EPI == 1 || wave == 0)) arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
 
     FATTN_STAMP(1);
     if (a.split_prio == 2) __builtin_amdgcn_s_setprio(0);
@@ -1303,41 +1341,20 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
         h.s4 = (f16)x1.x; h.s5 = (f16)x1.y; h.s6 = (f16)x1.z; h.s7 = (f16)x1.w;
         qop[b] = h;
     }
-    // Steps after the prologue, in issue (= compute) order: the live ones of
-    // steps [pro, 64) as a bit set, then every step from 64 on (not prefetched).
-    uint64_t todo = 0;
-    {
-        const int nb64 = min(nsteps, 64);
-        const uint64_t upto = nb64 == 64 ? ~0ull : (1ull << nb64) - 1;
-        todo = upto & ~((1ull << pro) - 1);
-        if (pre) {
-            constexpr uint32_t kNegInf2 = 0xFC00FC00u;  // two f16 -inf
-            bool lv = false;
+    // bit s: step s has a live key (steps past 64 and unprefetched waves: all)
+    uint64_t live = ~0ull;
+    if (pre) {
+        constexpr uint32_t kNegInf2 = 0xFC00FC00u;  // two f16 -inf
+        bool lv = false;
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                reg_fence(mraw[j]);
-                lv |= (mraw[j].x != kNegInf2) | (mraw[j].y != kNegInf2) | (mraw[j].z != kNegInf2) |
-                      (mraw[j].w != kNegInf2);
-            }
-            const uint64_t bl = __builtin_amdgcn_ballot_w64(lv && lane < n_rows * nsteps);
-            uint64_t live = 0;
-            for (int r = 0; r < n_rows; r++) live |= bl >> (r * nsteps);
-            todo &= live;
+        for (int j = 0; j < 4; j++) {
+            reg_fence(mraw[j]);
+            lv |= (mraw[j].x != kNegInf2) | (mraw[j].y != kNegInf2) | (mraw[j].z != kNegInf2) | (mraw[j].w != kNegInf2);
         }
+        const uint64_t bl = __builtin_amdgcn_ballot_w64(lv && lane < n_rows * nsteps);
+        live = 0;
+        for (int r = 0; r < n_rows; r++) live |= bl >> (r * nsteps);
     }
-    const int n_iter = pro + __builtin_popcountll(todo) + max(0, nsteps - 64);
-    uint64_t i_rem = todo;  // issue side
-    int i_dense = 64;
-    auto next_issue = [&]() -> int {
-        if (i_rem) {
-            const int st = __builtin_ctzll(i_rem);
-            i_rem &= i_rem - 1;
-            return st;
-        }
-        return i_dense++;
-    };
-    uint64_t c_rem = todo;  // compute side (the same sequence, nbuf behind)
-    int c_dense = 64;
 
     float m_run = kNegInf;  // reference max (natural units) of column m
     float l_run = 0.0f;     // this lane's partial row sum
@@ -1348,40 +1365,33 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
 #pragma unroll
     for (int b = 0; b < NB; b++) corr[b] = 0.0f;
 
-    int cur = 0;  // buffer of iteration i
-    for (int i = 0; i < n_iter; i++) {
-        int st = i;  // the step of iteration i
-        if (i >= pro) {
-            if (c_rem) {
-                st = __builtin_ctzll(c_rem);
-                c_rem &= c_rem - 1;
-            } else {
-                st = c_dense++;
-            }
-        }
-        const int ahead = min(nbuf - 1, n_iter - 1 - i);  // steps issued after this one
-        // K and mask of this step landed (its V and the later steps may fly on)
+    int cur = 0;  // buffer of step s
+    for (int s = 0; s < nsteps; s++) {
+        const int ahead = min(nbuf - 1, nsteps - 1 - s);  // steps issued after step s
+        // K and mask of step s landed (its V and the later steps may fly on)
         wait_steps_plus<NI, P::NIV>(ahead);
-        if (i < 8) FATTN_STAMP(2 + i);
+        if (s < 8) FATTN_STAMP(2 + s);
 #ifdef FATTN_DIAG_NOCOMPUTE
         // diagnostic build only: memory-side ceiling of this access pattern
         wait_steps<NI>(ahead);
-        if (i + nbuf < n_iter) {
-            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + next_issue() * kStep, mrow0, wbuf + cur * C::stepBytes,
-                                            lane);
+        if (s + nbuf < nsteps) {
+            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + (s + nbuf) * kStep, mrow0, wbuf + cur * C::stepBytes, lane);
         }
         cur = (cur + 1 == nbuf) ? 0 : cur + 1;
         continue;
 #endif
-        const int n0 = w_lo + st * kStep;
-        split_step<KT, VT, D, HM>(a, wbuf + cur * C::stepBytes, qop, mq, g, i16, min(kStep, w_hi - n0), i == 0, m_run,
-                                  l_run, o, corr, [&] { wait_steps<NI>(ahead); });
+        const int n0 = w_lo + s * kStep;
+        int s_opaque = s;  // hides "first step" from loop peeling (a second copy of the body)
+        asm volatile("" : "+s"(s_opaque));
+        split_step<KT, VT, D, HM>(a, wbuf + cur * C::stepBytes, qop, mq, g, i16, min(kStep, w_hi - n0), s_opaque == 0,
+                                  m_run, l_run, o, corr, [&] { wait_steps<NI>(ahead); });
 
-        // -- refill this buffer with the step nbuf iterations on
-        if (i + nbuf < n_iter) {
+        // -- refill this buffer with step s + nbuf (K/V not fetched if -inf)
+        if (s + nbuf < nsteps) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + next_issue() * kStep, mrow0, wbuf + cur * C::stepBytes,
-                                            lane);
+            const int sn = s + nbuf;
+            issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + sn * kStep, mrow0, wbuf + cur * C::stepBytes, lane,
+                                            sn >= 64 || ((live >> sn) & 1));
         }
         cur = (cur + 1 == nbuf) ? 0 : cur + 1;
     }

@@ -250,7 +250,7 @@ class Attention:
         import torch
         self.p = ext_params(q, k, v, mask, _tptr(dst), scale, 0, 0, kv_chunk)
         ws = workspace_size(self.p)
-        # zero-filled once: the chunk-arrival counters at its front must start at 0
+        # (zeroing is optional: each launch epoch-stamps the arrival words at its front)
         self.workspace = torch.zeros(max(ws, 16), dtype=torch.uint8, device=dst.device)
         self.p.workspace = _tptr(self.workspace)
         self.p.workspace_bytes = self.workspace.numel()

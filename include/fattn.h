@@ -94,16 +94,22 @@ typedef struct fattn_params {
     float* dst;
     float scale;
     int32_t kv_chunk;      /* split-KV chunk length in positions; 0 = auto */
-    void* workspace;       /* split-KV scratch, >= fattn_workspace_size() bytes, zero-filled
-                              before its first use (fattn_workspace_init); every launch
-                              leaves it re-armed, so zero it once per allocation */
+    void* workspace;       /* split-KV scratch, >= fattn_workspace_size() bytes.  Its arrival
+                              words are stamped with a fresh epoch by every launch, so
+                              neither zeroing nor a clean previous launch is required
+                              (fattn_workspace_init zeroes it all the same); launches that
+                              share one workspace must be ordered on one stream */
     size_t workspace_bytes;
 } fattn_params;
 
 size_t fattn_workspace_size(const fattn_params* p);
-/* Zero a freshly allocated workspace (hipMemsetAsync on `stream`).  Needed once
- * per allocation: the split-KV chunks of a tile meet through arrival counters
- * kept at the front of the workspace, and each launch leaves them at zero. */
+/* Zero a workspace (hipMemsetAsync on `stream`).  Optional: the split-KV chunks
+ * of a tile meet through 64-bit arrival words kept at the front of the
+ * workspace, [0xFFFF | epoch:32 | count:16]; each launch stamps them with its
+ * own epoch (atomic max) before counting, so memory left by an earlier or an
+ * aborted launch, or never initialised, is superseded -- except a word whose
+ * top 16 bits are all ones with an epoch above the current one (e.g. 0xFF
+ * fill), which this call clears. */
 int fattn_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 int fattn_ext(const fattn_params* p, void* stream);
 
@@ -172,7 +178,7 @@ int fattn_ext_f16_launch(const void* q, const void* k, const void* v, const void
 /* flash_attn_row + fa_reduce (flash_row_float.h): query f32 [H][D], key f16
  * [Hkv][N][D] (head_stride = D*N elements), value f16 [Hkv][D][N], mask f16 [N],
  * qkv f32 [H][D]; r_kv_heads = H / Hkv.  tmp: >= fattn_row_workspace_size(),
- * zero-filled once after allocation (as for fattn_params.workspace). */
+ * its arrival words are epoch-stamped per launch (as for fattn_params.workspace). */
 size_t fattn_row_workspace_size(int head_dim, int kv_size, int num_heads);
 int fattn_row(const float* query, const void* key, const void* value, const void* mask, void* tmp,
               size_t tmp_bytes, float* qkv, int head_dim, int kv_size, int num_heads, float scale,

@@ -188,6 +188,43 @@ def test_workspace_prefill_then_decode(dev):
         fattn.set_option(fattn.OPT_PF, 0)
 
 
+@pytest.mark.parametrize("fill", ["bytes5a", "stale_count"])
+@pytest.mark.parametrize("case", [
+    dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0"),                  # config 3: workgroup-level row merge
+    dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", waves=4),         # wave partials (wave_merge 1)
+    dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0"),                  # multi-row tiles: combine_tile
+    dict(D=128, NQ=64, H=32, Hkv=8, N=2048, kv_type="q8_0"),          # multi-query kernel
+], ids=["row_merge", "wave_merge", "combine", "mq"])
+def test_workspace_not_zeroed(dev, case, fill):
+    """The arrival words need no zeroing: each launch stamps them with its own
+    epoch before counting (fattn_split.h arrival_begin), so a workspace full of
+    garbage, or left mid-count by an aborted launch, gives the right result on
+    the first launch and leaves the words re-armed for the next."""
+    import torch
+    case = dict(case)
+    waves = case.pop("waves", 0)
+    p = make_problem(seed=71, **case)
+    t = upload(p, dev)
+    fattn.set_option(fattn.OPT_SPLIT_WAVES, waves)
+    try:
+        att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+        assert int(att.describe().split("grid(")[1].split(",")[0]) > 1, att.describe()  # several chunks
+        ws = att.workspace
+        if fill == "bytes5a":
+            ws.fill_(0x5A)
+        else:  # every 256-B counter line: tag | epoch 1 | 5 arrivals already counted
+            words = ws[: ws.numel() // 8 * 8].view(torch.int64)
+            words[::32] = (0xFFFF << 48 | 1 << 16 | 5) - (1 << 64)
+        ref = p.oracle()
+        for _ in range(2):
+            t["dst"].zero_()
+            att()
+            torch.cuda.synchronize()
+            assert attn_rel_err(t["dst"].cpu().numpy(), ref) <= RTOL
+    finally:
+        fattn.set_option(fattn.OPT_SPLIT_WAVES, 0)
+
+
 # ------------------------------------------------------------------ multi-GPU head shard, one GPU
 
 @pytest.mark.parametrize("world", [2, 8])
@@ -262,6 +299,8 @@ DEC_CASES = [
     dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", mask="tail"),
     dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0", mask="tail"),
     dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0", mask="tail"),
+    dict(D=128, NQ=1, H=8, N=32768, kv_type="q8_0", mask="tail"),            # >= 4 steps per wave: K/V of
+    dict(D=128, NQ=3, H=8, Hkv=2, N=16384, kv_type="q4_0", mask="tail"),     # -inf steps not fetched
 ]
 
 
@@ -272,6 +311,33 @@ def test_split_waves(dev, split_waves, case):
     att = fattn.Attention(*views(p, t), t["dst"], p.scale)
     assert "fattn_split_kernel" in att.describe(), att.describe()
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("case", [
+    dict(D=128, NQ=1, H=8, N=32768, kv_type="q8_0", mask="tail"),
+    dict(D=128, NQ=3, H=8, Hkv=2, N=16384, kv_type="q4_0", mask="tail"),
+    dict(D=64, NQ=1, H=16, N=16384, kv_type="f16", mask="neginf_blocks"),
+], ids=["q8_0_tail", "q4_0_gqa_tail", "f16_blocks"])
+def test_step_skip_bitexact(dev, case):
+    """Steps that are -inf for the whole tile are not fetched (K/V through
+    empty descriptors); their compute then adds exactly 0, so the output is
+    bit-identical to the run that fetches every step (FATTN_OPT_SPLIT_SKIP)."""
+    import torch
+    p = make_problem(seed=83, **case)
+    t = upload(p, dev)
+    att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+    outs = []
+    try:
+        for no_skip in (0, 1):
+            fattn.set_option(fattn.OPT_SPLIT_SKIP, no_skip)
+            t["dst"].zero_()
+            att()
+            torch.cuda.synchronize()
+            outs.append(t["dst"].cpu().clone())
+    finally:
+        fattn.set_option(fattn.OPT_SPLIT_SKIP, 0)
+    assert torch.equal(outs[0], outs[1])
+    assert attn_rel_err(outs[0].numpy(), p.oracle()) <= RTOL
 
 
 # ------------------------------------------------------------------ quantize-on-write (fattn_cpy)

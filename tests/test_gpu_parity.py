@@ -535,5 +535,8 @@ def test_chunk_merge_handoff_stress(dev, hkv):
         got = t["dst"].cpu().numpy()
         assert attn_rel_err(got, ref) <= RTOL, f"iteration {it} (plan {it % len(atts)})"
     assert multi > 0
-    # counters re-armed: the tiles' counters (one 256-B line each) are zero again
-    assert int(shared[: hkv * 256].view(torch.int32).abs().sum()) == 0
+    # arrival words re-armed: every tile's word (one per 256-B line) counts 0
+    # again; the top bits keep the tag and the last launch's epoch
+    words = shared[: hkv * 256].view(torch.int64)[::32]
+    assert int((words & 0xFFFF).abs().sum()) == 0
+    assert bool((((words >> 48) & 0xFFFF) == 0xFFFF).all())
