@@ -201,8 +201,8 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
         pl.ml_bytes = (parts * 2 * sizeof(float) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + parts * pl.D * 4;
     } else if (a.n_chunks > 1) {
-        // [arrival counters, one 256-B line per tile][(m, l) pairs][O partials];
-        // zero-filled once per allocation: each launch re-arms the counters
+        // [arrival words, one 256-B line per tile][(m, l) pairs][O partials];
+        // no zeroing needed: each launch epoch-stamps its arrival words
         pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
         pl.ml_bytes = ((size_t)S * Y * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + (size_t)S * Y * a.n_chunks * kRows * pl.D * 4;
@@ -409,10 +409,9 @@ int make_plan(const fattn_params* p, Plan& pl) {
                                             : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
-        // share the front of the workspace with the split-KV arrival counters
-        // a later decode on the same workspace relies on, so the launch
-        // re-zeroes them behind the prefill kernel (workspace contract,
-        // include/fattn.h: every launch leaves the workspace re-armed).
+        // share the front of the workspace with the split-KV arrival words; a
+        // later decode supersedes whatever the flags left there (its epoch
+        // stamp, arrival_begin in fattn_split.h), so nothing is re-zeroed.
         pl.pf_flags = has_mask && !g_opt_pf_no_skip;
         if (pl.pf_flags) pl.cnt_bytes = ((size_t)a.n_qt * (N / kPfKeys) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes;

@@ -145,7 +145,6 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
             hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,
                                pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
         hipLaunchKernelGGL(kern, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
-        if (HM && pl.a.pf_flags) (void)hipMemsetAsync((void*)pl.a.pf_flags, 0, pl.cnt_bytes, st);
     });
 }
 

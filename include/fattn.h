@@ -131,7 +131,7 @@ enum {
     FATTN_OPT_PF_STAGGER = 6,       /* prefill kernel, bit 0: SIMD partner waves staggered (default lockstep);
                                        bit 1 (default on): waves 4-7 at s_setprio 1; bit 2: XCD-grouped
                                        workgroup order (the query tiles of a kv head on one XCD) */
-    FATTN_OPT_PF_WAVES = 7,         /* prefill kernel: 8 = 8 waves x 32 rows, 4 = 4 waves x 64 rows (one per SIMD) */
+    FATTN_OPT_PF_WAVES = 7,         /* removed experiment (4 waves x 64 rows); accepted with 8 only */
     FATTN_OPT_PF_DEQUANT = 8        /* quantised prefill: 0 = auto, 1 = dequantise inside the kernel, 2 = convert K/V
                                        to f16 rows in the workspace first (fattn_workspace_size grows by
                                        2 * Skv * Hkv * N * D * 2 bytes; 8 waves only) */,

@@ -161,8 +161,8 @@ def test_positional_launch_odd_kv(dev):
 def test_workspace_prefill_then_decode(dev):
     """One workspace for a masked (causal) prefill and then a multi-chunk
     decode, as llama.cpp reuses it: the prefill's live-block flags share the
-    front of the workspace with the decode's arrival counters, and every
-    launch must leave it re-armed (include/fattn.h)."""
+    front of the workspace with the decode's arrival words, which the decode
+    supersedes by its epoch stamp (nothing re-zeroes the flags)."""
     import torch
     pre = make_problem(D=128, NQ=512, H=8, Hkv=2, N=512, kv_type="q8_0", mask="causal", seed=61)
     dec = make_problem(D=128, NQ=1, H=32, Hkv=8, N=4096, kv_type="q8_0", mask="random", seed=62)
