@@ -231,6 +231,8 @@ def parse_args(argv=None):
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
     ap.add_argument("--waves", type=int, default=0, help="split kernel waves per workgroup (4, 8, 16; 0 = planner)")
     ap.add_argument("--no-step-skip", action="store_true", help="split kernel: load and compute every step")
+    ap.add_argument("--fused-merge", action="store_true",
+                    help="split kernel, multi-row tiles: last-arriving workgroup merges (no second launch)")
     ap.add_argument("--mask-live", type=float, default=1.0,
                     help="diagnostics: mask positions from this fraction of N on to -inf (a padded cache)")
     ap.add_argument("--wave-merge", type=int, default=-1, help="split/dec one-row tiles: 0 per-wave merge, 1 LDS merge")
@@ -253,6 +255,7 @@ def apply_options(args):
             (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO),
             (args.waves, fattn.OPT_SPLIT_WAVES)]
     fattn.set_option(fattn.OPT_SPLIT_SKIP, 1 if args.no_step_skip else 0)
+    fattn.set_option(fattn.OPT_SPLIT_MERGE, 1 if args.fused_merge else 0)
     for val, opt in opts:
         if val:
             fattn.set_option(opt, val)

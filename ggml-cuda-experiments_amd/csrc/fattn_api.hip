@@ -56,6 +56,7 @@ std::atomic<int> g_opt_split_prio{0};     // split kernel wave priorities (FATTN
 std::atomic<int> g_opt_no_wave_merge{0};  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
 std::atomic<int> g_opt_split_waves{0};
 std::atomic<int> g_opt_split_no_skip{0};
+std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
 std::atomic<uint32_t> g_epoch{0};  // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
 
@@ -191,6 +192,13 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
         if (nwv == 4 && a.n_chunks > 1 && pl.D == 128 && a.n_chunks * nwv <= kWaveMergeParts) a.wave_merge = 1;
         else if (nwv > 4 || a.n_chunks > 1) a.wave_merge = 2;
     }
+    // multi-row tiles (and one-row tiles forced onto the same epilogue) with 4
+    // or more chunks: the chunk partials merge in a second launch, one wave per
+    // (tile, row) instead of one workgroup per tile (config 5 shard: 11.8 vs
+    // 14.8 us, config 4: 10.0 vs 10.7; with 2 chunks per tile, config 5 on
+    // one GPU, the extra launch costs more than it saves: 36.6 vs 35.6).
+    // FATTN_OPT_SPLIT_MERGE = 1: always the last-arriving workgroup (combine_tile).
+    a.merge_launch = (a.n_chunks >= 4 && a.wave_merge == 0 && !g_opt_split_fused_merge) ? 1 : 0;
     pl.lds = G.lds_bytes(nbuf, nwv);
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     if (a.n_chunks > 1 && a.wave_merge) {
@@ -485,6 +493,10 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
             g_opt_no_wave_merge = value;
             return FATTN_OK;
+        case FATTN_OPT_SPLIT_MERGE:
+            if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_fused_merge = value;
+            return FATTN_OK;
         case FATTN_OPT_PF_PIPE:  // removed experiments: only the lockstep kernel remains
             return value == 0 || value == 1 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_SPLIT_STEPS:
@@ -568,8 +580,8 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
     else if (pl.mq)
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>", tn(pl.kt), pl.D, pl.nw, hm);
     else
-        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>", tn(pl.kt), tn(pl.vt), pl.D,
-                      pl.gran, hm, pl.nwv);
+        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>%s", tn(pl.kt), tn(pl.vt),
+                      pl.D, pl.gran, hm, pl.nwv, pl.a.merge_launch ? " + fattn_merge_kernel" : "");
     const int n = std::snprintf(out, cap, "%s grid(%u,%u,%u) lds %d chunk %d steps/slots %d ws %zu", kern, pl.grid.x,
                                 pl.grid.y, pl.grid.z, pl.lds, pl.a.chunk_len, pl.a.nbuf, pl.ws_bytes);
     return n < 0 || (size_t)n >= cap ? FATTN_ERR_INVALID_ARG : FATTN_OK;

@@ -79,6 +79,12 @@ int launch_split_e(const Plan& pl, hipStream_t st, const Events& ev) {
     auto kern = fattn_split_kernel<KT, VT, D, GRAN, HM, NWV, EPI>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         hipLaunchKernelGGL(kern, pl.grid, dim3(NWV * kWave), pl.lds, st, pl.a);
+        if constexpr (EPI == 0) {
+            // multi-row tiles: the chunk partials merge in a second launch
+            if (pl.a.merge_launch)
+                hipLaunchKernelGGL(fattn_merge_kernel<D>, dim3(kRows / 4, pl.grid.y, pl.grid.z), dim3(256), 0, st,
+                                   pl.a);
+        }
     });
 }
 

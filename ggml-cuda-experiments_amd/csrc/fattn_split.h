@@ -88,6 +88,7 @@ struct SplitArgs {
                         // 2 = one-row tiles: LDS merge, then one partial per workgroup
                         // (wg_row_merge)
     uint64_t arrival_stamp;  // kArrivalTag | launch epoch << 16 (arrival_begin)
+    int merge_launch;   // split kernel, multi-row tiles: 1 = partials merged by fattn_merge_kernel (second launch)
     int step_skip;      // split kernel: 1 = skip steps whose mask is all -inf for the tile (FATTN_OPT_SPLIT_SKIP)
                         // flight beside the compute), 0 = refill a buffer once its step is computed
 };
@@ -689,26 +690,27 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
 // src/flash_row_float.h:415-472, in fp32.
 template <int D>
 __device__ __forceinline__ void merge_row_parts(const float* parts_o, const float* parts_ml, int NP, float* out,
-                                                int lane) {
+                                                int lane, int ostride = D, int mstride = 2) {
     constexpr float kNegInf = -__builtin_inff();
     constexpr int LPP = D / 4;                         // lanes per part
     constexpr int PPR = 64 % LPP == 0 ? 64 / LPP : 1;  // parts per lane row (4, 2, 1; D = 80 / 96: 1)
     constexpr int kIt = 16;        // loads per lane per round trip
     const int h = lane / LPP, d4 = 4 * (lane % LPP);
-    const i32x4 osrd = make_srd(parts_o, (uint32_t)(NP * D * 4));
-    const i32x4 msrd = make_srd(parts_ml, (uint32_t)(NP * 8));
+    // (part p's O row at p * ostride floats, its (m, l) at p * mstride)
+    const i32x4 osrd = make_srd(parts_o, (uint32_t)(NP * ostride * 4));
+    const i32x4 msrd = make_srd(parts_ml, (uint32_t)(NP * mstride * 4));
     u32x4 v[kIt];
     auto issue = [&](int p0) {
 #pragma unroll
-        for (int i = 0; i < kIt; i++) v[i] = ld_sc1_buf(osrd, (uint32_t)(((p0 + PPR * i + h) * D + d4) * 4));
+        for (int i = 0; i < kIt; i++) v[i] = ld_sc1_buf(osrd, (uint32_t)(((p0 + PPR * i + h) * ostride + d4) * 4));
     };
     auto fence = [&] {
 #pragma unroll
         for (int i = 0; i < kIt; i++) reg_fence(v[i]);
     };
     issue(0);
-    uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
-    uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8 + 4));  //          l of part p
+    uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * mstride * 4));      // lane p: m of part p
+    uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * mstride * 4 + 4));  //          l of part p
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     reg_fence(mlm);
     reg_fence(mll);
@@ -1007,6 +1009,9 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
         }
         if (tj == 0) st_sc1_x2(a.ws_ml + 2 * slot, u32x2{bits(M), bits(L)});
     }
+    // second-launch merge (fattn_merge_kernel): the kernel boundary orders
+    // these stores before its loads; no drain, no counter
+    if (a.merge_launch) return;
     // every storing wave drains: the merging workgroup reads its own partial back too
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef FATTN_DIAG_NOATOMIC
@@ -1325,7 +1330,8 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     // this launch's stamp on the tile's arrival word, by each lane that will
     // count an arrival: issued after the prologue's DMA, so no wait is spent
     // on it (at most one DMA instruction's worth in the counted waits below)
-    if (a.n_chunks > 1 && lane == 0 && (EPI == 1 || wave == 0)) arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
+    if (a.n_chunks > 1 && !a.merge_launch && lane == 0 && (EPI == 1 || wave == 0))
+        arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
 
     FATTN_STAMP(1);
     if (a.split_prio == 2) __builtin_amdgcn_s_setprio(0);
@@ -1409,6 +1415,34 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     FATTN_STAMP(10);
     split_epilogue<KT, VT, D, NWV, EPI>(a, o, m_run, l_run, corr, wave, lane, qt, hs, ik2, iq3, y, chunk, smem, a.wave_bytes,
                                    true, false);
+}
+
+// ---------------------------------------------------------------- merge launch
+// Second launch of a multi-row split (SplitArgs::merge_launch): one wave per
+// (tile, packed row) merges the row's chunk partials (merge_row_parts: the
+// fa_reduce LSE merge of src/flash_row_float.h:415-472 in fp32, fixed order)
+// and writes the normalised dst row.  The last-arriver form (combine_tile)
+// pulls a whole tile's 16 rows x chunks into ONE workgroup (config 5 shard:
+// 128 KB, 6.4 us of a 14.7 us launch); here the same bytes spread over
+// (tiles x rows) waves, and the kernel boundary replaces drain + counter.
+template <int D>
+__global__ __launch_bounds__(256) void fattn_merge_kernel(const SplitArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int tm = blockIdx.x * 4 + (threadIdx.x >> 6);  // packed row of the tile
+    const int y = blockIdx.y, iq3 = blockIdx.z;
+    int qt = 0, hs = 0, ik2 = y;  // the split kernel's tile decode
+    if (a.n_qt != 1 || a.n_hsub != 1) {
+        qt = y % a.n_qt;
+        hs = (y / a.n_qt) % a.n_hsub;
+        ik2 = y / (a.n_qt * a.n_hsub);
+    }
+    if (tm >= tile_rows(a, qt, hs)) return;
+    const int64_t slot0 = ((int64_t)iq3 * gridDim.y + y) * a.n_chunks * kRows + tm;  // chunk 0's row tm
+    const int rq = div_R(a, tm);
+    const int riq1 = qt * a.QPT + rq;
+    const int riq2 = ik2 * a.rk2 + hs * a.R + (tm - rq * a.R);
+    float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D;
+    merge_row_parts<D>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kRows * D, 2 * kRows);
 }
 
 // ---------------------------------------------------------------- combine

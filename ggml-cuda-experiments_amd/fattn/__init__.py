@@ -56,6 +56,7 @@ OPT_DEC_DIAG = 17
 OPT_DEC_AHEAD = 18
 OPT_SPLIT_WAVES = 19
 OPT_SPLIT_SKIP = 20
+OPT_SPLIT_MERGE = 21
 
 
 class FattnError(RuntimeError):

@@ -158,7 +158,10 @@ enum {
                                        16 needs the Q8_0/Q4_0 register budget, else clamped to 8) */
     FATTN_OPT_SPLIT_SKIP = 20       /* split kernel, masked: 0 = steps whose mask is -inf for every key and row
                                        of the tile are neither loaded nor computed (default; the mask words are
-                                       read beside Q), 1 = every step loaded and computed */
+                                       read beside Q), 1 = every step loaded and computed */,
+    FATTN_OPT_SPLIT_MERGE = 21      /* split kernel, tiles of several packed rows: 0 = the chunk partials merge in
+                                       a second launch, one wave per (tile, row) (default), 1 = the last-arriving
+                                       workgroup merges the whole tile (combine_tile) */
 };
 int fattn_set_option(int option, int value);
 

@@ -196,6 +196,8 @@ def test_workspace_prefill_then_decode(dev):
     dict(D=128, NQ=64, H=32, Hkv=8, N=2048, kv_type="q8_0"),          # multi-query kernel
 ], ids=["row_merge", "wave_merge", "combine", "mq"])
 def test_workspace_not_zeroed(dev, case, fill):
+    # (the multi-row case merges in a second launch and never reads the words;
+    # it checks that the garbage does not leak into the partials either)
     """The arrival words need no zeroing: each launch stamps them with its own
     epoch before counting (fattn_split.h arrival_begin), so a workspace full of
     garbage, or left mid-count by an aborted launch, gives the right result on
@@ -338,6 +340,32 @@ def test_step_skip_bitexact(dev, case):
         fattn.set_option(fattn.OPT_SPLIT_SKIP, 0)
     assert torch.equal(outs[0], outs[1])
     assert attn_rel_err(outs[0].numpy(), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("fused", [0, 1], ids=["merge_launch", "fused"])
+@pytest.mark.parametrize("case", [
+    dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0"),                  # config 5 shard: 16-row tiles, 16 chunks
+    dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0"),           # config 4: 4-row tiles, 32 chunks
+    dict(D=96, NQ=4, H=16, Hkv=4, N=4096, kv_type="q8_0", mask="tail"),
+    dict(D=80, NQ=3, H=8, Hkv=2, N=4096, kv_type="f16"),
+    dict(D=256, NQ=2, H=8, Hkv=4, N=4096, kv_type="f16", S=2),
+    dict(D=64, NQ=9, H=8, Hkv=2, N=4096, kv_type="q4_0", mask="causal"),
+], ids=["config5_shard", "config4", "d96_tail", "d80", "d256_s2", "d64_causal"])
+def test_multirow_merge_paths(dev, case, fused):
+    """Multi-row split tiles: the second-launch merge (one wave per tile row,
+    fattn_merge_kernel) and the last-arriving-workgroup merge (combine_tile)
+    both match the oracle."""
+    p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    t = upload(p, dev)
+    fattn.set_option(fattn.OPT_SPLIT_MERGE, fused)
+    try:
+        att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+        d = att.describe()
+        assert "fattn_split_kernel" in d and int(d.split("grid(")[1].split(",")[0]) >= 4, d
+        assert ("fattn_merge_kernel" in d) == (not fused), d
+        assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+    finally:
+        fattn.set_option(fattn.OPT_SPLIT_MERGE, 0)
 
 
 # ------------------------------------------------------------------ quantize-on-write (fattn_cpy)

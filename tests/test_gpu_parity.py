@@ -537,6 +537,7 @@ def test_chunk_merge_handoff_stress(dev, hkv):
     assert multi > 0
     # arrival words re-armed: every tile's word (one per 256-B line) counts 0
     # again; the top bits keep the tag and the last launch's epoch
+    # (plans whose partials merge in a second launch never touch the words)
     words = shared[: hkv * 256].view(torch.int64)[::32]
     assert int((words & 0xFFFF).abs().sum()) == 0
-    assert bool((((words >> 48) & 0xFFFF) == 0xFFFF).all())
+    assert bool(((((words >> 48) & 0xFFFF) == 0xFFFF) | (words == 0)).all())
