@@ -163,6 +163,14 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
             if ((need <= slots && reducer_ok) || nch == 1) break;
             spw++;
         }
+        // multi-row tiles with long per-wave slices: twice the chunks (two
+        // workgroups per CU); their merge is a second launch from 4 chunks on
+        // (config 5 on one GPU: 16 -> 8 steps per wave, 2 -> 4 chunks, 36.5 ->
+        // 30.0 us; halving again, 8 chunks: 36.1)
+        if (rv_max > 1 && spw >= 8 && !g_opt_split_fused_merge) {
+            const int64_t nch2 = (N + (int64_t)(spw / 2) * quantum - 1) / ((int64_t)(spw / 2) * quantum);
+            if (combine_ok(nch2, rv_max, pl.D)) spw /= 2;
+        }
         if (g_opt_split_spw > 0) {
             spw = (int)std::min<int64_t>(g_opt_split_spw, (steps + nwv - 1) / nwv);
             const int64_t nch = (N + (int64_t)spw * quantum - 1) / ((int64_t)spw * quantum);
