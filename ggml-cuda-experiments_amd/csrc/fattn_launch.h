@@ -80,10 +80,17 @@ int launch_split_e(const Plan& pl, hipStream_t st, const Events& ev) {
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         hipLaunchKernelGGL(kern, pl.grid, dim3(NWV * kWave), pl.lds, st, pl.a);
         if constexpr (EPI == 0) {
-            // multi-row tiles: the chunk partials merge in a second launch
-            if (pl.a.merge_launch)
-                hipLaunchKernelGGL(fattn_merge_kernel<D>, dim3(kRows / 4, pl.grid.y, pl.grid.z), dim3(256), 0, st,
-                                   pl.a);
+            // multi-row tiles: the chunk partials merge in a second launch, with
+            // as few load slots per lane as the chunk count allows (the slots
+            // past it still cost issue cycles)
+            if (pl.a.merge_launch) {
+                const dim3 g(kRows / 4, pl.grid.y, pl.grid.z);
+                const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
+                if (need <= 2) hipLaunchKernelGGL((fattn_merge_kernel<D, 2>), g, dim3(256), 0, st, pl.a);
+                else if (need <= 4) hipLaunchKernelGGL((fattn_merge_kernel<D, 4>), g, dim3(256), 0, st, pl.a);
+                else if (need <= 8) hipLaunchKernelGGL((fattn_merge_kernel<D, 8>), g, dim3(256), 0, st, pl.a);
+                else hipLaunchKernelGGL((fattn_merge_kernel<D, 16>), g, dim3(256), 0, st, pl.a);
+            }
         }
     });
 }

@@ -689,12 +689,14 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
 // order (deterministic).  `out` = the tile's dst row.  fa_reduce math,
 // src/flash_row_float.h:415-472, in fp32.
 template <int D>
+constexpr int merge_ppr() { return 64 % (D / 4) == 0 ? 64 / (D / 4) : 1; }  // parts per lane row (4, 2, 1)
+
+template <int D, int kIt = 16>  // kIt: loads per lane per round trip
 __device__ __forceinline__ void merge_row_parts(const float* parts_o, const float* parts_ml, int NP, float* out,
                                                 int lane, int ostride = D, int mstride = 2) {
     constexpr float kNegInf = -__builtin_inff();
-    constexpr int LPP = D / 4;                         // lanes per part
-    constexpr int PPR = 64 % LPP == 0 ? 64 / LPP : 1;  // parts per lane row (4, 2, 1; D = 80 / 96: 1)
-    constexpr int kIt = 16;        // loads per lane per round trip
+    constexpr int LPP = D / 4;              // lanes per part
+    constexpr int PPR = merge_ppr<D>();     // D = 80 / 96: 1
     const int h = lane / LPP, d4 = 4 * (lane % LPP);
     // (part p's O row at p * ostride floats, its (m, l) at p * mstride)
     const i32x4 osrd = make_srd(parts_o, (uint32_t)(NP * ostride * 4));
@@ -1425,7 +1427,7 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
 // pulls a whole tile's 16 rows x chunks into ONE workgroup (config 5 shard:
 // 128 KB, 6.4 us of a 14.7 us launch); here the same bytes spread over
 // (tiles x rows) waves, and the kernel boundary replaces drain + counter.
-template <int D>
+template <int D, int KIT>  // KIT: loads per lane per round trip, >= the tile's chunks / merge_ppr<D>() when possible
 __global__ __launch_bounds__(256) void fattn_merge_kernel(const SplitArgs a) {
     const int lane = threadIdx.x & 63;
     const int tm = blockIdx.x * 4 + (threadIdx.x >> 6);  // packed row of the tile
@@ -1442,7 +1444,7 @@ __global__ __launch_bounds__(256) void fattn_merge_kernel(const SplitArgs a) {
     const int riq1 = qt * a.QPT + rq;
     const int riq2 = ik2 * a.rk2 + hs * a.R + (tm - rq * a.R);
     float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D;
-    merge_row_parts<D>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kRows * D, 2 * kRows);
+    merge_row_parts<D, KIT>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kRows * D, 2 * kRows);
 }
 
 // ---------------------------------------------------------------- combine
