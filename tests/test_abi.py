@@ -63,6 +63,32 @@ def test_workspace_size_config3():
     assert ws > 0 and ws >= 32 * 2 * (128 * 4 + 8) + 32 * 256
 
 
+@pytest.mark.parametrize("kw,want", [
+    (dict(), ["8waves>", "grid(8,32,1)", "steps/slots 1"]),                                 # config 3
+    (dict(N=2048, kt=fattn.TYPE_F16), ["f16,f16", "8waves>", "grid(8,32,1)"]),              # config 2
+    (dict(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0), ["4waves> + fattn_merge_kernel", "grid(32,8,1)"]),  # config 4
+    (dict(NQ=64), ["4waves> + fattn_merge_kernel", "grid(4,128,1)", "chunk 1024"]),         # config 5, one GPU
+    (dict(NQ=64, H=4, Hkv=4), ["4waves> + fattn_merge_kernel", "grid(16,16,1)"]),           # config 5, 8-rank shard
+], ids=["config3", "config2", "config4", "config5", "config5_shard"])
+def test_planner_picks(kw, want):
+    """The plans the round-2 measurements chose, at 256 CUs:
+    one-row tiles take 8 waves with the fused row merge; multi-row tiles with
+    4+ chunks merge in a second launch; long multi-row slices take twice the
+    chunks."""
+    d = fattn.describe(_params(**kw))
+    for w in want:
+        assert w in d, d
+
+
+def test_split_merge_option_restores_fused_merge():
+    fattn.set_option(fattn.OPT_SPLIT_MERGE, 1)
+    try:
+        d = fattn.describe(_params(NQ=64, H=4, Hkv=4))
+    finally:
+        fattn.set_option(fattn.OPT_SPLIT_MERGE, 0)
+    assert "fattn_merge_kernel" not in d and "grid(16,16,1)" in d, d
+
+
 def test_single_chunk_needs_no_workspace():
     assert fattn.workspace_size(_params(N=128)) == 0
 
