@@ -390,6 +390,20 @@ int make_plan(const fattn_params* p, Plan& pl) {
         // 256 rows per workgroup once that still gives one workgroup per CU
         const int64_t wg256 = Hkv * S * ((NQ * a.rk2 + 255) / 256);
         pl.nw = g_opt_mq_rpw ? (g_opt_mq_rpw == 32 ? 8 : 4) : wg256 >= pl.cus ? 8 : 4;
+        // ... and only when its tiles need at most 4 KV chunks to fill the chip:
+        // with more, its last-arriver merge of 64/256-row tiles costs more than
+        // the split kernel's 16-row re-reads plus second-launch merge (32/8
+        // heads, n_q = 64: 46.2 vs 28.6 us; 8 heads x N = 8192, n_q = 256: 59.8
+        // vs 44.1; n_q = 128: 50.8 vs 45.6; 32 heads, n_q = 256, 4 chunks: mq
+        // 76.2 vs 89.3, profiles/r02_merge/mq_vs_split.txt)
+        const int64_t ymq = Hkv * S * ((NQ * a.rk2 + (pl.nw == 8 ? 255 : 63)) / (pl.nw == 8 ? 256 : 64));
+        const int64_t want = pl.nw == 8 ? pl.cus : 2 * pl.cus;
+        // (automatic mode only: a threshold or tile size set by FATTN_OPT_MQ_*
+        // or a forced chunk keeps the multi-query kernel)
+        if (g_opt_mq_min_rows == 256 && !g_opt_mq_rpw && p->kv_chunk <= 0 && (want + ymq - 1) / ymq > 4)
+            pl.mq = false;
+    }
+    if (pl.mq) {
         a.R = a.rk2;
         a.QPT = (pl.nw == 8 ? 256 : 64) / a.R;
         a.R_inv = 1.0f / (float)a.R;

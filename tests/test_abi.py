@@ -69,7 +69,9 @@ def test_workspace_size_config3():
     (dict(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0), ["4waves> + fattn_merge_kernel", "grid(32,8,1)"]),  # config 4
     (dict(NQ=64), ["4waves> + fattn_merge_kernel", "grid(4,128,1)", "chunk 1024"]),         # config 5, one GPU
     (dict(NQ=64, H=4, Hkv=4), ["4waves> + fattn_merge_kernel", "grid(16,16,1)"]),           # config 5, 8-rank shard
-], ids=["config3", "config2", "config4", "config5", "config5_shard"])
+    (dict(NQ=256), ["fattn_mq_kernel", "grid(4,128,1)"]),                                   # batched: mq, 4 chunks
+    (dict(NQ=64, H=32, Hkv=8), ["fattn_split_kernel", "+ fattn_merge_kernel"]),             # mq would need 16 chunks
+], ids=["config3", "config2", "config4", "config5", "config5_shard", "mq_nq256", "split_nq64_gqa"])
 def test_planner_picks(kw, want):
     """The plans the round-2 measurements chose, at 256 CUs:
     one-row tiles take 8 waves with the fused row merge; multi-row tiles with

@@ -124,6 +124,9 @@ MQ_CASES = [
 @pytest.mark.parametrize("case", MQ_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_mq_sweep(dev, mq_on, case):
     p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert "fattn_mq_kernel" in d or "fattn_pf_kernel" in d, d
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
