@@ -13,9 +13,9 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-functi
 CSRC := $(wildcard $(PKG)/csrc/*.hip)
 CHDR := $(wildcard $(PKG)/csrc/*.h) include/fattn.h
 
-.PHONY: all lib harness oracle clean asm stamps tests-hip
+.PHONY: all lib harness oracle clean asm stamps tests-hip probe
 
-all: lib harness oracle tests-hip
+all: lib harness oracle tests-hip probe
 
 lib: $(LIB)
 
@@ -50,6 +50,13 @@ $(HARNESS): $(PKG)/host/kernel_test.cpp $(LIB) include/fattn.h
 
 oracle:
 	$(MAKE) -C oracle
+
+# measurement probe for bench.py's roofline (dwordx4 copy / read ceilings); not part of libfattn
+PROBE := $(LIBDIR)/libhbmcopy.so
+probe: $(PROBE)
+$(PROBE): tools/hbm_copy.hip
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared $< -o $@
 
 # ISA dump for inspection (not part of the build): make asm ASMSRC=fattn_launch_d128
 ASMSRC ?= fattn_launch_d128

@@ -41,10 +41,13 @@ import subprocess
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ggml-cuda-experiments_amd"))
 sys.path.insert(0, ROOT)
 
+ROTATE_BYTES = 512 << 20  # KV bytes one rank reads per pass of the rotation
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_F16_PEAK_TFLOPS = 2500.0
 METRIC = "attn TFLOPS & HBM GB/s per GPU; head_dim=128 seq=4096 Q8_0 KV"
@@ -119,26 +122,82 @@ def cpu_baseline(seconds: float, threads: int):
             "single_thread": single, "nproc": os.cpu_count(), "host_cpu": _cpu_model()}
 
 
-def measured_copy_peak(dev):
-    """Measured HBM ceiling for the roofline's secondary fraction: a 1 GiB
-    device-to-device copy (torch's copy kernel), read + write bytes / time,
-    median of 10 (fraction against a measured copy-kernel peak)."""
-    import torch
-    n = 1 << 30
-    a = torch.empty(n, dtype=torch.uint8, device=dev)
-    b = torch.empty(n, dtype=torch.uint8, device=dev)
-    a.fill_(1)
-    ts = []
-    for _ in range(12):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        b.copy_(a)
-        e1.record()
-        torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1))
-    del a, b
-    ms = statistics.median(ts[2:])
-    return round(2 * n / (ms * 1e-3) / 1e9, 1)
+def measured_hbm_peaks():
+    """Measured HBM ceilings for the roofline's secondary fractions (BASELINE.md:
+    fraction against a measured copy-kernel peak): tools/hbm_copy.hip built into
+    lib/libhbmcopy.so -- a global_load_dwordx4 / global_store_dwordx4 copy of
+    1 GiB (read + written bytes / median launch time, the form of
+    MI355X_MICROARCH.md's 6.29 TB/s float4-copy figure) and a dwordx4 read-only
+    stream of the same buffer (the decode kernel's access mix is read-only)."""
+    path = os.path.join(ROOT, "ggml-cuda-experiments_amd", "lib", "libhbmcopy.so")
+    if not os.path.exists(path):
+        return None
+    import torch  # noqa: F401  (the probe binds to torch's HIP runtime)
+    L = C.CDLL(path)
+    L.hbm_probe.restype = C.c_int
+    L.hbm_probe.argtypes = [C.c_size_t, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+    cp, rd = C.c_float(), C.c_float()
+    if L.hbm_probe(1 << 30, 10, C.byref(cp), C.byref(rd)) != 0:
+        return None
+    return {"copy_dwordx4": round(cp.value, 1), "read_dwordx4": round(rd.value, 1)}
+
+
+def source_hash():
+    """Hash of the kernel sources + ABI header: tags the committed PMC traffic so
+    a changed kernel never reports stale bytes."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "ggml-cuda-experiments_amd", "csrc")
+    for f in sorted(os.listdir(csrc)) + ["../../include/fattn.h"]:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def committed_traffic(workload, kernel):
+    """PMC traffic (profiles/traffic_*.json, tools/pmc_summary.py --traffic) for
+    this workload, only if it was measured on this exact kernel plan (describe
+    string) and kernel sources (source_hash); else None."""
+    import glob
+    for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json")), reverse=True):
+        try:
+            tj = json.load(open(tf))
+        except (OSError, ValueError):
+            continue
+        if (tj.get("workload") == workload and tj.get("plan") == kernel and
+                tj.get("source_hash") == source_hash()):
+            return tj.get("hbm_bytes_per_launch")
+    return None
+
+
+def cpu_baseline_prefill(rows=256):
+    """Prefill-shape CPU baseline (one head timed, extrapolation
+    labelled): the reference's own mulmat_cpu / softmax (src/utils.h:5-49,
+    oracle/_ref; the restated oracle when that library is absent) for ONE head
+    of the prefill shape (N = 4096 keys, D = 128) over `rows` of its 4096 query
+    rows, single thread; scaled linearly to 4096 rows x 32 heads."""
+    from oracle import oracle as orc
+    D, N, NQ, H = 128, 4096, 4096, 32
+    impl = "ref" if orc.ref_available() else "oracle"
+    rng = np.random.default_rng(7)
+    q = (1 - 2 * rng.random((rows, D), dtype=np.float32)).astype(np.float32)
+    k = (1 - 2 * rng.random((N, D), dtype=np.float32)).astype(np.float32)
+    v = (1 - 2 * rng.random((N, D), dtype=np.float32)).astype(np.float32)
+    m = (1 - 2 * rng.random(N, dtype=np.float32)).astype(np.float32)
+    t0 = time.perf_counter()
+    s = orc.mulmat_f32(q, k, m, rows, N, D, 1.0 / np.sqrt(np.float32(D)), True, impl=impl)
+    p = orc.softmax(s, N, rows, impl=impl)
+    orc.mulmat_f32(p, v, None, rows, D, N, 1.0, False, impl=impl)
+    dt = time.perf_counter() - t0
+    flops = 4 * rows * N * D
+    full_s = dt * (NQ / rows) * H
+    return {"value": round(flops / dt / 1e9, 4), "unit": "GFLOP/s", "cores": 1,
+            "kind": "reference" if impl == "ref" else "port",
+            "sample": f"1 head x {rows} of 4096 query rows x 4096 keys x D 128 (src/utils.h mulmat_cpu (Q.K^T, "
+                      f"B transposed) + softmax + mulmat_cpu (P.V)), one thread, {dt:.2f} s; the mask row is "
+                      f"broadcast over rows as mulmat_cpu's f32 form does",
+            "extrapolated_full_prefill_s": round(full_s, 1),
+            "extrapolation": f"linear: x {NQ // rows} rows x {H} heads (not measured)"}
 
 
 def prefill_measure(dev, hip, evs, kvn="q8_0", causal=False, steps=5):
@@ -212,7 +271,8 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="auto", choices=["auto", "config3", "config5"],
                     help="auto: config3 on one GPU, config5 (head-sharded) on several")
-    ap.add_argument("--rotate", type=int, default=16, help="independent KV caches cycled through")
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="independent KV caches cycled through (0 = enough that one pass reads >= 512 MiB per rank)")
     ap.add_argument("--kv-type", default=None, choices=["q8_0", "q4_0", "f16"])
     ap.add_argument("--heads", type=int, default=None)
     ap.add_argument("--kv-heads", type=int, default=None)
@@ -246,6 +306,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-prefill", action="store_true", help="skip the prefill-shape MFMA measurement")
     ap.add_argument("--no-scale-ref", action="store_true", help="N=1: skip the config-5 strong-scaling reference")
     ap.add_argument("--no-copy-peak", action="store_true", help="skip the measured copy-kernel peak")
+    ap.add_argument("--dump-out", default="", help="rank 0 writes rotation 0's inputs and gathered output (.npz)")
     return ap.parse_args(argv)
 
 
@@ -298,8 +359,11 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
     Hkv = shape["kv_heads"] or H
     typ = fattn.TYPE_NAMES[shape["kv_type"]]
     rb = fattn.row_size(typ, D)
-    R = args.rotate
     sh = shard_heads(H, Hkv, world, rank)
+    # rotation sized by bytes: the caches one rank reads over a
+    # pass of the rotation exceed the 256 MiB Infinity Cache twice over, so a
+    # step never finds its KV on-die from the previous pass
+    R = args.rotate or max(16, -(-ROTATE_BYTES // (2 * sh.n_kv * N * rb)))
     g = torch.Generator(device=dev)
     g.manual_seed(1234)  # the same global problem on every rank; each reads only its slice
 
@@ -317,9 +381,14 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
         kv_sets.append(pair)
     q = torch.rand((1, NQ, H, D), generator=g, device=dev) * 2 - 1
     npad = (N + 63) // 64 * 64
-    mask = (torch.rand((NQ, npad), generator=g, device=dev) * 2 - 1).to(torch.float16)
-    if args.mask_live < 1.0:  # diagnostics: a padded cache, positions past the live fraction -inf
-        mask[:, int(args.mask_live * N):] = float("-inf")
+    # one mask per cache of the rotation too (config 5's 64 rows are 512 KB a step)
+    masks = []
+    for r in range(R):
+        mask = (torch.rand((NQ, npad), generator=g, device=dev) * 2 - 1).to(torch.float16)
+        if args.mask_live < 1.0:  # diagnostics: a padded cache, positions past the live fraction -inf
+            mask[:, int(args.mask_live * N):] = float("-inf")
+        masks.append(mask)
+    mask = masks[0]
     Hl = sh.n_heads
     outs = torch.empty((R, 1, NQ, Hl, D), dtype=torch.float32, device=dev)
 
@@ -334,7 +403,8 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
 
     def step(i, stream=None, ev=None):
         kvs = kv_sets[i % R]
-        att.retarget(k=kvs[0].data_ptr() + k_off, v=kvs[1].data_ptr() + v_off, dst=outs[i % R].data_ptr())
+        att.retarget(k=kvs[0].data_ptr() + k_off, v=kvs[1].data_ptr() + v_off, dst=outs[i % R].data_ptr(),
+                     mask=None if args.no_mask else masks[i % R].data_ptr())
         if ev is None:
             att(stream)
         else:
@@ -399,6 +469,13 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
     kern_ms_avg = f.value / K
 
     res = {"kernel": kname, "kernel_ms_avg": kern_ms_avg, "kernel_ms_median": kern_ms_median, "elapsed": elapsed}
+    if args.dump_out and rank == 0:
+        # rotation 0's inputs and the (gathered) output, for the multi-rank
+        # parity test (tests/test_rehearsal.py checks them against the oracle)
+        out0 = (full[0] if world > 1 else outs[0]).cpu().numpy()
+        np.savez(args.dump_out, q=q.cpu().numpy(), k=kv_sets[0][0].cpu().numpy(), v=kv_sets[0][1].cpu().numpy(),
+                 mask=masks[0].cpu().view(torch.int16).numpy().view(np.uint16), out=out0,
+                 shape=np.array([D, NQ, H, Hkv, N, typ, world]), kernel=np.array(kname))
     if world > 1:
         assert tuple(full.shape) == (R, 1, NQ, H, D)
         # 3) per-step cost of the gather, and kernel + gather per step (eager),
@@ -441,7 +518,7 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
     return res
 
 
-def roofline(res, args, traffic=None, copy_peak=None):
+def roofline(res, args, traffic=None, peaks=None):
     ach = res["rank_bytes"] / (res["kernel_ms_avg"] * 1e-3) / 1e9
     ach_tf = res["rank_flops"] / (res["kernel_ms_avg"] * 1e-3) / 1e12
     if res["rank_flops"] / res["rank_bytes"] > MFMA_F16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9):
@@ -450,9 +527,12 @@ def roofline(res, args, traffic=None, copy_peak=None):
     r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": res["kernel"],
          "frac_median_kernel": round(res["rank_bytes"] / (res["kernel_ms_median"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    if copy_peak:
-        r["peak_measured_copy"] = copy_peak
-        r["frac_of_measured_copy"] = round(ach / copy_peak, 4)
+    if peaks:
+        r["peak_measured_copy"] = peaks["copy_dwordx4"]
+        r["frac_of_measured_copy"] = round(ach / peaks["copy_dwordx4"], 4)
+        r["peak_measured_read"] = peaks["read_dwordx4"]
+        r["frac_of_measured_read"] = round(ach / peaks["read_dwordx4"], 4)
+        r["measured_peaks"] = "tools/hbm_copy.hip: dwordx4 copy (read + write bytes) and read stream, 1 GiB, median"
     return r
 
 
@@ -497,16 +577,8 @@ def main():
     res = run_decode(args, dev, shape, rank, world)
 
     if rank == 0:
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic_r02.json")
-        if os.path.exists(tf):
-            try:
-                tj = json.load(open(tf))
-                if tj.get("workload") == res["workload"] and world == 1:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        copy_peak = None if args.no_copy_peak or world > 1 else measured_copy_peak(dev)
+        traffic = committed_traffic(res["workload"], res["kernel"]) if world == 1 else None
+        peaks = None if args.no_copy_peak or world > 1 else measured_hbm_peaks()
         sh = res["shard"]
         K = args.steps
         value = res["job_bytes"] * K / res["elapsed"] / 1e9
@@ -534,7 +606,8 @@ def main():
             "kernel_ms_median": round(res["kernel_ms_median"], 5),
             "kernel_timing": "avg: HIP events around the timed graph replay on the launch stream, / steps; "
                              "median: per-launch HIP events, eager",
-            "roofline": roofline(res, args, traffic, copy_peak),
+            "roofline": roofline(res, args, traffic, peaks),
+            "source_hash": source_hash(),
         }
         if world > 1:
             if REHEARSE:
@@ -563,6 +636,8 @@ def main():
         if not args.no_cpu_baseline and shape["n_q"] == 1:  # kernel_test.h's CPU path is one query row
             threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads)
+            if "prefill" in line:
+                line["prefill"]["cpu_baseline"] = cpu_baseline_prefill()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -50,15 +50,17 @@ std::atomic<int> g_opt_split_spw{0};
 std::atomic<int> g_opt_split_nbuf{0};
 std::atomic<int> g_opt_pf{0};  // 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_pf_stagger{2};
-std::atomic<int> g_opt_mq_min_rows{256};  // multi-query kernel from this many packed rows per kv head (>= 32)
+constexpr int kMqMinRowsDefault = 64;
+std::atomic<int> g_opt_mq_min_rows{kMqMinRowsDefault};  // multi-query kernel from this many packed rows per kv head (>= 32)
 std::atomic<int> g_opt_pf_no_skip{0};     // 1: masked prefill without the live-block pre-pass (FATTN_OPT_PF_SKIP)
 std::atomic<int> g_opt_split_prio{0};     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
 std::atomic<int> g_opt_no_wave_merge{0};  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
-std::atomic<int> g_opt_split_waves{0};
-std::atomic<int> g_opt_split_no_skip{0};
+std::atomic<int> g_opt_split_waves{0};      // split kernel waves per workgroup (FATTN_OPT_SPLIT_WAVES), 0 = planner
+std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
+std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
-std::atomic<uint32_t> g_epoch{0};  // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
+std::atomic<uint32_t> g_epoch{0};
 
 inline bool is_quant(int t) { return t == FATTN_TYPE_Q8_0 || t == FATTN_TYPE_Q4_0; }
 inline int type_size_elem(int t) { return t == FATTN_TYPE_F32 ? 4 : t == FATTN_TYPE_F16 ? 2 : 0; }
@@ -253,13 +255,18 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     }
     nch = std::max<int64_t>(1, std::min<int64_t>(nch, tiles));
     int64_t tpc = (tiles + nch - 1) / nch;
-    for (;;) {  // the merge takes at most 16 chunks for 16-row subtiles
+    // the chunk partials merge in a second launch (one wave per packed row,
+    // at most 64 chunks: one (m, l) pair per lane); FATTN_OPT_SPLIT_MERGE = 1:
+    // in the tile's last-arriving workgroup (at most 16 chunks per 16-row subtile)
+    const bool fused = g_opt_split_fused_merge != 0;
+    for (;;) {
         nch = (tiles + tpc - 1) / tpc;
-        if (nch == 1 || combine_ok(nch, kRows, pl.D)) break;
+        if (nch == 1 || (fused ? combine_ok(nch, kRows, pl.D) : nch <= kWaveMergeParts)) break;
         tpc++;
     }
     a.chunk_len = (int)(tpc * kStep);
     a.n_chunks = (int)nch;
+    a.merge_launch = (nch > 1 && !fused) ? 1 : 0;
     a.ncp = 1;
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     a.nbuf = 0;
@@ -271,6 +278,47 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
         pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
         pl.ml_bytes = (subs * a.n_chunks * kRows * 2 * sizeof(float) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + subs * a.n_chunks * kRows * pl.D * 4;
+    } else {
+        pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
+    }
+    return FATTN_OK;
+}
+
+// Batched-decode sizing: one 8-wave workgroup (64 packed rows, 134 KiB of
+// LDS) per CU; the KV sequence of each (kv head x 64-row tile) splits into
+// chunks of whole 128-key tiles until the workgroups cover the CUs (at most
+// 64 chunks: the merge launch takes one (m, l) pair per lane).
+int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
+    SplitArgs& a = pl.a;
+    const int64_t tiles = (N + kBdKeys - 1) / kBdKeys;
+    int64_t nch;
+    if (kv_chunk > 0) {
+        nch = (N + kv_chunk - 1) / kv_chunk;
+    } else {
+        nch = (pl.cus + Y * S - 1) / (Y * S);
+    }
+    nch = std::max<int64_t>(1, std::min<int64_t>(nch, tiles));
+    int64_t tpc = (tiles + nch - 1) / nch;
+    nch = (tiles + tpc - 1) / tpc;
+    while (nch > kWaveMergeParts) {
+        tpc++;
+        nch = (tiles + tpc - 1) / tpc;
+    }
+    a.chunk_len = (int)(tpc * kBdKeys);
+    a.n_chunks = (int)nch;
+    a.ncp = 1;
+    while (a.ncp < a.n_chunks) a.ncp <<= 1;
+    a.merge_launch = nch > 1 ? 1 : 0;
+    a.nbuf = 0;
+    a.wave_bytes = 0;
+    pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? BdCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
+    pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
+    if (nch > 1) {
+        // [(m, l) pairs][O partials]: [S][Y][chunks][64 rows]
+        const size_t slots = (size_t)S * Y * nch * kBdRows;
+        pl.cnt_bytes = 0;
+        pl.ml_bytes = (slots * 2 * sizeof(float) + 255) / 256 * 256;
+        pl.ws_bytes = pl.ml_bytes + slots * pl.D * 4;
     } else {
         pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
     }
@@ -390,18 +438,6 @@ int make_plan(const fattn_params* p, Plan& pl) {
         // 256 rows per workgroup once that still gives one workgroup per CU
         const int64_t wg256 = Hkv * S * ((NQ * a.rk2 + 255) / 256);
         pl.nw = g_opt_mq_rpw ? (g_opt_mq_rpw == 32 ? 8 : 4) : wg256 >= pl.cus ? 8 : 4;
-        // ... and only when its tiles need at most 4 KV chunks to fill the chip:
-        // with more, its last-arriver merge of 64/256-row tiles costs more than
-        // the split kernel's 16-row re-reads plus second-launch merge (32/8
-        // heads, n_q = 64: 46.2 vs 28.6 us; 8 heads x N = 8192, n_q = 256: 59.8
-        // vs 44.1; n_q = 128: 50.8 vs 45.6; 32 heads, n_q = 256, 4 chunks: mq
-        // 76.2 vs 89.3, profiles/r02_merge/mq_vs_split.txt)
-        const int64_t ymq = Hkv * S * ((NQ * a.rk2 + (pl.nw == 8 ? 255 : 63)) / (pl.nw == 8 ? 256 : 64));
-        const int64_t want = pl.nw == 8 ? pl.cus : 2 * pl.cus;
-        // (automatic mode only: a threshold or tile size set by FATTN_OPT_MQ_*
-        // or a forced chunk keeps the multi-query kernel)
-        if (g_opt_mq_min_rows == 256 && !g_opt_mq_rpw && p->kv_chunk <= 0 && (want + ymq - 1) / ymq > 4)
-            pl.mq = false;
     }
     if (pl.mq) {
         a.R = a.rk2;
@@ -426,8 +462,23 @@ int make_plan(const fattn_params* p, Plan& pl) {
         a.QPT = kPfRows / a.R;
         a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
     }
+    // batched decode (config 5: 64 query rows per kv head): 64-row workgroups
+    // over 128-key tiles, the KV split over workgroups to fill the chip, the
+    // chunk partials merged in a second launch
+    pl.bd = false;
+    if (!pl.pf && g_opt_bd != 1 && mq_ok && D == 128 && N % kStep == 0 &&
+        (g_opt_bd == 2 || NQ * a.rk2 >= kBdRows)) {
+        pl.bd = true;
+        pl.mq = false;
+        a.R = a.rk2;
+        a.R_inv = 1.0f / (float)a.R;
+        a.n_hsub = 1;
+        a.QPT = kBdRows / a.R;
+        a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
+    }
     const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
     if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
+    if (pl.bd) return size_bd(pl, p->kv_chunk, Y, S, N);
     if (pl.pf) {
         a.chunk_len = (int)N;
         a.pf_stagger = g_opt_pf_stagger;
@@ -495,13 +546,9 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 7) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_stagger = value;
             return FATTN_OK;
-        case FATTN_OPT_PF_WAVES:  // removed experiments: only the default remains
-            return value == 8 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
-        case FATTN_OPT_PF_DEQUANT:
-            return value == 0 || value == 1 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_MQ_MIN_ROWS:
-            if (value < 32) return FATTN_ERR_INVALID_ARG;
-            g_opt_mq_min_rows = value;
+            if (value != 0 && value < 32) return FATTN_ERR_INVALID_ARG;
+            g_opt_mq_min_rows = value ? value : kMqMinRowsDefault;
             return FATTN_OK;
         case FATTN_OPT_PF_SKIP:
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
@@ -519,19 +566,10 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
             g_opt_split_fused_merge = value;
             return FATTN_OK;
-        case FATTN_OPT_PF_PIPE:  // removed experiments: only the lockstep kernel remains
-            return value == 0 || value == 1 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_SPLIT_STEPS:
             if (value < 0 || value > 64) return FATTN_ERR_INVALID_ARG;
             g_opt_split_spw = value;
             return FATTN_OK;
-        case FATTN_OPT_DEC:  // the loader-wave decode kernel was removed (slower)
-            return value == 0 || value == 1 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
-        case FATTN_OPT_DEC_LOADERS:
-        case FATTN_OPT_DEC_COMPUTE:
-        case FATTN_OPT_DEC_AHEAD:
-        case FATTN_OPT_DEC_DIAG:
-            return value == 0 ? FATTN_OK : FATTN_ERR_INVALID_ARG;
         case FATTN_OPT_SPLIT_SKIP:
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
             g_opt_split_no_skip = value;
@@ -539,6 +577,10 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_SPLIT_WAVES:
             if (value != 0 && value != 4 && value != 8 && value != 16) return FATTN_ERR_INVALID_ARG;
             g_opt_split_waves = value;
+            return FATTN_OK;
+        case FATTN_OPT_BD:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_bd = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:
             if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
@@ -599,8 +641,12 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
     if (pl.pf)
         std::snprintf(kern, sizeof kern, "%sfattn_pf_kernel<%s,D%d,%s>", pl.pf_flags ? "pf_mask_flags_kernel + " : "",
                       tn(pl.kt), pl.D, hm);
+    else if (pl.bd)
+        std::snprintf(kern, sizeof kern, "fattn_bd_kernel<%s,D%d,%s>%s", tn(pl.kt), pl.D, hm,
+                      pl.a.merge_launch ? " + fattn_bd_merge_kernel" : "");
     else if (pl.mq)
-        std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>", tn(pl.kt), pl.D, pl.nw, hm);
+        std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,
+                      pl.a.merge_launch ? " + fattn_mq_merge_kernel" : "");
     else
         std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>%s", tn(pl.kt), tn(pl.vt),
                       pl.D, pl.gran, hm, pl.nwv, pl.a.merge_launch ? " + fattn_merge_kernel" : "");

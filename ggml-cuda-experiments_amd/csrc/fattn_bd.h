@@ -1,0 +1,522 @@
+// fattn_bd.h -- batched decode over ggml-quantised KV for gfx950: 64 packed
+// (query row x q-head) rows per kv head and workgroup (BASELINE config 5: 64
+// query rows x 32 heads over a 4096-position Q8_0 cache, and its per-GPU head
+// shards).
+//
+// Replaces flash_attn_ext_f16<D,Q,C> (src/flash-llama.h:5-438; its 16-row Q
+// tiles read K/V once per 16 rows) for the batched-decode shape.  Same math as
+// the other kernels (scale * q.k + mask, online softmax, P.V; f16 operands,
+// f32 accumulation; chunk partials merged by the fa_reduce LSE rule,
+// src/flash_row_float.h:415-472):
+//
+//  * one workgroup = 8 waves = 64 packed rows of one kv head x one KV chunk;
+//    wave w takes row group rg = w & 1 (32 rows: the 32 MFMA columns) and key
+//    quarter kq = w >> 1 of every 128-key tile, so each K / V byte of the tile
+//    is read from HBM once for all 64 rows;
+//  * HBM -> LDS: the tile's raw ggml K and V rows by buffer_load ... lds (1-KiB
+//    wave instructions dealt round-robin over the waves), three raw tiles in
+//    the ring, two in flight beyond the one being computed;
+//  * K: dequantised on the LDS -> VGPR hop straight into the A operand of
+//    S^T = K.Q^T (v_mfma_f32_32x32x16_f16; lane = key, 8 dims): h(q * d), one f16
+//    rounding, exactly the oracle's (src/utils.h:10-11);
+//  * V: the workgroup dequantises the tile once into an f16 image (the prefill
+//    kernel's [dim block][key][64 B] swizzled layout) read back transposed by
+//    ds_read_b64_tr_b16 as the A operand of O^T = V^T.P^T, with P^T the S^T
+//    accumulator itself converted to f16 (no lane movement);
+//  * the mask: each lane's 16 keys of its row per tile by four 16-B buffer
+//    loads into registers, one tile ahead (LDS holds only K/V);
+//  * online softmax in the log2 domain with the deferred max (T13); a wave
+//    whose 32 x 32 mask block is -inf everywhere skips the block (exact);
+//  * epilogue: the four key quarters of each row group merge through LDS;
+//    one chunk: normalised dst rows; several: (O, m, l) partials merged by
+//    fattn_bd_merge_kernel in a second launch.
+//
+// LDS (D = 128, Q8_0): [0, 32 KiB) the V image; then 3 raw tiles
+// [K rows | V rows] of 17 KiB each.  134 KiB: one workgroup per CU, two waves
+// per SIMD.
+#pragma once
+
+#include "fattn_pf.h"
+
+namespace fattn {
+
+constexpr int kBdWaves = 8;
+constexpr int kBdRowsW = 32;                   // packed rows per wave (MFMA columns)
+constexpr int kBdRows = 2 * kBdRowsW;          // per workgroup (two row groups)
+constexpr int kBdKeys = 128;                   // keys per tile (four 32-key quarters)
+
+template <int KT, int D>
+struct BdCfg {
+    static_assert(D == 128, "four 32-dim blocks: one ggml block per V image block");
+    static constexpr int rowB = row_bytes<KT, D>();
+    static constexpr int kvRaw = kBdKeys * rowB;                 // raw K (or V) bytes per tile
+    static constexpr int rawBytes = (2 * kvRaw + 15) / 16 * 16;  // [K rows | V rows]
+    static constexpr int nRaw = 3;
+    static constexpr int img = kBdKeys * D * 2;                  // f16 V image
+    static constexpr int rawOff = img;
+    static constexpr int ringEnd = rawOff + nRaw * rawBytes;
+    static constexpr int NI = (kvRaw + 1023) / 1024;             // 1-KiB DMA instructions per K (or V) tile
+    // instructions j = 0 .. 2 NI - 1 (K then V) go to wave j % 8
+    static constexpr int ni_wave(int w) { return (2 * NI - w + kBdWaves - 1) / kBdWaves; }
+    static constexpr int NM = 4;                                 // mask loads per lane and tile
+    // epilogue: every wave parks its (O, m, l) rows here, [4 key quarters][64
+    // rows][D + 4] f32 (+16 B per row: the accumulator-layout writes are
+    // conflict-free) then [4][64] (m, l)
+    static constexpr int parkStride = D + 4;
+    static constexpr int parkMl = 4 * kBdRows * parkStride * 4;
+    static constexpr int parkBytes = parkMl + 4 * kBdRows * 8;
+    static constexpr int ldsBytes = ringEnd > parkBytes ? ringEnd : parkBytes;
+    // Q staged as f32 rows [64][D] in the V image's place before the first tile
+    static_assert(kBdRows * D * 4 <= img && D * 4 / 16 == 32, "Q rows of 32 16-B chunks in the image's place");
+    static_assert(ldsBytes <= 163840, "");
+};
+
+template <int KT, int D>
+__device__ __forceinline__ void bd_issue(const StepSrc& rs, int n0, uint32_t lds, int wave, int lane) {
+#ifdef FATTN_MQ_NOMEM
+    return;  // diagnostic build only
+#endif
+    using C = BdCfg<KT, D>;
+    for (int j = wave; j < 2 * C::NI; j += kBdWaves) {  // wave-uniform
+        const bool is_v = j >= C::NI;
+        const int i = is_v ? j - C::NI : j;
+        const int byte = i * 1024 + lane * 16;
+        // pieces past the tile's bytes stay idle (the instruction still counts)
+        if (C::kvRaw % 1024 == 0 || byte < C::kvRaw)
+            dma<16, kDecodeNT>(is_v ? rs.v : rs.k, lds + (is_v ? C::kvRaw : 0) + i * 1024,
+                               (uint32_t)n0 * C::rowB + byte);
+    }
+}
+
+// counted wait: the awaited group is done once at most the `nraw` raw-tile
+// DMA groups and `nmask` mask groups this wave issued after it are still in
+// flight (vmcnt counts in issue order)
+template <int KT, int D, bool HM, int W>
+__device__ __forceinline__ void bd_vm_wait_w(int nraw, int nmask) {
+    constexpr int NI = BdCfg<KT, D>::ni_wave(W);
+    constexpr int NM = HM ? BdCfg<KT, D>::NM : 0;
+    switch (nraw * 4 + nmask) {
+        case 0: wait_vmcnt_c<0>(); break;
+        case 1: wait_vmcnt_c<NM>(); break;
+        case 2: wait_vmcnt_c<2 * NM>(); break;
+        case 4: wait_vmcnt_c<NI>(); break;
+        case 5: wait_vmcnt_c<NI + NM>(); break;
+        case 6: wait_vmcnt_c<NI + 2 * NM>(); break;
+        case 8: wait_vmcnt_c<2 * NI>(); break;
+        case 9: wait_vmcnt_c<2 * NI + NM>(); break;
+        default: wait_vmcnt_c<2 * NI + 2 * NM>(); break;  // 10
+    }
+}
+template <int KT, int D, bool HM>
+__device__ __forceinline__ void bd_vm_wait(int wave, int nraw, int nmask) {
+    switch (wave) {
+        case 0: bd_vm_wait_w<KT, D, HM, 0>(nraw, nmask); break;
+        case 1: bd_vm_wait_w<KT, D, HM, 1>(nraw, nmask); break;
+        case 2: bd_vm_wait_w<KT, D, HM, 2>(nraw, nmask); break;
+        case 3: bd_vm_wait_w<KT, D, HM, 3>(nraw, nmask); break;
+        case 4: bd_vm_wait_w<KT, D, HM, 4>(nraw, nmask); break;
+        case 5: bd_vm_wait_w<KT, D, HM, 5>(nraw, nmask); break;
+        case 6: bd_vm_wait_w<KT, D, HM, 6>(nraw, nmask); break;
+        default: bd_vm_wait_w<KT, D, HM, 7>(nraw, nmask); break;
+    }
+}
+
+// raw V of a tile -> the f16 V image: wave w dequantises half h = w & 1 of
+// block b = w >> 1 of keys lane and 64 + lane (prefill kernel's V layout:
+// [4 dim blocks][128 keys][64 B], chunk c of key r at c ^ ((r >> 2) & 3))
+template <int KT, int D>
+__device__ __forceinline__ void bd_dequant_v(const uint8_t* vraw, uint8_t* v16, int wave, int lane) {
+#ifdef FATTN_MQ_NODEQ
+    return;  // diagnostic build only
+#endif
+    const int b = wave >> 1, h = wave & 1;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const int r = 64 * i + lane;
+        u32x4 cv[2];
+        dequant_half<KT, D>(vraw, r, b, h, cv);
+        uint8_t* vd = v16 + b * (kBdKeys * 64) + r * 64;
+        const int sv = (r >> 2) & 3;
+        *(u32x4*)(vd + ((2 * h) ^ sv) * 16) = cv[0];
+        *(u32x4*)(vd + ((2 * h + 1) ^ sv) * 16) = cv[1];
+    }
+}
+
+// A operand of S^T = K.Q^T for 16-dim k-step kk: key row `row` of the raw
+// tile, dims 16 kk + 8 h .. + 8, dequantised h(q * d)
+template <int KT, int D>
+__device__ __forceinline__ f16x8 bd_k_operand(const uint8_t* kraw, int row, int h, int kk, uint32_t dbits) {
+    constexpr int RB = row_bytes<KT, D>();
+    constexpr int BB = TypeInfo<KT>::block_bytes;
+    const int b = kk >> 1;
+    const f16x2 d = as_h2(dbits);
+    f16x2 h0, h1, h2, h3;
+    if constexpr (KT == FATTN_TYPE_Q8_0) {
+        // qs bytes 16 (kk & 1) + 8 h .. + 8 of block b (row * RB is 8-aligned)
+        const uint32_t off = row * RB + BB * b + 2 + 16 * (kk & 1) + 8 * h;
+        u32x2 raw;
+        switch ((BB * b + 2 + 16 * (kk & 1)) & 7) {  // kk is unrolled: compile-time
+            case 0: raw = read8_at<0>(kraw, off); break;
+            case 2: raw = read8_at<2>(kraw, off); break;
+            case 4: raw = read8_at<4>(kraw, off); break;
+            default: raw = read8_at<6>(kraw, off); break;
+        }
+        i8x4_to_h2x2(raw.x, h0, h1);
+        i8x4_to_h2x2(raw.y, h2, h3);
+    } else {  // Q4_0: elements 0-15 low nibbles of qs bytes 0-15, 16-31 high nibbles
+        const uint32_t off = row * RB + BB * b + 2 + 8 * h;
+        u32x2 raw;
+        switch ((BB * b + 2) & 7) {
+            case 0: raw = read8_at<0>(kraw, off); break;
+            case 2: raw = read8_at<2>(kraw, off); break;
+            case 4: raw = read8_at<4>(kraw, off); break;
+            default: raw = read8_at<6>(kraw, off); break;
+        }
+        const uint32_t sh = 4 * (kk & 1);
+        u4x4_to_h2x2((raw.x >> sh) & 0x0F0F0F0Fu, h0, h1);
+        u4x4_to_h2x2((raw.y >> sh) & 0x0F0F0F0Fu, h2, h3);
+    }
+    h0 *= d; h1 *= d; h2 *= d; h3 *= d;
+    f16x8 r;
+    r.s01 = h0; r.s23 = h1; r.s45 = h2; r.s67 = h3;
+    return r;
+}
+
+template <int KT, int D, bool HM>
+__global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const SplitArgs a) {
+    using C = BdCfg<KT, D>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NK = D / 16;   // 16-dim k-steps of S^T = K.Q^T
+    constexpr int NDB = D / 32;  // 32-dim blocks of O^T (= ggml blocks of a row)
+    constexpr float kNegInf = -__builtin_inff();
+    constexpr float kDeferLog2 = 8.0f;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rg = wave & 1, kq = wave >> 1;  // row group, key quarter
+    const int h = lane >> 5;                  // k-group of the MFMA operands
+    const int c32 = lane & 31;                // MFMA column: packed row 32 rg + c32; MFMA row: key 32 kq + c32
+
+    // ---- tile decode: y -> (kv head, 64-row query tile); R = rk2
+    const int chunk = blockIdx.x;
+    const int y = blockIdx.y;
+    const int iq3 = blockIdx.z;
+    int qt = 0, ik2 = y, ik3 = iq3;
+    if (a.n_qt != 1) {
+        qt = y % a.n_qt;
+        ik2 = y / a.n_qt;
+    }
+    if (a.rk3 != 1) ik3 = iq3 / a.rk3;
+    const int p = kBdRowsW * rg + c32;  // packed row of the workgroup tile (its q head only
+    const int iq1 = qt * a.QPT + div_R(a, p);  // matters to Q and dst, both addressed per row below)
+    const bool row_ok = iq1 < a.NQ;
+
+    // ---- this workgroup's KV chunk: 128-key tiles (N % 32 == 0; a tile's
+    // quarters past the chunk are idle)
+    const int c_lo = chunk * a.chunk_len;
+    const int c_hi = min(a.N, c_lo + a.chunk_len);
+    const int ntiles = c_hi > c_lo ? (c_hi - c_lo + kBdKeys - 1) / kBdKeys : 0;
+
+    StepSrc rs;
+    rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
+    rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
+    rs.m = make_srd(a.mask, HM ? a.m_span : 0);
+    const uint32_t lds0 = lds_addr(smem);
+    auto raw_lds = [&](int s) { return lds0 + C::rawOff + (s % C::nRaw) * C::rawBytes; };
+    auto raw_ptr = [&](int s) { return smem + C::rawOff + (s % C::nRaw) * C::rawBytes; };
+
+    // ---- Q: the workgroup's 64 rows (f32, D per row) copied HBM -> LDS into the
+    // V image's place by 1-KiB LDS-DMA instructions (2 rows each, dealt over
+    // the waves); each wave then reads its rows' Q^T operands from there.
+    // Rows past n_q come from past the descriptor: zeros.
+    const i32x4 qs = make_srd(a.q + (int64_t)iq3 * a.q_nb3, a.q_span);
+    {
+        constexpr int kQInst = kBdRows * D * 4 / 1024;  // 32 at D = 128
+        static_assert(kQInst % kBdWaves == 0, "");
+#pragma unroll
+        for (int i = 0; i < kQInst / kBdWaves; i++) {
+            const int j = wave + kBdWaves * i;              // instruction: rows 2j, 2j + 1
+            const int pr = 2 * j + (lane >> 5);              // packed row of this lane's 16 B
+            const int rq = div_R(a, pr);
+            const int q1 = qt * a.QPT + rq, q2 = ik2 * a.rk2 + (pr - rq * a.R);
+            // LDS chunk (lane & 31) of row pr holds the row's chunk (lane & 31) ^ (pr & 31):
+            // the operand reads below (32 rows at once) then spread over the banks
+            const uint32_t off = q1 < a.NQ ? (uint32_t)q1 * (uint32_t)a.q_nb1 + (uint32_t)q2 * (uint32_t)a.q_nb2 +
+                                                 (((lane & 31) ^ (pr & 31)) * 16)
+                                           : a.q_span;
+            dma<16>(qs, lds0 + j * 1024, off);
+        }
+    }
+    constexpr int kQInstW = kBdRows * D * 4 / 1024 / kBdWaves;  // Q DMA instructions per wave
+
+    // ---- mask: this lane's row, keys 32 kq + 8 u + 4 h + 0..3 of a tile, from
+    // four 16-B loads (keys 32 kq + 8 u .. + 8; the lane keeps half h)
+    const uint32_t mrow = row_ok ? (uint32_t)iq1 * (uint32_t)a.m_nb1 : a.m_span;
+    auto mask_issue = [&](int s, u32x4 (&mk)[4]) {
+        if constexpr (HM) {
+            const uint32_t n2 = (uint32_t)(c_lo + s * kBdKeys + 32 * kq) * 2;
+#pragma unroll
+            for (int u = 0; u < 4; u++) mk[u] = ld_buf(rs.m, mrow == a.m_span ? a.m_span : mrow + n2 + 16 * u);
+        }
+    };
+
+    // per-lane V^T gather bases (prefill kernel's, 128-key image):
+    // 16-lane group (h, dh), lane gi: key 32 kq + 16 q + 8 e + 4 h + gi / 4
+    const int gi = lane & 15, dh = (lane >> 4) & 1;
+    uint32_t vbase[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int row = 8 * e + 4 * h + (gi >> 2);
+        const int ch = (2 * dh + ((gi & 3) >> 1)) ^ ((h + 2 * e) & 3);
+        vbase[e] = kq * 2048 + row * 64 + ch * 16 + (gi & 1) * 8;
+    }
+
+    // ---- this wave's issue order: prologue raw 0 | raw 1 | mask 0, then per
+    // tile s: raw s + 2 (after the first barrier) | mask s + 1 (once mask s has
+    // been read).  So at the top of tile s, mask s - 1 (s >= 1), raw s + 1 and
+    // mask s were issued after raw s; after the second barrier only raw s + 2
+    // was issued after mask s.
+    if (ntiles > 0) bd_issue<KT, D>(rs, c_lo, raw_lds(0), wave, lane);
+    if (ntiles > 1) bd_issue<KT, D>(rs, c_lo + kBdKeys, raw_lds(1), wave, lane);
+    u32x4 mk[4] = {};
+    if (ntiles > 0) mask_issue(0, mk);
+
+    float m_run = kNegInf;    // reference max (log2 domain) of this lane's row
+    f32x2 l2 = {0.0f, 0.0f};  // this lane's partial row sums (16 of every 32 keys)
+    f32x16 o[NDB];
+#pragma unroll
+    for (int db = 0; db < NDB; db++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) o[db][j] = 0.0f;
+    }
+    const float log2e = 1.4426950408889634f;
+    const float scale = a.scale;
+
+    // Q landed (raw 0, raw 1 and mask 0 may fly on); every wave's Q pieces in LDS
+    {
+        const int n1 = ntiles > 1 ? 1 : 0, n0 = ntiles > 0 ? 1 : 0;
+        bd_vm_wait<KT, D, HM>(wave, n0 + n1, n0);
+    }
+    __syncthreads();
+    // Q^T operands (B of S^T = K.Q^T): dims 16 kk + 8 h .. + 8 of this lane's
+    // row, rounded to f16 like src/utils.h:10
+    f16x8 qop[NK];
+#pragma unroll
+    for (int kk = 0; kk < NK; kk++) {
+        const float* qr = (const float*)smem + p * D;
+        const f32x4 x0 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h) ^ (p & 31)));
+        const f32x4 x1 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h + 1) ^ (p & 31)));
+        f16x8 hq;
+        hq.s0 = (f16)x0.x; hq.s1 = (f16)x0.y; hq.s2 = (f16)x0.z; hq.s3 = (f16)x0.w;
+        hq.s4 = (f16)x1.x; hq.s5 = (f16)x1.y; hq.s6 = (f16)x1.z; hq.s7 = (f16)x1.w;
+        qop[kk] = hq;
+    }
+    (void)kQInstW;
+
+    for (int s = 0; s < ntiles; s++) {
+        // raw s landed (mask s - 1 (s >= 1), raw s + 1, mask s may fly on)
+        bd_vm_wait<KT, D, HM>(wave, s + 1 < ntiles ? 1 : 0, s > 0 ? 2 : 1);
+        // every wave's pieces of raw s landed; every wave is done with tile
+        // s - 1 (the V image and raw s - 1's slot are free)
+        __syncthreads();
+        if (s + 2 < ntiles) bd_issue<KT, D>(rs, c_lo + (s + 2) * kBdKeys, raw_lds(s + 2), wave, lane);
+        const uint8_t* kraw = raw_ptr(s);
+        bd_dequant_v<KT, D>(kraw + C::kvRaw, smem, wave, lane);
+        // the V image is complete
+        __syncthreads();
+        // this lane's mask values of tile s (keys 8 u + 4 h + 0..3 of the
+        // quarter), then mask s + 1 into the same registers
+        u32x2 mh[4];
+        uint32_t open = 1;  // any key not at -inf (f16 0xFC00)
+        if constexpr (HM) {
+            bd_vm_wait<KT, D, HM>(wave, s + 2 < ntiles ? 1 : 0, 0);
+            open = 0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                reg_fence(mk[u]);
+                mh[u] = h ? u32x2{mk[u].z, mk[u].w} : u32x2{mk[u].x, mk[u].y};
+                open |= (mh[u].x ^ 0xFC00FC00u) | (mh[u].y ^ 0xFC00FC00u);
+            }
+            if (s + 1 < ntiles) mask_issue(s + 1, mk);
+        }
+#ifdef FATTN_MQ_NOCOMPUTE
+        continue;  // diagnostic build only: copies, V dequant and barriers
+#endif
+        // this wave's 32 keys past the chunk: nothing to compute (N % 32 == 0)
+        if (c_lo + s * kBdKeys + 32 * kq >= c_hi) continue;
+        // a 32 x 32 block that is -inf for every valid row adds nothing (exact skip)
+        if (HM && __builtin_amdgcn_ballot_w64(open != 0 && row_ok) == 0) continue;
+
+        // -- S^T = K.Q^T for this wave's 32 keys: A from the raw K rows
+        const int krow = 32 * kq + c32;
+        const RowScales<KT, D> ks = row_scales<KT, D>(kraw + krow * C::rowB);
+        f32x16 st;
+#pragma unroll
+        for (int j = 0; j < 16; j++) st[j] = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < NK; kk++)
+            st = mfma32(bd_k_operand<KT, D>(kraw, krow, h, kk, scale_bcast(ks, kk >> 1)), qop[kk], st);
+
+        // -- u = scale * s + mask (natural units); element j = key 8 (j/4) + 4 h + j%4
+        float u[16];
+#pragma unroll
+        for (int uu = 0; uu < 4; uu++) {
+            if constexpr (HM) {
+                const f16x2 m01 = as_h2(mh[uu].x), m23 = as_h2(mh[uu].y);
+                u[4 * uu + 0] = fmaf(st[4 * uu + 0], scale, (float)m01.x);
+                u[4 * uu + 1] = fmaf(st[4 * uu + 1], scale, (float)m01.y);
+                u[4 * uu + 2] = fmaf(st[4 * uu + 2], scale, (float)m23.x);
+                u[4 * uu + 3] = fmaf(st[4 * uu + 3], scale, (float)m23.y);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; r++) u[4 * uu + r] = st[4 * uu + r] * scale;
+            }
+        }
+        float tmax = kNegInf;
+#pragma unroll
+        for (int j = 0; j < 16; j++) tmax = fmaxf(tmax, u[j]);
+        tmax = xor32_pair(tmax, true) * log2e;
+        // deferred max (cdna_hip_programming.md T13): the reference max moves
+        // only when the row's block max passes it by more than 2^8 in p
+        if (__builtin_amdgcn_ballot_w64(tmax > m_run + kDeferLog2)) {
+            const float m_new = fmaxf(m_run, tmax);
+            const float alpha = (m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run - m_new);
+            l2 *= alpha;
+#pragma unroll
+            for (int db = 0; db < NDB; db++) o[db] *= alpha;
+            m_run = m_new;
+        }
+        const float nm = (m_run == kNegInf) ? 0.0f : -m_run;
+        f16x8 pb[2];
+        {
+            float pv[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) pv[j] = __builtin_amdgcn_exp2f(fmaf(u[j], log2e, nm));
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) l2 += f32x2{pv[j], pv[j + 1]};
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                f16x8 x;
+                x.s0 = (f16)pv[8 * q]; x.s1 = (f16)pv[8 * q + 1]; x.s2 = (f16)pv[8 * q + 2]; x.s3 = (f16)pv[8 * q + 3];
+                x.s4 = (f16)pv[8 * q + 4]; x.s5 = (f16)pv[8 * q + 5]; x.s6 = (f16)pv[8 * q + 6]; x.s7 = (f16)pv[8 * q + 7];
+                pb[q] = x;
+            }
+        }
+
+        // -- O^T += V^T.P^T: k-step q covers keys 32 kq + 16 q + 8 (i/4) + 4 h + i%4
+        // (i = 0..7); V^T gathered from the image in that order
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+            u32x4 va[NDB];
+#pragma unroll
+            for (int db = 0; db < NDB; db++) {
+                const uint32_t off = db * (kBdKeys * 64) + q * 1024;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + vbase[0] + off));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + vbase[1] + off));
+                const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                va[db] = u32x4{a2.x, a2.y, b2.x, b2.y};
+            }
+#pragma unroll
+            for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[q], o[db]);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+    // ---- merge the four key quarters of each row.  Every wave parks its
+    // rows' (O, m, l) in LDS (accumulator layout -> [kq][row][D + 4]); then each
+    // of the 512 threads merges 16 dims of one row (fixed order, kq = 0..3) and
+    // stores them as 64 contiguous bytes, so every store instruction writes
+    // whole rows (row-per-lane stores from the accumulator layout issue 32
+    // lines per instruction: MI355X_MICROARCH.md, epilogue store tail)
+    const float l_own = xor32_pair(l2.x + l2.y, false);
+    __syncthreads();  // every wave is done with the tiles' LDS
+    {
+        float* pk = (float*)smem + (kq * kBdRows + p) * C::parkStride + 4 * h;
+#pragma unroll
+        for (int db = 0; db < NDB; db++) {
+#pragma unroll
+            for (int uu = 0; uu < 4; uu++)
+                *(f32x4*)(pk + 32 * db + 8 * uu) = f32x4{o[db][4 * uu], o[db][4 * uu + 1], o[db][4 * uu + 2],
+                                                         o[db][4 * uu + 3]};
+        }
+        if (h == 0) ((f32x2*)(smem + C::parkMl))[kq * kBdRows + p] = f32x2{m_run, l_own};
+    }
+    __syncthreads();
+    constexpr int kDpt = kBdRows * D / (kBdWaves * kWave);  // dims per thread: 16
+    const int pr = tid / (D / kDpt), c0 = (tid % (D / kDpt)) * kDpt;
+    const f32x2* pml = (const f32x2*)(smem + C::parkMl);
+    f32x2 mlk[4];
+    float M = kNegInf;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        mlk[k] = pml[k * kBdRows + pr];
+        M = fmaxf(M, mlk[k].x);
+    }
+    float L = 0.0f;
+    float acc[kDpt];
+#pragma unroll
+    for (int e = 0; e < kDpt; e++) acc[e] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float wk = (mlk[k].x == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mlk[k].x - M);
+        L += wk * mlk[k].y;
+        const float* src = (const float*)smem + (k * kBdRows + pr) * C::parkStride + c0;
+#pragma unroll
+        for (int e = 0; e < kDpt; e += 4) {
+            const f32x4 x = *(const f32x4*)(src + e);
+            acc[e] += wk * x.x;
+            acc[e + 1] += wk * x.y;
+            acc[e + 2] += wk * x.z;
+            acc[e + 3] += wk * x.w;
+        }
+    }
+    const int rq = div_R(a, pr);
+    const int q1 = qt * a.QPT + rq;
+    if (q1 >= a.NQ) return;
+    if (a.n_chunks == 1) {
+        const int q2 = ik2 * a.rk2 + (pr - rq * a.R);
+        float* out = a.dst + (((int64_t)iq3 * a.NQ + q1) * a.H + q2) * D + c0;
+        const float inv = 1.0f / L;  // fully masked row -> NaN like the reference
+#pragma unroll
+        for (int e = 0; e < kDpt; e += 4) {
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; r++) v[r] = L == 0.0f ? __builtin_nanf("") : acc[e + r] * inv;
+            *(f32x4*)(out + e) = v;
+        }
+        return;
+    }
+    // several chunks: the partial (O, m, l) of packed row pr for
+    // fattn_bd_merge_kernel, [tile][chunk][64 rows][D] and [..][64 rows][2] (the
+    // kernel boundary orders these stores before the merge's loads)
+    const int64_t slot = (((int64_t)iq3 * gridDim.y + y) * a.n_chunks + chunk) * kBdRows + pr;
+    float* po = a.ws_o + slot * D + c0;
+#pragma unroll
+    for (int e = 0; e < kDpt; e += 4) *(f32x4*)(po + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
+    if (c0 == 0) *(f32x2*)(a.ws_ml + 2 * slot) = f32x2{M, L};
+}
+
+// Second launch of a split batched-decode plan: one wave per (tile, packed
+// row) merges the row's chunk partials (merge_row_parts: the fa_reduce LSE
+// merge of src/flash_row_float.h:415-472 in fp32, fixed order) and writes the
+// normalised dst row.
+template <int D, int KIT>
+__global__ __launch_bounds__(256) void fattn_bd_merge_kernel(const SplitArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);  // packed row of the tile
+    const int y = blockIdx.y, iq3 = blockIdx.z;
+    int qt = 0, ik2 = y;
+    if (a.n_qt != 1) {
+        qt = y % a.n_qt;
+        ik2 = y / a.n_qt;
+    }
+    if (p >= min(a.QPT, a.NQ - qt * a.QPT) * a.R) return;
+    const int64_t slot0 = ((int64_t)iq3 * gridDim.y + y) * a.n_chunks * kBdRows + p;  // chunk 0's row
+    const int rq = div_R(a, p);
+    float* out = a.dst + (((int64_t)iq3 * a.NQ + qt * a.QPT + rq) * a.H + ik2 * a.rk2 + (p - rq * a.R)) * D;
+    merge_row_parts<D, KIT>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kBdRows * D,
+                            2 * kBdRows);
+}
+
+}  // namespace fattn

@@ -13,6 +13,7 @@
 #include "fattn_quant.h"
 #include "fattn_mq.h"
 #include "fattn_pf.h"
+#include "fattn_bd.h"
 #include "fattn_split.h"
 
 namespace fattn {
@@ -31,6 +32,7 @@ struct Plan {
     int nwv;  // split kernel: waves per workgroup (4, 8, 16)
     bool mq;  // multi-query kernel (fattn_mq.h)
     bool pf;  // prefill kernel (fattn_pf.h)
+    bool bd;  // batched-decode kernel (fattn_bd.h)
     bool pf_flags;          // masked prefill: live-block flags pre-pass (tile-range skipping)
     int nw;   // mq kernel: waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
 };
@@ -140,6 +142,17 @@ int launch_mq_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     auto kern = fattn_mq_kernel<KT, D, NW, HM>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         hipLaunchKernelGGL(kern, pl.grid, dim3(NW * kWave), pl.lds, st, pl.a);
+        if (pl.a.merge_launch) {
+            // the chunk partials of every 16-row subtile (4 per 64-row tile,
+            // 16 per 256-row tile) merge in a second launch
+            constexpr int SUBS = NW == 8 ? 16 : 4;
+            const dim3 g(kRows / 4, pl.grid.y * SUBS, pl.grid.z);
+            const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
+            if (need <= 2) hipLaunchKernelGGL((fattn_mq_merge_kernel<D, 2, SUBS>), g, dim3(256), 0, st, pl.a);
+            else if (need <= 4) hipLaunchKernelGGL((fattn_mq_merge_kernel<D, 4, SUBS>), g, dim3(256), 0, st, pl.a);
+            else if (need <= 8) hipLaunchKernelGGL((fattn_mq_merge_kernel<D, 8, SUBS>), g, dim3(256), 0, st, pl.a);
+            else hipLaunchKernelGGL((fattn_mq_merge_kernel<D, 16, SUBS>), g, dim3(256), 0, st, pl.a);
+        }
     });
 }
 
@@ -161,6 +174,27 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     });
 }
 
+template <int KT, bool HM>
+int launch_bd_hm(const Plan& pl, hipStream_t st, const Events& ev) {
+    auto kern = fattn_bd_kernel<KT, 128, HM>;
+    return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        hipLaunchKernelGGL(kern, pl.grid, dim3(kBdWaves * kWave), pl.lds, st, pl.a);
+        if (pl.a.merge_launch) {
+            const dim3 g(kBdRows / 4, pl.grid.y, pl.grid.z);
+            const int need = (pl.a.n_chunks + merge_ppr<128>() - 1) / merge_ppr<128>();
+            if (need <= 2) hipLaunchKernelGGL((fattn_bd_merge_kernel<128, 2>), g, dim3(256), 0, st, pl.a);
+            else if (need <= 4) hipLaunchKernelGGL((fattn_bd_merge_kernel<128, 4>), g, dim3(256), 0, st, pl.a);
+            else if (need <= 8) hipLaunchKernelGGL((fattn_bd_merge_kernel<128, 8>), g, dim3(256), 0, st, pl.a);
+            else hipLaunchKernelGGL((fattn_bd_merge_kernel<128, 16>), g, dim3(256), 0, st, pl.a);
+        }
+    });
+}
+
+template <int KT>
+int launch_bd(const Plan& pl, hipStream_t st, const Events& ev) {
+    return pl.a.has_mask ? launch_bd_hm<KT, true>(pl, st, ev) : launch_bd_hm<KT, false>(pl, st, ev);
+}
+
 template <int KT>
 int launch_pf(const Plan& pl, hipStream_t st, const Events& ev) {
     return pl.a.has_mask ? launch_pf_hm<KT, true>(pl, st, ev) : launch_pf_hm<KT, false>(pl, st, ev);
@@ -177,6 +211,11 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
             if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0>(pl, st, ev);
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
+        if (pl.bd) {
+            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_bd<FATTN_TYPE_Q8_0>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_bd<FATTN_TYPE_Q4_0>(pl, st, ev);
+            return FATTN_ERR_UNSUPPORTED_TYPE;
+        }
     }
     if constexpr (D == 64 || D == 128) {
         if (pl.mq) {
@@ -185,7 +224,7 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
     }
-    if (pl.pf || pl.mq) return FATTN_ERR_UNSUPPORTED_HEAD_DIM;
+    if (pl.pf || pl.mq || pl.bd) return FATTN_ERR_UNSUPPORTED_HEAD_DIM;
     if constexpr (D % QK == 0) {
         if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0)
             return launch_gran<FATTN_TYPE_Q8_0, FATTN_TYPE_Q8_0, D>(pl, st, ev);

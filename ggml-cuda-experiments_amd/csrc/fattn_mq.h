@@ -412,10 +412,22 @@ __global__ __launch_bounds__(NW * kWave, NW == 8 ? 1 : 2) void fattn_mq_kernel(c
     }
 
     // ---- several chunks: publish each column group's 16 rows as subtile
-    // (tile, 4*NG) in the decode kernel's partial layout; the last workgroup
-    // of the tile merges the subtiles (same hand-off as fattn_split_kernel)
+    // (tile, 4*NG) in the decode kernel's partial layout.  merge_launch: the
+    // subtiles' chunk partials merge in fattn_mq_merge_kernel (the kernel
+    // boundary orders the stores before its loads); otherwise the last
+    // workgroup of the tile merges them (same hand-off as fattn_split_kernel)
     constexpr int SUBS = NW * NG;
     const int64_t tile = (int64_t)iq3 * gridDim.y + y;
+    if (a.merge_launch) {
+#pragma unroll
+        for (int gi = 0; gi < NG; gi++) {
+            const int64_t slot = ((tile * SUBS + wave * NG + gi) * a.n_chunks + chunk) * kRows + i16;
+#pragma unroll
+            for (int c = 0; c < NC; c++) *(f32x4*)(a.ws_o + slot * D + 16 * c + 4 * g) = o[gi][c];
+            if (g == 0) *(f32x2*)(a.ws_ml + 2 * slot) = f32x2{m_run[gi], l_tot[gi]};
+        }
+        return;
+    }
     // this launch's stamp on the tile's arrival word (arrival_begin,
     // fattn_split.h): ahead of the publish, so the drain below covers it
     if (tid == 0) arrival_begin(a, tile);
@@ -447,6 +459,31 @@ __global__ __launch_bounds__(NW * kWave, NW == 8 ? 1 : 2) void fattn_mq_kernel(c
         combine_tile<D>(a, tile * SUBS + j, qt, 0, ik2, iq3, rv, kRows * j, smem);
         __syncthreads();
     }
+}
+
+// Second launch of a split multi-query plan (SplitArgs::merge_launch): one
+// wave per packed row of a 16-row subtile merges the row's chunk partials
+// (merge_row_parts: the fa_reduce LSE merge of src/flash_row_float.h:415-472
+// in fp32, fixed order) and writes the normalised dst row.  grid.y runs over
+// (tile, subtile) pairs, y' = tile_y * SUBS + sub, so the partial slots are
+// the multi-query kernel's ((tile * SUBS + sub) * chunks + chunk) * 16 + row.
+template <int D, int KIT, int SUBS>
+__global__ __launch_bounds__(256) void fattn_mq_merge_kernel(const SplitArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int tm = blockIdx.x * 4 + (threadIdx.x >> 6);  // row of the subtile
+    const int ys = blockIdx.y, iq3 = blockIdx.z;
+    const int y = ys / SUBS, sub = ys % SUBS;
+    int qt = 0, ik2 = y;  // the multi-query kernel's tile decode
+    if (a.n_qt != 1) {
+        qt = y % a.n_qt;
+        ik2 = y / a.n_qt;
+    }
+    const int p = kRows * sub + tm;  // packed row of the tile
+    if (p >= min(a.QPT, a.NQ - qt * a.QPT) * a.R) return;
+    const int64_t slot0 = ((int64_t)iq3 * gridDim.y + ys) * a.n_chunks * kRows + tm;  // chunk 0's row
+    const int rq = div_R(a, p);
+    float* out = a.dst + (((int64_t)iq3 * a.NQ + qt * a.QPT + rq) * a.H + ik2 * a.rk2 + (p - rq * a.R)) * D;
+    merge_row_parts<D, KIT>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kRows * D, 2 * kRows);
 }
 
 }  // namespace fattn

@@ -6,7 +6,7 @@
 // unnormalised P.V, merged with the log-sum-exp rule of fa_reduce
 // (src/flash_row_float.h:429-471) -- but built MI355X-first:
 //
-//  * Work unit: one workgroup = 4 waves = (KV chunk, 16 packed query rows).
+//  * Work unit: one workgroup = 4, 8 or 16 waves = (KV chunk, 16 packed query rows).
 //    The 16 MFMA rows pack (query row x q-head) pairs that share one KV head
 //    (GQA broadcast ik2 = iq2 / (ne02/ne12), flash-llama.h:128-140), so a
 //    32q/8kv decode packs 4 heads into one tile instead of re-reading K/V 4x.
@@ -26,8 +26,10 @@
 //    l^48).  Dequant is h(q*d) with one f16 rounding -- exactly the oracle's
 //    fp16 rounding of the dequantised value (src/utils.h:10-11).
 //  * fp32 MFMA accumulators, fp32 softmax state (the reference keeps fp16).
-//  * The 4 waves' states merge through LDS; with several chunks the partials
-//    (O, m, l) go to the caller's workspace and fattn_combine merges them.
+//  * The waves' states merge through LDS (or, for one-row tiles, per wave);
+//    with several chunks the partials (O, m, l) go to the caller's workspace
+//    and merge in the last-arriving workgroup or wave (one-row tiles) or in a
+//    second launch, fattn_merge_kernel (multi-row tiles).
 #pragma once
 
 #include "fattn_common.h"

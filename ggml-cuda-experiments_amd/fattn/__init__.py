@@ -42,21 +42,14 @@ OPT_SPLIT_STEPS = 3
 OPT_SPLIT_INFLIGHT = 4
 OPT_PF = 5
 OPT_PF_STAGGER = 6
-OPT_PF_WAVES = 7
-OPT_PF_DEQUANT = 8
-OPT_PF_PIPE = 9
 OPT_SPLIT_WAVE_MERGE = 10
 OPT_SPLIT_PRIO = 11
 OPT_PF_SKIP = 12
 OPT_MQ_MIN_ROWS = 13
-OPT_DEC = 14
-OPT_DEC_LOADERS = 15
-OPT_DEC_COMPUTE = 16
-OPT_DEC_DIAG = 17
-OPT_DEC_AHEAD = 18
 OPT_SPLIT_WAVES = 19
 OPT_SPLIT_SKIP = 20
 OPT_SPLIT_MERGE = 21
+OPT_BD = 22
 
 
 class FattnError(RuntimeError):
@@ -257,8 +250,10 @@ class Attention:
         self.p.workspace_bytes = self.workspace.numel()
         self.dst = dst
 
-    def retarget(self, q=None, k=None, v=None, dst=None):
+    def retarget(self, q=None, k=None, v=None, dst=None, mask=None):
         """Point the same call at other buffers with identical shapes/strides."""
+        if mask is not None:
+            self.p.mask.data = mask
         if q is not None:
             self.p.q.data = q
         if k is not None:

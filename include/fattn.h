@@ -35,8 +35,10 @@
  *     allocates on the hot path; `stream` is a hipStream_t (NULL = default).
  *   - return value: FATTN_OK (0) or a negative fattn_status; nothing is launched
  *     when an error is returned.  fattn_strerror() names the code.
- *   - stream-ordered and asynchronous; thread-compatible (the only global state is
- *     fattn_set_option's planner overrides, meant for tests and benchmarks).
+ *   - stream-ordered and asynchronous; thread-compatible.  Global state: the
+ *     process-wide planner overrides of fattn_set_option (tests, benchmarks), a
+ *     per-device CU count cache, and a launch-epoch counter that stamps the
+ *     split-KV arrival words (monotonic; any thread may advance it).
  */
 #ifndef FATTN_H
 #define FATTN_H
@@ -60,7 +62,7 @@ enum fattn_status {
     FATTN_OK = 0,
     FATTN_ERR_INVALID_ARG = -1,     /* NULL pointer, bad shape, ne not divisible */
     FATTN_ERR_UNSUPPORTED_TYPE = -2,
-    FATTN_ERR_UNSUPPORTED_HEAD_DIM = -3,  /* D must be 64, 128 or 256 (256: split-KV kernel only) */
+    FATTN_ERR_UNSUPPORTED_HEAD_DIM = -3,  /* D must be 64, 80 (f16 K/V only), 96, 128 or 256 */
     FATTN_ERR_BAD_STRIDE = -4,       /* layout the kernels cannot address */
     FATTN_ERR_WORKSPACE = -5,        /* workspace too small */
     FATTN_ERR_LAUNCH = -6,           /* HIP launch failure */
@@ -114,13 +116,19 @@ int fattn_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 int fattn_ext(const fattn_params* p, void* stream);
 
 /* Same as fattn_ext, additionally recording the hipEvent_t `ev_begin` / `ev_end`
- * on `stream` immediately before / after the attention kernel (one launch: the
- * split-KV chunk merge is fused into it), so a caller can time that kernel alone
- * with hipEventElapsedTime.  Either event may be NULL. */
+ * on `stream` immediately before the first and after the last kernel of the
+ * plan -- the attention kernel, plus the chunk-merge kernel when the plan
+ * merges its split-KV partials in a second launch (fattn_describe names both),
+ * plus the prefill mask-flags pass before it -- so a caller can time the whole
+ * attention op on the device with hipEventElapsedTime.  Either event may be NULL. */
 int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* ev_end);
 
-/* Process-wide planner overrides (tests, benchmarks).  Not thread-safe against
- * concurrent launches.  Returns FATTN_OK or FATTN_ERR_INVALID_ARG. */
+/* Planner overrides (tests, benchmarks).  They are PROCESS-WIDE: one call changes
+ * the plans of every later fattn_ext / fattn_describe / fattn_workspace_size on
+ * every host thread (stored in atomics, so never torn, but a thread that sets an
+ * option while another plans races with it).  Set them before launching, or from
+ * one thread.  Option ids of removed experiments are not reused.  Returns
+ * FATTN_OK or FATTN_ERR_INVALID_ARG. */
 enum {
     FATTN_OPT_MQ_ROWS_PER_WAVE = 1, /* multi-query kernel: 0 = auto, 16 (4 waves x 16 rows), 32 (8 waves x 32 rows) */
     FATTN_OPT_MQ_DISABLE = 2,       /* 1 = never pick the multi-query kernel (split-KV kernel only) */
@@ -131,12 +139,6 @@ enum {
     FATTN_OPT_PF_STAGGER = 6,       /* prefill kernel, bit 0: SIMD partner waves staggered (default lockstep);
                                        bit 1 (default on): waves 4-7 at s_setprio 1; bit 2: XCD-grouped
                                        workgroup order (the query tiles of a kv head on one XCD) */
-    FATTN_OPT_PF_WAVES = 7,         /* removed experiment (4 waves x 64 rows); accepted with 8 only */
-    FATTN_OPT_PF_DEQUANT = 8        /* quantised prefill: 0 = auto, 1 = dequantise inside the kernel, 2 = convert K/V
-                                       to f16 rows in the workspace first (fattn_workspace_size grows by
-                                       2 * Skv * Hkv * N * D * 2 bytes; 8 waves only) */,
-    FATTN_OPT_PF_PIPE = 9           /* removed prefill schedule experiments (software-pipelined, SIMD-partner
-                                       ping-pong: parity-green, not faster); accepts 0 or 1 only */,
     FATTN_OPT_SPLIT_WAVE_MERGE = 10 /* split kernel, one-row tiles with <= 32 wave partials: 0 = every wave
                                        publishes and the last-arriving wave merges (default), 1 = the
                                        workgroup-level merge used for all other tiles */,
@@ -147,21 +149,18 @@ enum {
                                        first (default; the workspace holds n_qt * N/64 flag bytes),
                                        1 = no pre-pass (every tile fetched; all -inf wave blocks still skipped) */,
     FATTN_OPT_MQ_MIN_ROWS = 13,     /* multi-query kernel only from this many packed (query x head) rows per kv
-                                       head (default 256, minimum 32); fewer rows take the split-KV kernel */
-    FATTN_OPT_DEC = 14,             /* removed (the loader-wave decode kernel measured slower than the split
-                                       kernel); accepted with 0 or 1 only */
-    FATTN_OPT_DEC_LOADERS = 15,     /* removed; accepted with 0 only */
-    FATTN_OPT_DEC_COMPUTE = 16,     /* removed; accepted with 0 only */
-    FATTN_OPT_DEC_DIAG = 17,        /* removed; accepted with 0 only */
-    FATTN_OPT_DEC_AHEAD = 18,       /* removed; accepted with 0 only */
+                                       head (0 = the default, 64; minimum 32); fewer rows take the split-KV kernel */
     FATTN_OPT_SPLIT_WAVES = 19,     /* split kernel waves per workgroup: 0 = auto, 4, 8 or 16 (16-B row path;
                                        16 needs the Q8_0/Q4_0 register budget, else clamped to 8) */
     FATTN_OPT_SPLIT_SKIP = 20       /* split kernel, masked: 0 = steps whose mask is -inf for every key and row
                                        of the tile are neither loaded nor computed (default; the mask words are
                                        read beside Q), 1 = every step loaded and computed */,
-    FATTN_OPT_SPLIT_MERGE = 21      /* split kernel, tiles of several packed rows: 0 = the chunk partials merge in
+    FATTN_OPT_SPLIT_MERGE = 21,     /* split kernel, tiles of several packed rows: 0 = the chunk partials merge in
                                        a second launch, one wave per (tile, row) (default), 1 = the last-arriving
                                        workgroup merges the whole tile (combine_tile) */
+    FATTN_OPT_BD = 22               /* batched-decode kernel (64-row workgroups, D = 128 Q8_0 / Q4_0, contiguous
+                                       rows): 0 = auto (from 64 packed rows per kv head, below the prefill
+                                       shapes), 1 = never, 2 = whenever eligible */
 };
 int fattn_set_option(int option, int value);
 

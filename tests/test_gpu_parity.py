@@ -104,8 +104,10 @@ def mq_on():
     """The multi-query kernel from 32 packed rows per kv head (the planner's
     default threshold is 256; below it the split kernel is faster)."""
     fattn.set_option(fattn.OPT_MQ_MIN_ROWS, 32)
+    fattn.set_option(fattn.OPT_BD, 1)  # (64+ rows at D = 128 would take the batched-decode kernel)
     yield
-    fattn.set_option(fattn.OPT_MQ_MIN_ROWS, 256)
+    fattn.set_option(fattn.OPT_MQ_MIN_ROWS, 0)  # the planner default
+    fattn.set_option(fattn.OPT_BD, 0)
 
 
 MQ_CASES = [
@@ -206,6 +208,92 @@ def test_mq_fully_masked_rows_are_nan(dev, mq_on):
     got, ref = run_gpu(p), p.oracle()
     assert np.isnan(ref[:, 5]).all() and np.isnan(got[:, 5]).all()
     assert attn_rel_err(got, ref) <= RTOL
+
+
+# ------------------------------------------------------------------ batched-decode kernel (fattn_bd.h)
+# 64 packed rows per workgroup, 128-key tiles over 8 waves, chunk partials
+# merged by a second launch.  The planner takes it from 64 packed rows per kv
+# head (D = 128, Q8_0 / Q4_0, contiguous rows); FATTN_OPT_BD = 2 forces it.
+
+@pytest.fixture
+def bd_force():
+    fattn.set_option(fattn.OPT_BD, 2)
+    yield
+    fattn.set_option(fattn.OPT_BD, 0)
+
+
+BD_CASES = [
+    dict(kv_type="q8_0", NQ=64, H=8, Hkv=8, N=4096, mask="random"),          # config 5 shape, 8 heads
+    dict(kv_type="q4_0", NQ=64, H=4, Hkv=4, N=2048, mask="random"),
+    dict(kv_type="q8_0", NQ=16, H=16, Hkv=4, N=1024, mask="random"),         # GQA: 16 queries x 4 heads
+    dict(kv_type="q4_0", NQ=8, H=64, Hkv=8, N=512, mask="random"),           # R = 8
+    dict(kv_type="q8_0", NQ=40, H=2, Hkv=2, N=800, mask="random"),           # ragged rows, N % 128 = 32
+    dict(kv_type="q8_0", NQ=130, H=2, Hkv=2, N=4064, mask="random"),         # three query tiles, tail quarter
+    dict(kv_type="q8_0", NQ=64, H=2, Hkv=2, N=96, mask="random"),            # one partial tile
+    dict(kv_type="q4_0", NQ=64, H=4, Hkv=4, N=1024, mask="none"),
+    dict(kv_type="q8_0", NQ=64, H=2, Hkv=2, N=2048, mask="neginf_blocks"),   # -inf block skip
+    dict(kv_type="q8_0", NQ=64, H=2, Hkv=2, N=1024, mask="causal"),
+    dict(kv_type="q8_0", NQ=33, H=2, Hkv=2, N=1024, mask="random", S=2),     # ne03 batch
+    dict(kv_type="q4_0", NQ=64, H=4, Hkv=2, N=640, mask="tail", S=2, Skv=1),  # seq broadcast, padded cache
+]
+
+
+@pytest.mark.parametrize("case", BD_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_bd_sweep(dev, bd_force, case):
+    p = make_problem(D=128, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert "fattn_bd_kernel" in d, d
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("chunk", [128, 384, 1024, 100000])
+def test_bd_chunking_invariance(dev, bd_force, chunk):
+    p = make_problem(D=128, NQ=64, H=4, N=2048, kv_type="q8_0", seed=27)
+    assert attn_rel_err(run_gpu(p, kv_chunk=chunk), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
+def test_bd_extreme_rescale(dev, bd_force, kt):
+    p = make_problem(D=128, NQ=64, H=2, N=2048, kv_type=kt, seed=28, extreme=True)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
+def test_bd_rescale_ramp(dev, bd_force, kt):
+    p = make_problem(D=128, NQ=64, H=2, N=4096, kv_type=kt, seed=29, ramp=12.0, mask="none")
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+def test_bd_fully_masked_rows_are_nan(dev, bd_force):
+    p = make_problem(D=128, NQ=64, H=2, N=1024, kv_type="q8_0", mask="random", seed=31)
+    m = orc.f16_bits_to_f32(p.mask_bits)
+    m[5, :] = -np.inf
+    m[40, :] = -np.inf
+    p.mask_bits = orc.f32_to_f16_bits(m)
+    got, ref = run_gpu(p), p.oracle()
+    assert np.isnan(ref[:, 5]).all() and np.isnan(got[:, 5]).all()
+    assert np.isnan(got[:, 40]).all()
+    assert attn_rel_err(got, ref) <= RTOL
+
+
+def test_bd_deterministic(dev, bd_force):
+    p = make_problem(D=128, NQ=64, H=4, N=4096, kv_type="q8_0", seed=32)
+    a, b = run_gpu(p), run_gpu(p)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_bd_matches_split_kernel(dev, bd_force):
+    """The batched-decode kernel against the split kernel on one problem."""
+    p = make_problem(D=128, NQ=64, H=4, Hkv=2, N=1024, kv_type="q4_0", seed=33)
+    a = run_gpu(p)
+    fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
+    try:
+        b = run_gpu(p)
+    finally:
+        fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
+    assert attn_rel_err(a, b) <= RTOL
+    assert attn_rel_err(a, p.oracle()) <= RTOL
 
 
 @pytest.mark.parametrize("kt,N,chunk", [("q8_0", 4096, 0), ("q4_0", 2048, 256), ("f16", 1024, 128), ("q8_0", 96, 32),
