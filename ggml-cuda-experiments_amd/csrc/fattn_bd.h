@@ -196,6 +196,10 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     const int rg = wave & 1, kq = wave >> 1;  // row group, key quarter
     const int h = lane >> 5;                  // k-group of the MFMA operands
     const int c32 = lane & 31;                // MFMA column: packed row 32 rg + c32; MFMA row: key 32 kq + c32
+    // diagnostic build only (FATTN_STAMPS, tools/stamps_bd.py): 0 start, 1 prologue
+    // issued, 2 Q ready, 3 + 2s / 4 + 2s tile s (< 4) landed / computed, 14 / 15
+    // tile 0 barriers passed, 11 loop done, 12 states parked, 13 stores drained
+    FATTN_STAMP(0);
 
     // ---- tile decode: y -> (kv head, 64-row query tile); R = rk2
     const int chunk = blockIdx.x;
@@ -292,6 +296,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     const float log2e = 1.4426950408889634f;
     const float scale = a.scale;
 
+    FATTN_STAMP(1);
     // Q landed (raw 0, raw 1 and mask 0 may fly on); every wave's Q pieces in LDS
     {
         const int n1 = ntiles > 1 ? 1 : 0, n0 = ntiles > 0 ? 1 : 0;
@@ -312,18 +317,22 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
         qop[kk] = hq;
     }
     (void)kQInstW;
+    FATTN_STAMP(2);
 
     for (int s = 0; s < ntiles; s++) {
         // raw s landed (mask s - 1 (s >= 1), raw s + 1, mask s may fly on)
         bd_vm_wait<KT, D, HM>(wave, s + 1 < ntiles ? 1 : 0, s > 0 ? 2 : 1);
+        if (s < 4) FATTN_STAMP(3 + 2 * s);
         // every wave's pieces of raw s landed; every wave is done with tile
         // s - 1 (the V image and raw s - 1's slot are free)
         __syncthreads();
+        if (s == 0) FATTN_STAMP(14);
         if (s + 2 < ntiles) bd_issue<KT, D>(rs, c_lo + (s + 2) * kBdKeys, raw_lds(s + 2), wave, lane);
         const uint8_t* kraw = raw_ptr(s);
         bd_dequant_v<KT, D>(kraw + C::kvRaw, smem, wave, lane);
         // the V image is complete
         __syncthreads();
+        if (s == 0) FATTN_STAMP(15);
         // this lane's mask values of tile s (keys 8 u + 4 h + 0..3 of the
         // quarter), then mask s + 1 into the same registers
         u32x2 mh[4];
@@ -420,7 +429,16 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
 #pragma unroll
             for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[q], o[db]);
         }
+#ifdef FATTN_STAMPS
+        if (s < 4) {
+            float z = 0.0f;
+            for (int db = 0; db < NDB; db++) z += o[db][0];
+            asm volatile("" ::"v"(z));  // the MFMA results are in before the stamp
+            FATTN_STAMP(4 + 2 * s);
+        }
+#endif
     }
+    FATTN_STAMP(11);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
     // ---- merge the four key quarters of each row.  Every wave parks its
@@ -443,6 +461,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
         if (h == 0) ((f32x2*)(smem + C::parkMl))[kq * kBdRows + p] = f32x2{m_run, l_own};
     }
     __syncthreads();
+    FATTN_STAMP(12);
     constexpr int kDpt = kBdRows * D / (kBdWaves * kWave);  // dims per thread: 16
     const int pr = tid / (D / kDpt), c0 = (tid % (D / kDpt)) * kDpt;
     const f32x2* pml = (const f32x2*)(smem + C::parkMl);
@@ -495,6 +514,10 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
 #pragma unroll
     for (int e = 0; e < kDpt; e += 4) *(f32x4*)(po + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
     if (c0 == 0) *(f32x2*)(a.ws_ml + 2 * slot) = f32x2{M, L};
+#ifdef FATTN_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FATTN_STAMP(13);
+#endif
 }
 
 // Second launch of a split batched-decode plan: one wave per (tile, packed

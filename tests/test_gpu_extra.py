@@ -192,9 +192,11 @@ def test_workspace_prefill_then_decode(dev):
 @pytest.mark.parametrize("case", [
     dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0"),                  # config 3: workgroup-level row merge
     dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", waves=4),         # wave partials (wave_merge 1)
-    dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0"),                  # multi-row tiles: combine_tile
-    dict(D=128, NQ=64, H=32, Hkv=8, N=2048, kv_type="q8_0"),          # multi-query kernel
-], ids=["row_merge", "wave_merge", "combine", "mq"])
+    dict(D=128, NQ=16, H=4, N=4096, kv_type="q8_0", merge=1),         # multi-row tiles, fused: combine_tile
+    dict(D=128, NQ=16, H=4, N=4096, kv_type="q8_0"),                  # multi-row tiles, second-launch merge
+    dict(D=128, NQ=64, H=32, Hkv=8, N=2048, kv_type="q8_0", mq=1, merge=1),  # multi-query kernel, fused
+    dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0"),                  # batched-decode kernel (merge launch)
+], ids=["row_merge", "wave_merge", "combine", "merge_launch", "mq", "bd"])
 def test_workspace_not_zeroed(dev, case, fill):
     # (the multi-row case merges in a second launch and never reads the words;
     # it checks that the garbage does not leak into the partials either)
@@ -205,9 +207,15 @@ def test_workspace_not_zeroed(dev, case, fill):
     import torch
     case = dict(case)
     waves = case.pop("waves", 0)
+    merge = case.pop("merge", 0)
+    mq = case.pop("mq", 0)
     p = make_problem(seed=71, **case)
     t = upload(p, dev)
     fattn.set_option(fattn.OPT_SPLIT_WAVES, waves)
+    fattn.set_option(fattn.OPT_SPLIT_MERGE, merge)
+    if mq:
+        fattn.set_option(fattn.OPT_BD, 1)
+        fattn.set_option(fattn.OPT_MQ_MIN_ROWS, 32)
     try:
         att = fattn.Attention(*views(p, t), t["dst"], p.scale)
         assert int(att.describe().split("grid(")[1].split(",")[0]) > 1, att.describe()  # several chunks
@@ -225,6 +233,9 @@ def test_workspace_not_zeroed(dev, case, fill):
             assert attn_rel_err(t["dst"].cpu().numpy(), ref) <= RTOL
     finally:
         fattn.set_option(fattn.OPT_SPLIT_WAVES, 0)
+        fattn.set_option(fattn.OPT_SPLIT_MERGE, 0)
+        fattn.set_option(fattn.OPT_BD, 0)
+        fattn.set_option(fattn.OPT_MQ_MIN_ROWS, 0)
 
 
 # ------------------------------------------------------------------ multi-GPU head shard, one GPU
