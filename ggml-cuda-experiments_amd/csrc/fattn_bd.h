@@ -14,26 +14,31 @@
 //    quarter kq = w >> 1 of every 128-key tile, so each K / V byte of the tile
 //    is read from HBM once for all 64 rows;
 //  * HBM -> LDS: the tile's raw ggml K and V rows by buffer_load ... lds (1-KiB
-//    wave instructions dealt round-robin over the waves), three raw tiles in
-//    the ring, two in flight beyond the one being computed;
-//  * K: dequantised on the LDS -> VGPR hop straight into the A operand of
-//    S^T = K.Q^T (v_mfma_f32_32x32x16_f16; lane = key, 8 dims): h(q * d), one f16
-//    rounding, exactly the oracle's (src/utils.h:10-11);
-//  * V: the workgroup dequantises the tile once into an f16 image (the prefill
-//    kernel's [dim block][key][64 B] swizzled layout) read back transposed by
-//    ds_read_b64_tr_b16 as the A operand of O^T = V^T.P^T, with P^T the S^T
-//    accumulator itself converted to f16 (no lane movement);
+//    wave instructions dealt round-robin over the waves), two raw slots: tile
+//    s + 2 is issued into tile s's slot once s is dequantised, so two tiles
+//    are in flight while the waves compute;
+//  * the workgroup dequantises each tile ONCE -- wave w takes half block w of
+//    every key, K and V -- into f16 K and V images (the prefill kernel's
+//    layouts), h(q * d) with one f16 rounding, exactly the oracle's
+//    (src/utils.h:10-11);
+//  * "swapped" products on v_mfma_f32_32x32x16_f16: S^T = K.Q^T (K rows from
+//    the image by ds_read_b128, all eight read before the chain; Q^T in
+//    registers), then O^T = V^T.P^T with P^T the S^T accumulator itself
+//    converted to f16 (no lane movement) and V^T gathered by ds_read_b64_tr_b16;
+//  * Q: the workgroup's 64 f32 rows staged HBM -> LDS once by DMA (in the K
+//    image's place), not re-read per wave;
 //  * the mask: each lane's 16 keys of its row per tile by four 16-B buffer
 //    loads into registers, one tile ahead (LDS holds only K/V);
 //  * online softmax in the log2 domain with the deferred max (T13); a wave
 //    whose 32 x 32 mask block is -inf everywhere skips the block (exact);
-//  * epilogue: the four key quarters of each row group merge through LDS;
-//    one chunk: normalised dst rows; several: (O, m, l) partials merged by
-//    fattn_bd_merge_kernel in a second launch.
+//  * epilogue: every wave parks its rows' (O, m, l) in LDS, then all 512
+//    threads merge the four key quarters of a row and store whole rows (no
+//    row-per-lane store tail); one chunk: normalised dst rows; several:
+//    (O, m, l) partials merged by fattn_bd_merge_kernel in a second launch.
 //
-// LDS (D = 128, Q8_0): [0, 32 KiB) the V image; then 3 raw tiles
-// [K rows | V rows] of 17 KiB each.  134 KiB: one workgroup per CU, two waves
-// per SIMD.
+// LDS (D = 128, Q8_0): [0, 32 KiB) K image, [32, 64 KiB) V image, then 2 raw
+// tiles [K rows | V rows] of 34 KiB; the epilogue reuses it all (134 KiB):
+// one workgroup per CU, two waves per SIMD.
 #pragma once
 
 #include "fattn_pf.h"
@@ -51,9 +56,9 @@ struct BdCfg {
     static constexpr int rowB = row_bytes<KT, D>();
     static constexpr int kvRaw = kBdKeys * rowB;                 // raw K (or V) bytes per tile
     static constexpr int rawBytes = (2 * kvRaw + 15) / 16 * 16;  // [K rows | V rows]
-    static constexpr int nRaw = 3;
-    static constexpr int img = kBdKeys * D * 2;                  // f16 V image
-    static constexpr int rawOff = img;
+    static constexpr int nRaw = 2;
+    static constexpr int img = kBdKeys * D * 2;                  // one f16 image (K, then V)
+    static constexpr int rawOff = 2 * img;
     static constexpr int ringEnd = rawOff + nRaw * rawBytes;
     static constexpr int NI = (kvRaw + 1023) / 1024;             // 1-KiB DMA instructions per K (or V) tile
     // instructions j = 0 .. 2 NI - 1 (K then V) go to wave j % 8
@@ -66,7 +71,7 @@ struct BdCfg {
     static constexpr int parkMl = 4 * kBdRows * parkStride * 4;
     static constexpr int parkBytes = parkMl + 4 * kBdRows * 8;
     static constexpr int ldsBytes = ringEnd > parkBytes ? ringEnd : parkBytes;
-    // Q staged as f32 rows [64][D] in the V image's place before the first tile
+    // Q staged as f32 rows [64][D] in the K image's place before the first tile
     static_assert(kBdRows * D * 4 <= img && D * 4 / 16 == 32, "Q rows of 32 16-B chunks in the image's place");
     static_assert(ldsBytes <= 163840, "");
 };
@@ -121,65 +126,34 @@ __device__ __forceinline__ void bd_vm_wait(int wave, int nraw, int nmask) {
     }
 }
 
-// raw V of a tile -> the f16 V image: wave w dequantises half h = w & 1 of
-// block b = w >> 1 of keys lane and 64 + lane (prefill kernel's V layout:
-// [4 dim blocks][128 keys][64 B], chunk c of key r at c ^ ((r >> 2) & 3))
+// raw tile -> f16 K and V images (the prefill kernel's layouts, 128 keys):
+// wave w dequantises half h = w & 1 of block b = w >> 1 -- K dim slice w and V
+// dim block b, chunks 2h, 2h + 1 -- of keys lane and 64 + lane; h(q * d), one
+// f16 rounding (src/utils.h:10-11).
+//   K image [8 dim slices][128 keys][32 B], 16-B halves swapped on keys with bit 3 set
+//   V image [4 dim blocks][128 keys][64 B], chunk c of key r at c ^ ((r >> 2) & 3)
 template <int KT, int D>
-__device__ __forceinline__ void bd_dequant_v(const uint8_t* vraw, uint8_t* v16, int wave, int lane) {
+__device__ __forceinline__ void bd_dequant(const uint8_t* raw, uint8_t* k16, uint8_t* v16, int wave, int lane) {
 #ifdef FATTN_MQ_NODEQ
     return;  // diagnostic build only
 #endif
+    using C = BdCfg<KT, D>;
     const int b = wave >> 1, h = wave & 1;
 #pragma unroll
     for (int i = 0; i < 2; i++) {
         const int r = 64 * i + lane;
-        u32x4 cv[2];
-        dequant_half<KT, D>(vraw, r, b, h, cv);
+        u32x4 ck[2], cv[2];
+        dequant_half<KT, D>(raw, r, b, h, ck);
+        dequant_half<KT, D>(raw + C::kvRaw, r, b, h, cv);
+        uint8_t* kd = k16 + wave * (kBdKeys * 32) + r * 32;
+        const int sk = (r >> 3) & 1;
+        *(u32x4*)(kd + sk * 16) = ck[0];
+        *(u32x4*)(kd + (sk ^ 1) * 16) = ck[1];
         uint8_t* vd = v16 + b * (kBdKeys * 64) + r * 64;
         const int sv = (r >> 2) & 3;
         *(u32x4*)(vd + ((2 * h) ^ sv) * 16) = cv[0];
         *(u32x4*)(vd + ((2 * h + 1) ^ sv) * 16) = cv[1];
     }
-}
-
-// A operand of S^T = K.Q^T for 16-dim k-step kk: key row `row` of the raw
-// tile, dims 16 kk + 8 h .. + 8, dequantised h(q * d)
-template <int KT, int D>
-__device__ __forceinline__ f16x8 bd_k_operand(const uint8_t* kraw, int row, int h, int kk, uint32_t dbits) {
-    constexpr int RB = row_bytes<KT, D>();
-    constexpr int BB = TypeInfo<KT>::block_bytes;
-    const int b = kk >> 1;
-    const f16x2 d = as_h2(dbits);
-    f16x2 h0, h1, h2, h3;
-    if constexpr (KT == FATTN_TYPE_Q8_0) {
-        // qs bytes 16 (kk & 1) + 8 h .. + 8 of block b (row * RB is 8-aligned)
-        const uint32_t off = row * RB + BB * b + 2 + 16 * (kk & 1) + 8 * h;
-        u32x2 raw;
-        switch ((BB * b + 2 + 16 * (kk & 1)) & 7) {  // kk is unrolled: compile-time
-            case 0: raw = read8_at<0>(kraw, off); break;
-            case 2: raw = read8_at<2>(kraw, off); break;
-            case 4: raw = read8_at<4>(kraw, off); break;
-            default: raw = read8_at<6>(kraw, off); break;
-        }
-        i8x4_to_h2x2(raw.x, h0, h1);
-        i8x4_to_h2x2(raw.y, h2, h3);
-    } else {  // Q4_0: elements 0-15 low nibbles of qs bytes 0-15, 16-31 high nibbles
-        const uint32_t off = row * RB + BB * b + 2 + 8 * h;
-        u32x2 raw;
-        switch ((BB * b + 2) & 7) {
-            case 0: raw = read8_at<0>(kraw, off); break;
-            case 2: raw = read8_at<2>(kraw, off); break;
-            case 4: raw = read8_at<4>(kraw, off); break;
-            default: raw = read8_at<6>(kraw, off); break;
-        }
-        const uint32_t sh = 4 * (kk & 1);
-        u4x4_to_h2x2((raw.x >> sh) & 0x0F0F0F0Fu, h0, h1);
-        u4x4_to_h2x2((raw.y >> sh) & 0x0F0F0F0Fu, h2, h3);
-    }
-    h0 *= d; h1 *= d; h2 *= d; h3 *= d;
-    f16x8 r;
-    r.s01 = h0; r.s23 = h1; r.s45 = h2; r.s67 = h3;
-    return r;
 }
 
 template <int KT, int D, bool HM>
@@ -264,6 +238,8 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
         }
     };
 
+    // per-lane K read base (prefill kernel's): key 32 kq + c32, half h (swapped on keys with bit 3 set)
+    const uint32_t kbase = c32 * 32 + ((h ^ ((c32 >> 3) & 1)) * 16);
     // per-lane V^T gather bases (prefill kernel's, 128-key image):
     // 16-lane group (h, dh), lane gi: key 32 kq + 16 q + 8 e + 4 h + gi / 4
     const int gi = lane & 15, dh = (lane >> 4) & 1;
@@ -272,7 +248,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     for (int e = 0; e < 2; e++) {
         const int row = 8 * e + 4 * h + (gi >> 2);
         const int ch = (2 * dh + ((gi & 3) >> 1)) ^ ((h + 2 * e) & 3);
-        vbase[e] = kq * 2048 + row * 64 + ch * 16 + (gi & 1) * 8;
+        vbase[e] = C::img + kq * 2048 + row * 64 + ch * 16 + (gi & 1) * 8;
     }
 
     // ---- this wave's issue order: prologue raw 0 | raw 1 | mask 0, then per
@@ -324,15 +300,16 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
         bd_vm_wait<KT, D, HM>(wave, s + 1 < ntiles ? 1 : 0, s > 0 ? 2 : 1);
         if (s < 4) FATTN_STAMP(3 + 2 * s);
         // every wave's pieces of raw s landed; every wave is done with tile
-        // s - 1 (the V image and raw s - 1's slot are free)
+        // s - 1 (the images are free)
         __syncthreads();
         if (s == 0) FATTN_STAMP(14);
-        if (s + 2 < ntiles) bd_issue<KT, D>(rs, c_lo + (s + 2) * kBdKeys, raw_lds(s + 2), wave, lane);
-        const uint8_t* kraw = raw_ptr(s);
-        bd_dequant_v<KT, D>(kraw + C::kvRaw, smem, wave, lane);
-        // the V image is complete
+        bd_dequant<KT, D>(raw_ptr(s), smem, smem + C::img, wave, lane);
+        // the images are complete and raw s's slot is free: tile s + 2 into it
+        // (a DMA issue that stalls on a full memory queue now overlaps the
+        // other waves' compute instead of holding a barrier)
         __syncthreads();
         if (s == 0) FATTN_STAMP(15);
+        if (s + 2 < ntiles) bd_issue<KT, D>(rs, c_lo + (s + 2) * kBdKeys, raw_lds(s + 2), wave, lane);
         // this lane's mask values of tile s (keys 8 u + 4 h + 0..3 of the
         // quarter), then mask s + 1 into the same registers
         u32x2 mh[4];
@@ -356,15 +333,17 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
         // a 32 x 32 block that is -inf for every valid row adds nothing (exact skip)
         if (HM && __builtin_amdgcn_ballot_w64(open != 0 && row_ok) == 0) continue;
 
-        // -- S^T = K.Q^T for this wave's 32 keys: A from the raw K rows
-        const int krow = 32 * kq + c32;
-        const RowScales<KT, D> ks = row_scales<KT, D>(kraw + krow * C::rowB);
+        // -- S^T = K.Q^T for this wave's 32 keys: the 8 K operands are read
+        // from the image before the MFMA chain (one LDS wait, not eight)
+        f16x8 ka[NK];
+#pragma unroll
+        for (int kk = 0; kk < NK; kk++) ka[kk] = *(const f16x8*)(smem + kk * (kBdKeys * 32) + kq * 1024 + kbase);
+        __builtin_amdgcn_sched_barrier(0);
         f32x16 st;
 #pragma unroll
         for (int j = 0; j < 16; j++) st[j] = 0.0f;
 #pragma unroll
-        for (int kk = 0; kk < NK; kk++)
-            st = mfma32(bd_k_operand<KT, D>(kraw, krow, h, kk, scale_bcast(ks, kk >> 1)), qop[kk], st);
+        for (int kk = 0; kk < NK; kk++) st = mfma32(ka[kk], qop[kk], st);
 
         // -- u = scale * s + mask (natural units); element j = key 8 (j/4) + 4 h + j%4
         float u[16];
@@ -426,6 +405,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
                 const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
                 va[db] = u32x4{a2.x, a2.y, b2.x, b2.y};
             }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[q], o[db]);
         }

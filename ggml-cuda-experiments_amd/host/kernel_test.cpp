@@ -228,9 +228,12 @@ int main(int argc, const char* argv[]) {
     // mask f16: one row for flash_attn_row; 32 rows (row 0 = the mask, the rest
     // zeros) for flash_attn_ext (kernel_test.h:74-85)
     const int mask_rows = parallel_kv ? 1 : 32;
-    HIP_CHECK(hipMalloc(&d_mask, 2 * (size_t)N * mask_rows));
+    // ext rows padded to an even length (ggml pads to GGML_KQ_MASK_PAD; the
+    // kernels read rows in dword pieces), so any --kv-size works
+    const int Np = parallel_kv ? N : N + (N & 1);
+    HIP_CHECK(hipMalloc(&d_mask, 2 * (size_t)Np * mask_rows));
     HIP_CHECK(hipMemcpyAsync(d_q, query.data(), sizeof(float) * D * H, hipMemcpyHostToDevice, stream));
-    std::vector<uint16_t> mask16((size_t)N * mask_rows, f2h(0.0f));
+    std::vector<uint16_t> mask16((size_t)Np * mask_rows, f2h(0.0f));
     for (int i = 0; i < N; i++) mask16[i] = f2h(mask[i]);
     HIP_CHECK(hipMemcpyAsync(d_mask, mask16.data(), 2 * mask16.size(), hipMemcpyHostToDevice, stream));
 
@@ -289,7 +292,17 @@ int main(int argc, const char* argv[]) {
         }
         ws_bytes = fattn_row_workspace_size(D, N, H);
     } else {
-        ws_bytes = 1 << 24;  // covers every plan of these shapes; zero-filled once (fattn_workspace_init)
+        // the plan fattn_ext_f16_launch makes of the call below, sized by the library
+        fattn_params pw;
+        std::memset(&pw, 0, sizeof(pw));
+        const int64_t eb = kv_type == FATTN_TYPE_F16 ? 2 : (int64_t)fattn_row_size(kv_type, 32);
+        pw.q = {d_q, FATTN_TYPE_F32, 0, {D, 1, H, 1}, {4, D * 4, D * 4, (int64_t)D * H * 4}};
+        pw.k = {d_k, kv_type, 0, {D, N, Hkv, 1}, {eb, (int64_t)rb, (int64_t)rb * N, (int64_t)rb * N * Hkv}};
+        pw.v = {d_v, kv_type, 0, {D, N, Hkv, 1}, {eb, (int64_t)rb, (int64_t)rb * N, (int64_t)rb * N * Hkv}};
+        pw.mask = {d_mask, FATTN_TYPE_F16, 0, {Np, 32, 1, 1}, {2, (int64_t)Np * 2, (int64_t)Np * 64, (int64_t)Np * 64}};
+        pw.dst = d_out;
+        pw.scale = scale;
+        ws_bytes = fattn_workspace_size(&pw);  // (0: one chunk, or a call the library rejects below)
     }
     HIP_CHECK(hipMalloc(&d_ws, std::max<size_t>(ws_bytes, 16)));
     ws_bytes = std::max<size_t>(ws_bytes, 16);
@@ -303,7 +316,7 @@ int main(int argc, const char* argv[]) {
         return fattn_ext_f16_launch(d_q, d_k, d_v, d_mask, d_out, scale,
                                     D, 1, H, 1,
                                     D, N, Hkv, 1,
-                                    32, N * 2,
+                                    32, Np * 2,
                                     D * 4, D * 4, D * H * 4,
                                     (int)rb, (int)rb * N, (int)rb * N * Hkv,
                                     D, H, 1, 1,

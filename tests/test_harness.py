@@ -48,6 +48,8 @@ def test_cpu_only_matches_reference_bitexact(tmp_path, fixture, args):
     ["--no-kv-parallel", "--kv-type", "q4_0"],
     ["--kv-size", "4096"],
     ["--no-kv-parallel", "--kv-type", "q8_0", "--kv-size", "4096", "--kv-heads", "32"],
+    ["--no-kv-parallel", "--kv-size", "1001"],             # odd kv size: mask rows padded to even
+    ["--no-kv-parallel", "--kv-size", "65536"],            # workspace sized by fattn_workspace_size
 ], ids=lambda a: "_".join(a) or "default")
 def test_harness_runs_on_gpu(dev, args):
     _need_bin()
