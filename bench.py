@@ -200,13 +200,15 @@ def cpu_baseline_prefill(rows=256):
             "extrapolation": f"linear: x {NQ // rows} rows x {H} heads (not measured)"}
 
 
-def prefill_measure(dev, hip, evs, kvn="q8_0", causal=False, steps=5):
+def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5):
     """The MFMA-bound prefill shape of SURVEY.md §8d (n_q = N = 4096, 32 heads,
-    head_dim 128, Q8_0 K/V, random f16 mask, non-causal): `steps` launches
-    captured in one HIP graph, HIP events around the replay on the launch
-    stream.  Two rotated KV caches (compute-bound: the cache state barely
-    matters).  The masked form's live-block flag pass (pf_mask_flags_kernel)
-    and the flag re-zeroing are inside the timed region."""
+    head_dim 128, Q8_0 K/V, non-causal, an f16 mask of zeros -- "zero mask":
+    every key visible; "random": U[-1,1) like kernel_test.h:48; "causal": 0 on
+    and below the diagonal, -inf above): `steps` launches captured in one HIP
+    graph, HIP events around the replay on the launch stream.  Two rotated KV
+    caches (compute-bound: the cache state barely matters).  The mask pre-pass
+    (pf_mask_flags_kernel: live / all-zero block flags) is inside the timed
+    region."""
     import torch
     import fattn
     D, H, N, NQ, R = 128, 32, 4096, 4096, 2
@@ -221,13 +223,17 @@ def prefill_measure(dev, hip, evs, kvn="q8_0", causal=False, steps=5):
         kv = [[fattn.quantize(torch.rand((H * N, D), generator=g, device=dev) * 2 - 1, typ).reshape(-1)
                for _ in range(2)] for _ in range(R)]
     q = torch.rand((1, NQ, H, D), generator=g, device=dev) * 2 - 1
-    mask = (torch.rand((NQ, N), generator=g, device=dev) * 2 - 1).to(torch.float16)
+    causal = mask_kind == "causal"
+    if mask_kind == "random":
+        mask = (torch.rand((NQ, N), generator=g, device=dev) * 2 - 1).to(torch.float16)
+    else:
+        mask = torch.zeros((NQ, N), dtype=torch.float16, device=dev)
     if causal:  # query i sees keys <= i (N == NQ): the upper triangle is -inf
         tri = torch.triu(torch.ones((NQ, N), dtype=torch.bool, device=dev), diagonal=1)
         mask = mask.masked_fill(tri, float("-inf"))
     out = torch.empty((R, 1, NQ, H, D), dtype=torch.float32, device=dev)
     att = fattn.Attention(fattn.q_view(q), fattn.kv_view(kv[0][0], typ, D, N, H), fattn.kv_view(kv[0][1], typ, D, N, H),
-                          fattn.mask_view(mask), out[0], 1.0 / D ** 0.5)
+                          None if mask_kind == "none" else fattn.mask_view(mask), out[0], 1.0 / D ** 0.5)
 
     def step(i):
         att.retarget(k=kv[i % R][0].data_ptr(), v=kv[i % R][1].data_ptr(), dst=out[i % R].data_ptr())
@@ -258,7 +264,7 @@ def prefill_measure(dev, hip, evs, kvn="q8_0", causal=False, steps=5):
     pairs = NQ * (NQ + 1) // 2 if causal else NQ * N
     flops = 4 * pairs * D * H
     tf = flops / (ms * 1e-3) / 1e12
-    return {"workload": f"prefill_{kvn}_h{H}_d{D}_n{N}_q{NQ}_{'causal' if causal else 'mask'}",
+    return {"workload": f"prefill_{kvn}_h{H}_d{D}_n{N}_q{NQ}_{mask_kind}_mask",
             "kernel": att.describe(), "kernel_ms_avg": round(ms, 5), "flops_per_step": flops,
             "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None}}
@@ -296,8 +302,9 @@ def parse_args(argv=None):
     ap.add_argument("--mask-live", type=float, default=1.0,
                     help="diagnostics: mask positions from this fraction of N on to -inf (a padded cache)")
     ap.add_argument("--wave-merge", type=int, default=-1, help="split/dec one-row tiles: 0 per-wave merge, 1 LDS merge")
-    ap.add_argument("--prefill-causal", action="store_true",
-                    help="causal mask on the prefill measurement (fully masked blocks are skipped)")
+    ap.add_argument("--prefill-mask", default="zero", choices=["zero", "random", "causal", "none"],
+                    help="mask of the prefill measurement (SURVEY.md §8d: zero); the random-mask form is "
+                         "reported beside it")
     ap.add_argument("--prefill-kv", default="q8_0", choices=["q8_0", "q4_0", "f16"],
                     help="K/V type of the prefill measurement (the metric's is q8_0)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -632,7 +639,10 @@ def main():
                         "value(N) / (N * this value)"}
         if not args.no_prefill and shape["n_q"] == 1:
             hip, evs = hip_events(2)
-            line["prefill"] = prefill_measure(dev, hip, evs, args.prefill_kv, args.prefill_causal)
+            line["prefill"] = prefill_measure(dev, hip, evs, args.prefill_kv, args.prefill_mask)
+            if args.prefill_mask != "random":
+                r = prefill_measure(dev, hip, evs, args.prefill_kv, "random")
+                line["prefill_random_mask"] = {k: r[k] for k in ("workload", "kernel_ms_avg", "roofline")}
         if not args.no_cpu_baseline and shape["n_q"] == 1:  # kernel_test.h's CPU path is one query row
             threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads)

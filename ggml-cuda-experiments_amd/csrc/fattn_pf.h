@@ -253,6 +253,20 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         t0 = lo;
         ntiles = hi >= lo ? hi - lo + 1 : 0;
     }
+    // live tiles whose mask block is +-0 everywhere (flag 2: the prefill of a
+    // zero or causal mask, away from the diagonal): their mask DMA goes through
+    // an offset past the descriptor -- no traffic, zeros land in the slot, so
+    // the instruction count (vmcnt budget) and the arithmetic are unchanged.
+    // Bit s of zb[s / 64]: tile t0 + s (the first 256 live tiles).
+    uint64_t zb[4] = {0, 0, 0, 0};
+    if (a.pf_flags) {
+        const uint8_t* fl = a.pf_flags + (int64_t)qt * (a.N / kPfKeys) + t0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const int b = 64 * w + lane;
+            zb[w] = __builtin_amdgcn_ballot_w64(b < ntiles && fl[b] == 2);
+        }
+    }
 
     StepSrc rs;
     rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
@@ -302,9 +316,10 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         if constexpr (HM) {
 #ifndef FATTN_MQ_NOMEM
             const uint32_t n2 = (uint32_t)(t0 + s) * kPfKeys * 2;
+            const bool zero = s < 256 && ((zb[s >> 6] >> (s & 63)) & 1);  // wave-uniform
 #pragma unroll
             for (int k = 0; k < C::NIM; k++) {
-                const uint32_t off = moff[k] == a.m_span ? a.m_span : moff[k] + n2;
+                const uint32_t off = (moff[k] == a.m_span || zero) ? a.m_span : moff[k] + n2;
                 dma<16>(rs.m, mslot + k * 1024, off);
             }
 #endif
@@ -627,25 +642,29 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     }
 }
 
-// ---- prefill mask pre-pass: flags[qt][s] = 1 when any of the query tile's
-// QPT mask rows has a key above -inf (f16 0xFC00) in KV tile s.  One workgroup
-// per (query tile, KV tile) block; every flag is written on every launch, so
-// the array needs no initialisation.  Reads the mask once (f16 [NQ][N]).
+// ---- prefill mask pre-pass: flags[qt][s] for the (query tile, KV tile) block
+// of the QPT mask rows x 64 keys: 0 when every value is -inf (f16 0xFC00; the
+// block adds nothing), 2 when every value is +-0 (the mask adds nothing: its
+// DMA is skipped), else 1.  One workgroup per block; every flag is written on
+// every launch, so the array needs no initialisation.  Reads the mask once
+// (f16 [NQ][N]).
 static __global__ __launch_bounds__(256) void pf_mask_flags_kernel(const uint8_t* __restrict__ mask, int64_t m_nb1, int NQ,
                                                             int QPT, int ntiles, uint8_t* __restrict__ flags) {
     const int s = blockIdx.x, qt = blockIdx.y;
     // thread -> (row qt*QPT + r, 16-B piece pc of the tile's 128 B): 8 pieces per row
-    uint32_t open = 0;
+    uint32_t open = 0, nonzero = 0;
     for (int i = threadIdx.x; i < QPT * 8; i += 256) {
         const int r = i >> 3, pc = i & 7;
         const int q = qt * QPT + r;
         if (q < NQ) {
             const u32x4 w = *(const u32x4*)(mask + (int64_t)q * m_nb1 + (int64_t)s * kPfKeys * 2 + pc * 16);
             open |= (w.x ^ 0xFC00FC00u) | (w.y ^ 0xFC00FC00u) | (w.z ^ 0xFC00FC00u) | (w.w ^ 0xFC00FC00u);
+            nonzero |= (w.x | w.y | w.z | w.w) & 0x7FFF7FFFu;
         }
     }
-    const int any = __syncthreads_or(open != 0);
-    if (threadIdx.x == 0) flags[(int64_t)qt * ntiles + s] = any ? 1 : 0;
+    const int any_open = __syncthreads_or(open != 0);
+    const int any_nonzero = __syncthreads_or(nonzero != 0);
+    if (threadIdx.x == 0) flags[(int64_t)qt * ntiles + s] = !any_open ? 0 : any_nonzero ? 1 : 2;
 }
 
 }  // namespace fattn

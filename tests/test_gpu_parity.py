@@ -388,6 +388,24 @@ def test_pf_fully_masked_rows_are_nan(dev, pf_force):
     assert attn_rel_err(got, ref) <= RTOL
 
 
+@pytest.mark.parametrize("kt", ["q8_0", "f16"])
+def test_pf_zero_mask_blocks(dev, pf_force, kt):
+    """Mask blocks classified by the pre-pass: all +-0 (flag 2: the block's mask
+    DMA fetches nothing, zeros land), mixed, all -inf (skipped), and -0.0
+    entries -- two query tiles x eight key tiles, against the oracle."""
+    p = make_problem(D=128, NQ=512, H=2, N=512, kv_type=kt, mask="random", seed=47)
+    m = orc.f16_bits_to_f32(p.mask_bits)
+    m[:, 0:128] = 0.0                     # zero blocks for both query tiles
+    m[:256, 128:192] = -0.0               # negative zeros still add nothing
+    m[256:, 192:256] = -np.inf            # one fully masked block of the second tile
+    m[:256, 448:512] = 0.0
+    m[300, 448] = 0.5                     # one value breaks the second tile's zero block
+    p.mask_bits = orc.f32_to_f16_bits(m)
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 @pytest.mark.parametrize("skip", [0, 1], ids=["range", "noprepass"])
 @pytest.mark.parametrize("kt", ["q8_0", "f16"])
 def test_pf_causal_block_skip(dev, kt, skip):
