@@ -27,8 +27,11 @@
 //    converted to f16 (no lane movement) and V^T gathered by ds_read_b64_tr_b16;
 //  * Q: the workgroup's 64 f32 rows staged HBM -> LDS once by DMA (in the K
 //    image's place), not re-read per wave;
-//  * the mask: each lane's 16 keys of its row per tile by four 16-B buffer
-//    loads into registers, one tile ahead (LDS holds only K/V);
+//  * the mask: each wave's 32 rows x 32 keys per tile by two 1-KiB LDS-DMA
+//    instructions into the wave's own 2-KiB slot, one tile ahead (issued once
+//    the wave has read the previous tile's values out of the slot).  Not by
+//    register loads: a load the compiler does not track, carried around the
+//    tile loop, gets copied at the loop's back edge before it has landed;
 //  * online softmax in the log2 domain with the deferred max (T13); a wave
 //    whose 32 x 32 mask block is -inf everywhere skips the block (exact);
 //  * epilogue: every wave parks its rows' (O, m, l) in LDS, then all 512
@@ -37,8 +40,8 @@
 //    (O, m, l) partials merged by fattn_bd_merge_kernel in a second launch.
 //
 // LDS (D = 128, Q8_0): [0, 32 KiB) K image, [32, 64 KiB) V image, then 2 raw
-// tiles [K rows | V rows] of 34 KiB; the epilogue reuses it all (134 KiB):
-// one workgroup per CU, two waves per SIMD.
+// tiles [K rows | V rows] of 34 KiB, then 8 mask slots of 2 KiB; the epilogue
+// reuses it all (148 KiB): one workgroup per CU, two waves per SIMD.
 #pragma once
 
 #include "fattn_pf.h"
@@ -63,14 +66,19 @@ struct BdCfg {
     static constexpr int NI = (kvRaw + 1023) / 1024;             // 1-KiB DMA instructions per K (or V) tile
     // instructions j = 0 .. 2 NI - 1 (K then V) go to wave j % 8
     static constexpr int ni_wave(int w) { return (2 * NI - w + kBdWaves - 1) / kBdWaves; }
-    static constexpr int NM = 4;                                 // mask loads per lane and tile
+    static constexpr int NM = 2;                                 // mask DMA instructions per wave and tile
+    // mask slot of wave w: [4 key octets u][32 rows][16 B] (8 keys per 16 B), so
+    // the lanes' 8-B reads of one octet are contiguous (conflict-free)
+    static constexpr int maskSlot = 2048;
+    static constexpr int maskOff = ringEnd;
+    static constexpr int maskEnd = maskOff + kBdWaves * maskSlot;
     // epilogue: every wave parks its (O, m, l) rows here, [4 key quarters][64
     // rows][D + 4] f32 (+16 B per row: the accumulator-layout writes are
     // conflict-free) then [4][64] (m, l)
     static constexpr int parkStride = D + 4;
     static constexpr int parkMl = 4 * kBdRows * parkStride * 4;
     static constexpr int parkBytes = parkMl + 4 * kBdRows * 8;
-    static constexpr int ldsBytes = ringEnd > parkBytes ? ringEnd : parkBytes;
+    static constexpr int ldsBytes = maskEnd > parkBytes ? maskEnd : parkBytes;
     // Q staged as f32 rows [64][D] in the K image's place before the first tile
     static_assert(kBdRows * D * 4 <= img && D * 4 / 16 == 32, "Q rows of 32 16-B chunks in the image's place");
     static_assert(ldsBytes <= 163840, "");
@@ -227,14 +235,22 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     }
     constexpr int kQInstW = kBdRows * D * 4 / 1024 / kBdWaves;  // Q DMA instructions per wave
 
-    // ---- mask: this lane's row, keys 32 kq + 8 u + 4 h + 0..3 of a tile, from
-    // four 16-B loads (keys 32 kq + 8 u .. + 8; the lane keeps half h)
-    const uint32_t mrow = row_ok ? (uint32_t)iq1 * (uint32_t)a.m_nb1 : a.m_span;
-    auto mask_issue = [&](int s, u32x4 (&mk)[4]) {
+    // ---- mask: the wave's 32 rows x keys 32 kq .. + 32 of a tile into its slot.
+    // DMA instruction i, lane l: octet u = 2 i + (l >> 5) of row l & 31 (rows
+    // past n_q come from past the descriptor: zeros, and count as not open)
+    const uint32_t mslot = lds0 + C::maskOff + wave * C::maskSlot;
+    uint32_t mrow_l;
+    {
+        const int r = kBdRowsW * rg + c32;
+        const int q1 = qt * a.QPT + div_R(a, r);
+        mrow_l = q1 < a.NQ ? (uint32_t)q1 * (uint32_t)a.m_nb1 : a.m_span;
+    }
+    auto mask_issue = [&](int s) {
         if constexpr (HM) {
             const uint32_t n2 = (uint32_t)(c_lo + s * kBdKeys + 32 * kq) * 2;
 #pragma unroll
-            for (int u = 0; u < 4; u++) mk[u] = ld_buf(rs.m, mrow == a.m_span ? a.m_span : mrow + n2 + 16 * u);
+            for (int i = 0; i < 2; i++)
+                dma<16>(rs.m, mslot + i * 1024, mrow_l == a.m_span ? a.m_span : mrow_l + n2 + 16 * (2 * i + h));
         }
     };
 
@@ -258,8 +274,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     // was issued after mask s.
     if (ntiles > 0) bd_issue<KT, D>(rs, c_lo, raw_lds(0), wave, lane);
     if (ntiles > 1) bd_issue<KT, D>(rs, c_lo + kBdKeys, raw_lds(1), wave, lane);
-    u32x4 mk[4] = {};
-    if (ntiles > 0) mask_issue(0, mk);
+    if (ntiles > 0) mask_issue(0);
 
     float m_run = kNegInf;    // reference max (log2 domain) of this lane's row
     f32x2 l2 = {0.0f, 0.0f};  // this lane's partial row sums (16 of every 32 keys)
@@ -311,19 +326,22 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
         if (s == 0) FATTN_STAMP(15);
         if (s + 2 < ntiles) bd_issue<KT, D>(rs, c_lo + (s + 2) * kBdKeys, raw_lds(s + 2), wave, lane);
         // this lane's mask values of tile s (keys 8 u + 4 h + 0..3 of the
-        // quarter), then mask s + 1 into the same registers
+        // quarter) out of the wave's slot, then mask s + 1 into the slot
         u32x2 mh[4];
         uint32_t open = 1;  // any key not at -inf (f16 0xFC00)
         if constexpr (HM) {
             bd_vm_wait<KT, D, HM>(wave, s + 2 < ntiles ? 1 : 0, 0);
             open = 0;
+            const uint8_t* ms = smem + C::maskOff + wave * C::maskSlot + c32 * 16 + h * 8;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                reg_fence(mk[u]);
-                mh[u] = h ? u32x2{mk[u].z, mk[u].w} : u32x2{mk[u].x, mk[u].y};
+                mh[u] = *(const u32x2*)(ms + u * 512);
                 open |= (mh[u].x ^ 0xFC00FC00u) | (mh[u].y ^ 0xFC00FC00u);
             }
-            if (s + 1 < ntiles) mask_issue(s + 1, mk);
+            if (s + 1 < ntiles) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot has been read
+                mask_issue(s + 1);
+            }
         }
 #ifdef FATTN_MQ_NOCOMPUTE
         continue;  // diagnostic build only: copies, V dequant and barriers

@@ -458,75 +458,68 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             live = __builtin_amdgcn_ballot_w64(open != 0) != 0;
         }
         if (live) {
-        // -- S^T = K.Q^T: two 32-key subtiles; each subtile's 8 K operands are
-        // read before its MFMA chain (one LDS wait per chain, not per MFMA)
-        f32x16 st[2];
+        // -- one tile, phases overlapped within the wave (cdna_hip_programming.md
+        // T19): the two subtiles' S^T chains back to back, the scores of subtile 0
+        // (u = fma(s, scale, mask)) computed under subtile 1's MFMAs, subtile 0's
+        // exponentials under nothing but their own latency, then subtile 1's
+        // exponentials under subtile 0's P.V MFMAs.  Same arithmetic as before
+        // (one max over the tile's 64 keys, one deferred-rescale decision).
+        // K operands of both subtiles first (16 ds_read_b128): one LDS wait
+        f16x8 ka[2][NK];
 #pragma unroll
         for (int t = 0; t < 2; t++) {
-            f16x8 ka[NK];
 #pragma unroll
-            for (int kk = 0; kk < NK; kk++) ka[kk] = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024);
-            __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the chain
-#pragma unroll
-            for (int j = 0; j < 16; j++) st[t][j] = 0.0f;
-#pragma unroll
-            for (int kk = 0; kk < NK; kk++) st[t] = mfma32(ka[kk], qop[kk], st[t]);
+            for (int kk = 0; kk < NK; kk++) ka[t][kk] = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024);
         }
-
-#ifdef FATTN_STAMPS
-        {   // wait for the S^T results before the stamp
-            float z = 0.0f;
-            for (int t = 0; t < 2; t++) z += st[t][0] + st[t][15];
-            asm volatile("" ::"v"(z));
-        }
-#endif
-        PF_T(3);
-        // -- scores (natural units) u = scale * s + mask; element j of subtile t
-        // is key 32t + 8(j/4) + 4h + (j%4) of this lane's row
-        float u[2][16];
-        if constexpr (HM) {
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 st0, st1;
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
+        for (int j = 0; j < 16; j++) st0[j] = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < NK; kk++) st0 = mfma32(ka[0][kk], qop[kk], st0);
+#pragma unroll
+        for (int j = 0; j < 16; j++) st1[j] = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < NK; kk++) st1 = mfma32(ka[1][kk], qop[kk], st1);
+        // scores (natural units) u = scale * s + mask; element j of subtile t is
+        // key 32t + 8(j/4) + 4h + (j%4) of this lane's row.  Subtile 0's depend
+        // only on st0: the scheduler places them between st1's MFMAs.
+        auto scores = [&](const f32x16& stt, int t, float (&ut)[16]) {
+            if constexpr (HM) {
 #pragma unroll
                 for (int uu = 0; uu < 4; uu++) {
                     const f16x2 m01 = as_h2(mk[t][uu].x), m23 = as_h2(mk[t][uu].y);
-                    u[t][4 * uu + 0] = fmaf(st[t][4 * uu + 0], scale, (float)m01.x);
-                    u[t][4 * uu + 1] = fmaf(st[t][4 * uu + 1], scale, (float)m01.y);
-                    u[t][4 * uu + 2] = fmaf(st[t][4 * uu + 2], scale, (float)m23.x);
-                    u[t][4 * uu + 3] = fmaf(st[t][4 * uu + 3], scale, (float)m23.y);
+                    ut[4 * uu + 0] = fmaf(stt[4 * uu + 0], scale, (float)m01.x);
+                    ut[4 * uu + 1] = fmaf(stt[4 * uu + 1], scale, (float)m01.y);
+                    ut[4 * uu + 2] = fmaf(stt[4 * uu + 2], scale, (float)m23.x);
+                    ut[4 * uu + 3] = fmaf(stt[4 * uu + 3], scale, (float)m23.y);
                 }
-            }
-        } else {
+            } else {
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
-#pragma unroll
-                for (int j = 0; j < 16; j++) u[t][j] = st[t][j];
+                for (int j = 0; j < 16; j++) ut[j] = stt[j];
             }
+        };
+        float u0[16], u1[16];
+        scores(st0, 0, u0);
+        float tmax0 = kNegInf;
+#pragma unroll
+        for (int j = 0; j < 16; j++) tmax0 = fmaxf(tmax0, u0[j]);
+        // st0's chain alone, then one MFMA of st1's chain, then up to 4 of
+        // subtile 0's VALU
+        __builtin_amdgcn_sched_group_barrier(0x008, NK, 0);
+#pragma unroll
+        for (int i = 0; i < NK; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
+        scores(st1, 1, u1);
+        float tmax = tmax0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) tmax = fmaxf(tmax, u1[j]);
         // exponent argument: x * c - m (log2 domain); c = log2e with a mask,
         // scale * log2e without (scale > 0: the planner's condition)
         const float c = HM ? log2e : a.scale_log2;
-#ifdef FATTN_PF_NOSOFTMAX
-        // diagnostic build only: P = raw scores (MFMA + LDS reads, no softmax)
-        f16x8 pb[2][2];
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-#pragma unroll
-            for (int q = 0; q < 2; q++) {
-                f16x8 x;
-#pragma unroll
-                for (int i = 0; i < 8; i++) x[i] = (f16)u[t][8 * q + i];
-                pb[t][q] = x;
-            }
-        }
-        l2.x += 1.0f;
-#else
-        float tmax = kNegInf;
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) tmax = fmaxf(tmax, u[t][j]);
-        }
         tmax = xor32_pair(tmax, true) * c;
         // deferred max (cdna_hip_programming.md T13), as in the multi-query kernel
         if (__builtin_amdgcn_ballot_w64(tmax > m_run + kDeferLog2)) {
@@ -538,12 +531,10 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             m_run = m_new;
         }
         const float nm = (m_run == kNegInf) ? 0.0f : -m_run;
-        f16x8 pb[2][2];
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
+        auto probs = [&](const float (&ut)[16], f16x8 (&pbt)[2]) {
             float pv[16];
 #pragma unroll
-            for (int j = 0; j < 16; j++) pv[j] = __builtin_amdgcn_exp2f(fmaf(u[t][j], c, nm));
+            for (int j = 0; j < 16; j++) pv[j] = __builtin_amdgcn_exp2f(fmaf(ut[j], c, nm));
 #pragma unroll
             for (int j = 0; j < 16; j += 2) l2 += f32x2{pv[j], pv[j + 1]};
 #pragma unroll
@@ -551,48 +542,53 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
                 f16x8 x;
                 x.s0 = (f16)pv[8 * q]; x.s1 = (f16)pv[8 * q + 1]; x.s2 = (f16)pv[8 * q + 2]; x.s3 = (f16)pv[8 * q + 3];
                 x.s4 = (f16)pv[8 * q + 4]; x.s5 = (f16)pv[8 * q + 5]; x.s6 = (f16)pv[8 * q + 6]; x.s7 = (f16)pv[8 * q + 7];
-                pb[t][q] = x;
+                pbt[q] = x;
             }
-        }
-#endif
-
-#ifdef FATTN_STAMPS
-        {
-            uint32_t z = 0;
-            for (int t = 0; t < 2; t++) z += __builtin_bit_cast(u32x4, pb[t][0]).x + __builtin_bit_cast(u32x4, pb[t][1]).w;
-            asm volatile("" ::"v"(z));
-        }
-#endif
-        PF_T(4);
-        // -- O^T += V^T.P^T: k-step (t, q) covers keys 32t + 16q + 8(i/4) + 4h + (i%4)
-        // of k-group h (i = 0..7); V^T gathered in that order (rows + 0 / + 8)
-        // (per k-step: the 8 transposed reads of its 4 dim blocks, then 4 MFMAs)
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
+        };
+        // V^T operands of subtile t, k-step q: keys 32t + 16q + 8(i/4) + 4h + (i%4)
+        // of k-group h (i = 0..7), gathered by ds_read_b64_tr_b16
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        auto v_reads = [&](int t, u32x4 (&va)[2][NDB]) {
 #pragma unroll
             for (int q = 0; q < 2; q++) {
-                typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-                u32x4 va[NDB];
 #pragma unroll
                 for (int db = 0; db < NDB; db++) {
                     const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
                     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[0] + off));
                     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[1] + off));
                     const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
-                    va[db] = u32x4{a2.x, a2.y, b2.x, b2.y};
+                    va[q][db] = u32x4{a2.x, a2.y, b2.x, b2.y};
                 }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[t][q], o[db]);
             }
+        };
+        f16x8 pb0[2], pb1[2];
+        u32x4 va0[2][NDB];
+        v_reads(0, va0);          // their LDS latency runs under subtile 0's exponentials
+        probs(u0, pb0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 64, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        // subtile 0's P.V (8 MFMAs) with subtile 1's exponentials between them
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+#pragma unroll
+            for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va0[q][db]), pb0[q], o[db]);
         }
-#ifdef FATTN_STAMPS
-        {
-            float z = 0.0f;
-            for (int db = 0; db < NDB; db++) z += o[db][0];
-            asm volatile("" ::"v"(z));
+        probs(u1, pb1);
+#pragma unroll
+        for (int i = 0; i < 2 * NDB; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
         }
-#endif
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 va1[2][NDB];
+        v_reads(1, va1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+#pragma unroll
+            for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va1[q][db]), pb1[q], o[db]);
+        }
         }  // live
         PF_T(5);
         if (late) {

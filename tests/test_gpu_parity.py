@@ -257,6 +257,25 @@ def test_bd_sweep(dev, bd_force, case):
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
+@pytest.mark.parametrize("case,chunk", [
+    (dict(NQ=1024, H=8, N=1024, mask="causal"), 0),   # 16 query tiles x 2 chunks of 4 tiles
+    (dict(NQ=1024, H=8, N=1024, mask="random"), 0),
+    (dict(NQ=64, H=1, N=512, mask="causal"), 512),     # one workgroup, 4 tiles, one chunk
+    (dict(NQ=64, H=1, N=512, mask="random"), 512),
+    (dict(NQ=64, H=1, N=512, mask="neginf_blocks"), 512),
+    (dict(NQ=64, H=4, N=4096, mask="neginf_blocks"), 1024),
+], ids=["causal-16qt", "random-16qt", "causal-1wg", "random-1wg", "neginf-1wg", "neginf-8tiles"])
+def test_bd_masked_multitile(dev, bd_force, case, chunk):
+    """Masked problems whose workgroups walk several 128-key tiles: the mask
+    of tile s + 1 is fetched while tile s computes (a one-workgroup launch
+    leaves the least time for it to land).  A register-held form of that
+    prefetch failed exactly these cases (rows 31 / 63 NaN)."""
+    p = make_problem(D=128, kv_type="q8_0", seed=43, **case)
+    got, ref = run_gpu(p, kv_chunk=chunk), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 @pytest.mark.parametrize("chunk", [128, 384, 1024, 100000])
 def test_bd_chunking_invariance(dev, bd_force, chunk):
     p = make_problem(D=128, NQ=64, H=4, N=2048, kv_type="q8_0", seed=27)
