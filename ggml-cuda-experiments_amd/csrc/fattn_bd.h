@@ -267,14 +267,15 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
         vbase[e] = C::img + kq * 2048 + row * 64 + ch * 16 + (gi & 1) * 8;
     }
 
-    // ---- this wave's issue order: prologue raw 0 | raw 1 | mask 0, then per
-    // tile s: raw s + 2 (after the first barrier) | mask s + 1 (once mask s has
-    // been read).  So at the top of tile s, mask s - 1 (s >= 1), raw s + 1 and
-    // mask s were issued after raw s; after the second barrier only raw s + 2
-    // was issued after mask s.
+    // ---- this wave's issue order: prologue mask 0 | raw 0 | raw 1, then per
+    // tile s, once the images are built and mask s has been read out of the
+    // slot: mask s + 1 | raw s + 2.  vmcnt retires in issue order, so each
+    // mask goes BEFORE the raw tile that is two ahead: at the top of tile s
+    // only mask s and raw s + 1 were issued after raw s, and only raw s + 1
+    // after mask s -- tile s computes while tile s + 1 is still in flight.
+    if (ntiles > 0) mask_issue(0);
     if (ntiles > 0) bd_issue<KT, D>(rs, c_lo, raw_lds(0), wave, lane);
     if (ntiles > 1) bd_issue<KT, D>(rs, c_lo + kBdKeys, raw_lds(1), wave, lane);
-    if (ntiles > 0) mask_issue(0);
 
     float m_run = kNegInf;    // reference max (log2 domain) of this lane's row
     f32x2 l2 = {0.0f, 0.0f};  // this lane's partial row sums (16 of every 32 keys)
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     const float scale = a.scale;
 
     FATTN_STAMP(1);
-    // Q landed (raw 0, raw 1 and mask 0 may fly on); every wave's Q pieces in LDS
+    // Q landed (mask 0, raw 0 and raw 1 may fly on); every wave's Q pieces in LDS
     {
         const int n1 = ntiles > 1 ? 1 : 0, n0 = ntiles > 0 ? 1 : 0;
         bd_vm_wait<KT, D, HM>(wave, n0 + n1, n0);
@@ -311,26 +312,27 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     FATTN_STAMP(2);
 
     for (int s = 0; s < ntiles; s++) {
-        // raw s landed (mask s - 1 (s >= 1), raw s + 1, mask s may fly on)
-        bd_vm_wait<KT, D, HM>(wave, s + 1 < ntiles ? 1 : 0, s > 0 ? 2 : 1);
+        // raw s landed (mask s (s >= 1) and raw s + 1 may fly on)
+        bd_vm_wait<KT, D, HM>(wave, s + 1 < ntiles ? 1 : 0, s > 0 ? 1 : 0);
         if (s < 4) FATTN_STAMP(3 + 2 * s);
         // every wave's pieces of raw s landed; every wave is done with tile
         // s - 1 (the images are free)
         __syncthreads();
         if (s == 0) FATTN_STAMP(14);
         bd_dequant<KT, D>(raw_ptr(s), smem, smem + C::img, wave, lane);
-        // the images are complete and raw s's slot is free: tile s + 2 into it
-        // (a DMA issue that stalls on a full memory queue now overlaps the
-        // other waves' compute instead of holding a barrier)
+        // the images are complete and raw s's slot is free
         __syncthreads();
         if (s == 0) FATTN_STAMP(15);
-        if (s + 2 < ntiles) bd_issue<KT, D>(rs, c_lo + (s + 2) * kBdKeys, raw_lds(s + 2), wave, lane);
         // this lane's mask values of tile s (keys 8 u + 4 h + 0..3 of the
-        // quarter) out of the wave's slot, then mask s + 1 into the slot
+        // quarter) out of the wave's slot (mask s landed: only raw s + 1 was
+        // issued after it; mask 0 went before raw 0), then mask s + 1 into the
+        // slot, then tile s + 2 into raw s's slot (a DMA issue that stalls on
+        // a full memory queue overlaps the other waves' compute instead of
+        // holding a barrier)
         u32x2 mh[4];
         uint32_t open = 1;  // any key not at -inf (f16 0xFC00)
         if constexpr (HM) {
-            bd_vm_wait<KT, D, HM>(wave, s + 2 < ntiles ? 1 : 0, 0);
+            if (s > 0) bd_vm_wait<KT, D, HM>(wave, s + 1 < ntiles ? 1 : 0, 0);
             open = 0;
             const uint8_t* ms = smem + C::maskOff + wave * C::maskSlot + c32 * 16 + h * 8;
 #pragma unroll
@@ -343,6 +345,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
                 mask_issue(s + 1);
             }
         }
+        if (s + 2 < ntiles) bd_issue<KT, D>(rs, c_lo + (s + 2) * kBdKeys, raw_lds(s + 2), wave, lane);
 #ifdef FATTN_MQ_NOCOMPUTE
         continue;  // diagnostic build only: copies, V dequant and barriers
 #endif

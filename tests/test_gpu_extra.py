@@ -290,11 +290,11 @@ def split_waves(request):
     waves, no_skip = request.param
     fattn.set_option(fattn.OPT_SPLIT_WAVES, waves)
     fattn.set_option(fattn.OPT_SPLIT_SKIP, no_skip)
-    fattn.set_option(fattn.OPT_BD, 1)  # the config-5 shard case exercises the split kernel
+    fattn.set_option(fattn.OPT_MQ_DISABLE, 1)  # the config-5 shard case exercises the split kernel
     yield request.param
     fattn.set_option(fattn.OPT_SPLIT_WAVES, 0)
     fattn.set_option(fattn.OPT_SPLIT_SKIP, 0)
-    fattn.set_option(fattn.OPT_BD, 0)
+    fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
 
 
 DEC_CASES = [
@@ -371,7 +371,7 @@ def test_multirow_merge_paths(dev, case, fused):
     p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
     t = upload(p, dev)
     fattn.set_option(fattn.OPT_SPLIT_MERGE, fused)
-    fattn.set_option(fattn.OPT_BD, 1)  # config 5's shard would take the batched-decode kernel
+    fattn.set_option(fattn.OPT_MQ_DISABLE, 1)  # config 5's shard would take the batched-decode kernel
     try:
         att = fattn.Attention(*views(p, t), t["dst"], p.scale)
         d = att.describe()
@@ -380,7 +380,7 @@ def test_multirow_merge_paths(dev, case, fused):
         assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
     finally:
         fattn.set_option(fattn.OPT_SPLIT_MERGE, 0)
-        fattn.set_option(fattn.OPT_BD, 0)
+        fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
 
 
 # ------------------------------------------------------------------ quantize-on-write (fattn_cpy)
