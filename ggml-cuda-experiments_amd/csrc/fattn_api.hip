@@ -84,10 +84,16 @@ Geom geom_of() {
 Geom geom(int kt, int vt, int D) {
     auto pick = [&](auto d) -> Geom {
         constexpr int DD = decltype(d)::value;
-        if (kt == FATTN_TYPE_Q8_0) return geom_of<FATTN_TYPE_Q8_0, FATTN_TYPE_Q8_0, DD>();
-        if (kt == FATTN_TYPE_Q4_0) return geom_of<FATTN_TYPE_Q4_0, FATTN_TYPE_Q4_0, DD>();
-        if (vt == VT_F16T) return geom_of<FATTN_TYPE_F16, VT_F16T, DD>();
-        return geom_of<FATTN_TYPE_F16, FATTN_TYPE_F16, DD>();
+        auto with_v = [&](auto k) -> Geom {
+            constexpr int KK = decltype(k)::value;
+            if (vt == FATTN_TYPE_Q8_0) return geom_of<KK, FATTN_TYPE_Q8_0, DD>();
+            if (vt == FATTN_TYPE_Q4_0) return geom_of<KK, FATTN_TYPE_Q4_0, DD>();
+            if (vt == VT_F16T) return geom_of<KK, VT_F16T, DD>();
+            return geom_of<KK, FATTN_TYPE_F16, DD>();
+        };
+        if (kt == FATTN_TYPE_Q8_0) return with_v(std::integral_constant<int, FATTN_TYPE_Q8_0>());
+        if (kt == FATTN_TYPE_Q4_0) return with_v(std::integral_constant<int, FATTN_TYPE_Q4_0>());
+        return with_v(std::integral_constant<int, FATTN_TYPE_F16>());
     };
     switch (D) {
         case 64: return pick(std::integral_constant<int, 64>());
@@ -343,7 +349,10 @@ int make_plan(const fattn_params* p, Plan& pl) {
     if (N > (int64_t)1 << 30 || NQ * H * S > (int64_t)1 << 31) return FATTN_ERR_INVALID_ARG;
     if (k.type != FATTN_TYPE_F16 && !is_quant(k.type)) return FATTN_ERR_UNSUPPORTED_TYPE;
     if (v.type != FATTN_TYPE_F16 && !is_quant(v.type)) return FATTN_ERR_UNSUPPORTED_TYPE;
-    if (k.type != v.type) return FATTN_ERR_UNSUPPORTED_TYPE;  // mixed K/V types: not instantiated
+    // mixed K/V types (llama.cpp's separate cache types, e.g. K Q8_0 with V F16):
+    // the split kernel, head dims 64 / 128 / 256
+    const bool mixed = k.type != v.type;
+    if (mixed && D != 64 && D != 128 && D != 256) return FATTN_ERR_UNSUPPORTED_TYPE;
     if ((uintptr_t)q.data % 16 || q.nb[1] % 16 || q.nb[2] % 16 || q.nb[3] % 16) return FATTN_ERR_ALIGNMENT;
 
     const size_t rowK = fattn_row_size(k.type, D), rowV = fattn_row_size(v.type, D);
@@ -367,19 +376,17 @@ int make_plan(const fattn_params* p, Plan& pl) {
         if ((uintptr_t)mk.data % 4 || mk.nb[1] % 4) return FATTN_ERR_ALIGNMENT;
     }
 
-    // fast path: 16-B pieces
-    bool g16 = true;
-    if (is_quant(k.type)) {
-        g16 = g16 && k.nb[1] == (int64_t)rowK && N % kStep == 0 && (uintptr_t)k.data % 16 == 0 && k.nb[2] % 16 == 0 &&
-              k.nb[3] % 16 == 0;
-        g16 = g16 && v.nb[1] == (int64_t)rowV && (uintptr_t)v.data % 16 == 0 && v.nb[2] % 16 == 0 && v.nb[3] % 16 == 0;
-    } else {
-        g16 = g16 && (uintptr_t)k.data % 16 == 0 && k.nb[1] % 16 == 0 && k.nb[2] % 16 == 0 && k.nb[3] % 16 == 0;
-        if (!v_trans)
-            g16 = g16 && (uintptr_t)v.data % 16 == 0 && v.nb[1] % 16 == 0 && v.nb[2] % 16 == 0 && v.nb[3] % 16 == 0;
-        else
-            g16 = g16 && v.nb[2] % 16 == 0 && v.nb[3] % 16 == 0;
-    }
+    // fast path: 16-B pieces.  Quantised rows: contiguous per head (a step of
+    // 32 rows is one run of bytes); f16 rows: 16-B aligned
+    auto rows16 = [&](const fattn_tensor& t, size_t row) {
+        const bool base = (uintptr_t)t.data % 16 == 0 && t.nb[2] % 16 == 0 && t.nb[3] % 16 == 0;
+        return is_quant(t.type) ? base && t.nb[1] == (int64_t)row && N % kStep == 0 : base && t.nb[1] % 16 == 0;
+    };
+    bool g16 = rows16(k, rowK);
+    if (!v_trans)
+        g16 = g16 && rows16(v, rowV);
+    else
+        g16 = g16 && v.nb[2] % 16 == 0 && v.nb[3] % 16 == 0;
     if (has_mask) g16 = g16 && (uintptr_t)mk.data % 16 == 0 && mk.nb[1] % 16 == 0 && N % kStep == 0;
     if (!g16 && v_trans) return FATTN_ERR_BAD_STRIDE;
     // the dword-granular path needs dword rows (D = 96 Q8_0 / Q4_0 rows are 102 / 54 B:
@@ -430,7 +437,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // are packed (R = rk2, a power of two <= 64).
     // (below 256 packed rows per kv head the split kernel measures faster:
     // config 5, 64 rows, 15.5 vs 37.6 us at 4 heads; FATTN_OPT_MQ_MIN_ROWS)
-    const bool mq_ok = !g_opt_mq_disable && is_quant(k.type) && g16 && (D == 64 || D == 128) && NQ * a.rk2 >= 32 &&
+    const bool mq_ok = !g_opt_mq_disable && !mixed && is_quant(k.type) && g16 && (D == 64 || D == 128) && NQ * a.rk2 >= 32 &&
                        a.rk2 <= 64 &&
                        (a.rk2 & (a.rk2 - 1)) == 0;
     pl.mq = mq_ok && NQ * a.rk2 >= g_opt_mq_min_rows;
@@ -451,7 +458,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // (f16 K/V rows, not transposed V: the same kernel, images filled by DMA)
     pl.pf = false;
     const bool heads_ok = NQ * a.rk2 >= 32 && a.rk2 <= 64 && (a.rk2 & (a.rk2 - 1)) == 0;
-    const bool pf_f16 = !g_opt_mq_disable && k.type == FATTN_TYPE_F16 && !v_trans && g16 && heads_ok;
+    const bool pf_f16 = !g_opt_mq_disable && !mixed && k.type == FATTN_TYPE_F16 && !v_trans && g16 && heads_ok;
     if ((mq_ok || pf_f16) && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
         p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= pl.cus)) {
         pl.pf = true;

@@ -200,10 +200,30 @@ int launch_pf(const Plan& pl, hipStream_t st, const Events& ev) {
     return pl.a.has_mask ? launch_pf_hm<KT, true>(pl, st, ev) : launch_pf_hm<KT, false>(pl, st, ev);
 }
 
+// split kernel over mixed K / V cache types (instantiated once per D in
+// fattn_launch_mixed_d<D>.hip; D = 64, 128, 256)
+template <int D>
+int launch_mixed(const Plan& pl, hipStream_t st, const Events& ev) {
+    constexpr int F16 = FATTN_TYPE_F16, Q8 = FATTN_TYPE_Q8_0, Q4 = FATTN_TYPE_Q4_0;
+    if (pl.kt == Q8 && pl.vt == F16) return launch_gran<Q8, F16, D>(pl, st, ev);
+    if (pl.kt == Q4 && pl.vt == F16) return launch_gran<Q4, F16, D>(pl, st, ev);
+    if (pl.kt == F16 && pl.vt == Q8) return launch_gran<F16, Q8, D>(pl, st, ev);
+    if (pl.kt == F16 && pl.vt == Q4) return launch_gran<F16, Q4, D>(pl, st, ev);
+    if (pl.kt == Q8 && pl.vt == Q4) return launch_gran<Q8, Q4, D>(pl, st, ev);
+    if (pl.kt == Q4 && pl.vt == Q8) return launch_gran<Q4, Q8, D>(pl, st, ev);
+    return FATTN_ERR_UNSUPPORTED_TYPE;
+}
+extern template int launch_mixed<64>(const Plan&, hipStream_t, const Events&);
+extern template int launch_mixed<128>(const Plan&, hipStream_t, const Events&);
+extern template int launch_mixed<256>(const Plan&, hipStream_t, const Events&);
+
 // every kernel of head dim D (defined here, instantiated once per D in
 // fattn_launch_d<D>.hip)
 template <int D>
 int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
+    if constexpr (D == 64 || D == 128 || D == 256) {
+        if (pl.kt != pl.vt && pl.vt != VT_F16T) return launch_mixed<D>(pl, st, ev);
+    }
     if constexpr (D == 128) {
         if (pl.pf) {
             if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_pf<FATTN_TYPE_F16>(pl, st, ev);

@@ -81,8 +81,10 @@ typedef struct fattn_tensor {
 /* GGML_OP_FLASH_ATTN_EXT:
  *   q    f32  ne = [D, n_q, H, S]        (any nb with nb[0] == 4)
  *   k    F16/Q8_0/Q4_0  ne = [D, N, Hkv, Skv]  rows contiguous (nb[0] = type size)
- *   v    same type family as k, ne = [D, N, Hkv, Skv]; rows contiguous, or for
- *        F16 only transposed (nb[1] == 2, nb[0] == N*2 style strides)
+ *   v    F16/Q8_0/Q4_0  ne = [D, N, Hkv, Skv]; rows contiguous, or for F16 only
+ *        transposed (nb[1] == 2, nb[0] == N*2 style strides).  v's type may
+ *        differ from k's (llama.cpp's separate K / V cache types) at D = 64,
+ *        128 and 256: the split-KV kernel takes every such pair
  *   mask F16 ne = [N', rows >= n_q] with N' >= N rounded up to even (ggml pads
  *        mask rows to GGML_KQ_MASK_PAD), 4-byte aligned rows; row = query
  *        index, broadcast over heads and sequences; or data == NULL for no mask
@@ -96,22 +98,27 @@ typedef struct fattn_params {
     float* dst;
     float scale;
     int32_t kv_chunk;      /* split-KV chunk length in positions; 0 = auto */
-    void* workspace;       /* split-KV scratch, >= fattn_workspace_size() bytes.  Its arrival
-                              words are stamped with a fresh epoch by every launch, so
-                              neither zeroing nor a clean previous launch is required
-                              (fattn_workspace_init zeroes it all the same); launches that
-                              share one workspace must be ordered on one stream */
+    void* workspace;       /* split-KV scratch, >= fattn_workspace_size() bytes.  Zero a new
+                              allocation once (fattn_workspace_init): a launch stamps its
+                              arrival words with a fresh epoch by atomic max, which
+                              supersedes any word an earlier launch left (re-armed, or
+                              mid-count after an abort) and any word whose top 16 bits are
+                              not all ones -- but an uninitialised word that happens to
+                              read 0xFFFF in its top bits with an epoch field ahead of the
+                              launch's would outrank the stamp.  No re-zeroing is needed
+                              between launches.  Launches that share one workspace must be
+                              ordered on one stream */
     size_t workspace_bytes;
 } fattn_params;
 
 size_t fattn_workspace_size(const fattn_params* p);
-/* Zero a workspace (hipMemsetAsync on `stream`).  Optional: the split-KV chunks
- * of a tile meet through 64-bit arrival words kept at the front of the
- * workspace, [0xFFFF | epoch:32 | count:16]; each launch stamps them with its
- * own epoch (atomic max) before counting, so memory left by an earlier or an
- * aborted launch, or never initialised, is superseded -- except a word whose
- * top 16 bits are all ones with an epoch above the current one (e.g. 0xFF
- * fill), which this call clears. */
+/* Zero a workspace (hipMemsetAsync on `stream`); call once per allocation.  The
+ * split-KV chunks of a tile meet through 64-bit arrival words kept at the front
+ * of the workspace, [0xFFFF | epoch:32 | count:16]; each launch stamps them with
+ * its own epoch (atomic max) before counting, so memory left by an earlier or an
+ * aborted launch is superseded -- but not a never-initialised word whose top
+ * 16 bits are all ones with an epoch above the current one (e.g. 0xFF fill),
+ * which this call clears. */
 int fattn_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 int fattn_ext(const fattn_params* p, void* stream);
 

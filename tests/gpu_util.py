@@ -23,7 +23,7 @@ def upload(prob: Problem, dev="cuda"):
 def views(prob: Problem, t):
     qv = fattn.View(t["q"].data_ptr(), fattn.TYPE_F32, prob.q_ne, prob.q_nb)
     kv = fattn.View(t["k"].data_ptr(), prob.kv_type, prob.kv_ne, prob.k_nb)
-    vv = fattn.View(t["v"].data_ptr(), prob.kv_type, prob.kv_ne, prob.v_nb)
+    vv = fattn.View(t["v"].data_ptr(), prob.v_type, prob.kv_ne, prob.v_nb)
     mv = fattn.View(t["mask"].data_ptr(), fattn.TYPE_F16, prob.mask_ne, prob.mask_nb) if t["mask"] is not None else None
     return qv, kv, vv, mv
 

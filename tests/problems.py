@@ -48,6 +48,11 @@ class Problem:
     v_trans: bool = False
     k_f32: np.ndarray = field(default=None, repr=False)   # logical [Skv][Hkv][N][D] before encoding
     v_f32: np.ndarray = field(default=None, repr=False)
+    v_type: Optional[int] = None                           # V cache type (None: kv_type)
+
+    def __post_init__(self):
+        if self.v_type is None:
+            self.v_type = self.kv_type
 
     # ggml views -------------------------------------------------------
     @property
@@ -79,7 +84,7 @@ class Problem:
     def oracle(self, n_threads=8) -> np.ndarray:
         q = (np.ascontiguousarray(self.q), orc.TYPE_F32, self.q_ne, self.q_nb)
         k = (self.k_bytes, self.kv_type, self.kv_ne, self.k_nb)
-        v = (self.v_bytes, self.kv_type, self.kv_ne, self.v_nb)
+        v = (self.v_bytes, self.v_type, self.kv_ne, self.v_nb)
         m = None
         if self.mask_bits is not None:
             m = (np.ascontiguousarray(self.mask_bits), orc.TYPE_F16, self.mask_ne, self.mask_nb)
@@ -87,9 +92,9 @@ class Problem:
 
     def algorithmic_bytes(self) -> int:
         """Q (f32) + K + V (stored) + mask (f16, n_q rows) + O (f32), each once."""
-        rb = row_bytes(self.kv_type, self.D)
+        rb = row_bytes(self.kv_type, self.D) + row_bytes(self.v_type, self.D)
         qo = self.S * self.NQ * self.H * self.D * 4
-        kv = 2 * self.Skv * self.Hkv * self.N * rb
+        kv = self.Skv * self.Hkv * self.N * rb
         mk = self.NQ * self.N * 2 if self.mask_bits is not None else 0
         return qo * 2 + kv + mk
 
@@ -99,12 +104,14 @@ class Problem:
 
 def make_problem(D=128, NQ=1, H=32, Hkv=None, N=4096, kv_type="q8_0", S=1, Skv=None, layout="head",
                  mask="random", seed=0, scale=None, v_trans=False, mask_pad=64, extreme=False,
-                 ramp=0.0) -> Problem:
+                 ramp=0.0, v_type=None) -> Problem:
     """Random problem.  mask: "none" | "random" (U[-1,1], like kernel_test.h:48) |
     "zero" | "causal" (query i sees positions <= N - NQ + i) | "neginf_blocks"
     (some 32-position blocks fully -inf for every row) | "tail" (a padded cache:
-    -inf from ~3N/8 on, so whole chunks of the split are masked)."""
+    -inf from ~3N/8 on, so whole chunks of the split are masked).  v_type: a V
+    cache type other than kv_type (llama.cpp's separate K / V cache types)."""
     typ = TYPES[kv_type] if isinstance(kv_type, str) else kv_type
+    vtyp = typ if v_type is None else (TYPES[v_type] if isinstance(v_type, str) else v_type)
     Hkv = H if Hkv is None else Hkv
     Skv = S if Skv is None else Skv
     rng = np.random.default_rng(seed)
@@ -122,33 +129,28 @@ def make_problem(D=128, NQ=1, H=32, Hkv=None, N=4096, kv_type="q8_0", S=1, Skv=N
         q *= 4.0
         k *= (1.0 + ramp * np.arange(N, dtype=np.float32) / max(N, 1))[:, None]
     scale = 1.0 / np.sqrt(np.float32(D)) if scale is None else scale
-    rb = row_bytes(typ, D)
-    k_rows = encode_rows(k, typ)   # [Skv][Hkv][N][rb]
-    v_rows = encode_rows(v, typ)
-    eb = 2 if typ == orc.TYPE_F16 else orc.BLOCK_BYTES[typ]
-    if layout == "head":
-        k_buf = np.ascontiguousarray(k_rows)
-        v_buf = np.ascontiguousarray(v_rows)
-        k_nb = (eb, rb, rb * N, rb * N * Hkv)
-        v_nb = k_nb
-    elif layout == "pos":
-        k_buf = np.ascontiguousarray(k_rows.transpose(0, 2, 1, 3))  # [Skv][N][Hkv][rb]
-        v_buf = np.ascontiguousarray(v_rows.transpose(0, 2, 1, 3))
-        k_nb = (eb, rb * Hkv, rb, rb * N * Hkv)
-        v_nb = k_nb
-    elif layout == "padded":
-        # rows with a stride larger than the row (forces the dword-granular path)
-        pad = rb + 8
-        k_buf = np.zeros((Skv, Hkv, N, pad), dtype=np.uint8)
-        v_buf = np.zeros((Skv, Hkv, N, pad), dtype=np.uint8)
-        k_buf[..., :rb] = k_rows
-        v_buf[..., :rb] = v_rows
-        k_nb = (eb, pad, pad * N, pad * N * Hkv)
-        v_nb = k_nb
-    else:
+    k_rows = encode_rows(k, typ)   # [Skv][Hkv][N][row bytes]
+    v_rows = encode_rows(v, vtyp)
+
+    def place(rows, t):
+        rb = row_bytes(t, D)
+        eb = 2 if t == orc.TYPE_F16 else orc.BLOCK_BYTES[t]
+        if layout == "head":
+            return np.ascontiguousarray(rows), (eb, rb, rb * N, rb * N * Hkv)
+        if layout == "pos":
+            return np.ascontiguousarray(rows.transpose(0, 2, 1, 3)), (eb, rb * Hkv, rb, rb * N * Hkv)  # [Skv][N][Hkv][rb]
+        if layout == "padded":
+            # rows with a stride larger than the row (forces the dword-granular path)
+            pad = rb + 8
+            buf = np.zeros((Skv, Hkv, N, pad), dtype=np.uint8)
+            buf[..., :rb] = rows
+            return buf, (eb, pad, pad * N, pad * N * Hkv)
         raise ValueError(layout)
+
+    k_buf, k_nb = place(k_rows, typ)
+    v_buf, v_nb = place(v_rows, vtyp)
     if v_trans:
-        assert typ == orc.TYPE_F16
+        assert typ == orc.TYPE_F16 and vtyp == orc.TYPE_F16
         vt = orc.f32_to_f16_bits(np.ascontiguousarray(v.transpose(0, 1, 3, 2)))  # [Skv][Hkv][D][N]
         v_buf = vt.view(np.uint8)
         v_nb = (N * 2, 2, D * N * 2, D * N * 2 * Hkv)
@@ -177,7 +179,7 @@ def make_problem(D=128, NQ=1, H=32, Hkv=None, N=4096, kv_type="q8_0", S=1, Skv=N
             raise ValueError(mask)
         mask_bits = orc.f32_to_f16_bits(m)
     return Problem(D, NQ, H, Hkv, N, S, Skv, typ, layout, float(np.float32(scale)), q, k_buf.reshape(-1).view(np.uint8),
-                   v_buf.reshape(-1).view(np.uint8), k_nb, v_nb, mask_bits, v_trans, k, v)
+                   v_buf.reshape(-1).view(np.uint8), k_nb, v_nb, mask_bits, v_trans, k, v, vtyp)
 
 
 def attn_rel_err(got: np.ndarray, ref: np.ndarray) -> float:

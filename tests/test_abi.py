@@ -46,13 +46,14 @@ def test_strerror_and_sizes():
     assert fattn.lib().fattn_version().startswith(b"fattn-gfx950")
 
 
-def _params(D=128, NQ=1, H=32, Hkv=32, N=4096, kt=fattn.TYPE_Q8_0, kv_chunk=0, ptr=1 << 20, mask=True):
-    rb = fattn.row_size(kt, D)
-    eb = 2 if kt == fattn.TYPE_F16 else fattn.BLOCK_BYTES.get(kt, 4)
+def _params(D=128, NQ=1, H=32, Hkv=32, N=4096, kt=fattn.TYPE_Q8_0, kv_chunk=0, ptr=1 << 20, mask=True, vt=None):
+    def view(t):
+        rb = fattn.row_size(t, D)
+        eb = 2 if t == fattn.TYPE_F16 else fattn.BLOCK_BYTES.get(t, 4)
+        return fattn.View(ptr, t, (D, N, Hkv, 1), (eb, rb, rb * N, rb * N * Hkv))
     q = fattn.View(ptr, fattn.TYPE_F32, (D, NQ, H, 1), (4, H * D * 4, D * 4, NQ * H * D * 4))
-    k = fattn.View(ptr, kt, (D, N, Hkv, 1), (eb, rb, rb * N, rb * N * Hkv))
     m = fattn.View(ptr, fattn.TYPE_F16, (N, NQ, 1, 1), (2, N * 2, N * 2 * NQ, N * 2 * NQ)) if mask else None
-    return fattn.ext_params(q, k, k, m, ptr, 0.088, kv_chunk=kv_chunk)
+    return fattn.ext_params(q, view(kt), view(kt if vt is None else vt), m, ptr, 0.088, kv_chunk=kv_chunk)
 
 
 def test_workspace_size_config3():
@@ -89,6 +90,22 @@ def test_split_merge_option_restores_fused_merge():
     finally:
         fattn.set_option(fattn.OPT_SPLIT_MERGE, 0)
     assert "merge_kernel" not in d2, d2   # split kernel, 32 rows per kv head: fused merge
+
+
+@pytest.mark.parametrize("kt,vt", [(fattn.TYPE_Q8_0, fattn.TYPE_F16), (fattn.TYPE_F16, fattn.TYPE_Q4_0),
+                                   (fattn.TYPE_Q4_0, fattn.TYPE_Q8_0)])
+@pytest.mark.parametrize("D,NQ", [(128, 1), (64, 64), (256, 4096)])
+def test_mixed_kv_types_take_the_split_kernel(kt, vt, D, NQ):
+    """Separate K and V cache types: the split kernel instantiated for the pair
+    (never the single-type batched-decode, multi-query or prefill kernels)."""
+    d = fattn.describe(_params(D=D, NQ=NQ, H=8, Hkv=8, N=2048, kt=kt, vt=vt))
+    names = {fattn.TYPE_F16: "f16", fattn.TYPE_Q8_0: "q8_0", fattn.TYPE_Q4_0: "q4_0"}
+    assert d.startswith(f"fattn_split_kernel<{names[kt]},{names[vt]},D{D},"), d
+
+
+def test_mixed_kv_types_other_head_dims_rejected():
+    p = _params(D=96, kt=fattn.TYPE_Q8_0, vt=fattn.TYPE_F16)
+    assert fattn.workspace_size(p) == 0
 
 
 def test_single_chunk_needs_no_workspace():

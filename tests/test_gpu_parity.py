@@ -220,6 +220,38 @@ def test_mq_fully_masked_rows_are_nan(dev, mq_on):
     assert attn_rel_err(got, ref) <= RTOL
 
 
+# ------------------------------------------------------------------ mixed K / V cache types
+# llama.cpp takes separate K and V cache types (-ctk / -ctv); the split kernel
+# is instantiated for every pair of F16 / Q8_0 / Q4_0 at D = 64, 128, 256.
+
+MIXED_PAIRS = [("q8_0", "f16"), ("q4_0", "f16"), ("f16", "q8_0"), ("f16", "q4_0"), ("q8_0", "q4_0"), ("q4_0", "q8_0")]
+
+
+@pytest.mark.parametrize("kt,vt", MIXED_PAIRS, ids=lambda x: x)
+@pytest.mark.parametrize("D", [64, 128, 256])
+def test_mixed_kv_types_decode(dev, kt, vt, D):
+    p = make_problem(D=D, NQ=1, H=8, N=1024, kv_type=kt, v_type=vt, seed=60 + D)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert d.startswith(f"fattn_split_kernel<{kt},{vt},D{D},"), d
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
+@pytest.mark.parametrize("kt,vt", MIXED_PAIRS[:3], ids=lambda x: x)
+@pytest.mark.parametrize("case", [
+    dict(NQ=16, H=32, Hkv=8, N=2048, mask="causal"),         # GQA multi-row tiles, merge launch
+    dict(NQ=3, H=8, Hkv=2, N=800, layout="pos", mask="tail"),  # llama.cpp [N][Hkv] cache, dword path, tails
+    dict(NQ=64, H=4, Hkv=4, N=4096),                         # config 5's shard shape
+], ids=["gqa_causal", "pos_tail", "cfg5_shard"])
+def test_mixed_kv_types_multirow(dev, kt, vt, case):
+    p = make_problem(D=128, kv_type=kt, v_type=vt, seed=61, **case)
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 # ------------------------------------------------------------------ batched-decode kernel (fattn_bd.h)
 # 64 packed rows per workgroup, 128-key tiles over 8 waves, chunk partials
 # merged by a second launch.  The planner takes it from 64 packed rows per kv

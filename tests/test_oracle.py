@@ -252,10 +252,10 @@ def _fp64_attention(p):
     stride / GQA / mask plumbing."""
     from problems import encode_rows
     D, NQ, H, N = p.D, p.NQ, p.H, p.N
-    dec = lambda a: (orc.f16_bits_to_f32(orc.f32_to_f16_bits(a)) if p.kv_type == orc.TYPE_F16 else
-                     orc.dequantize(encode_rows(a, p.kv_type), p.kv_type, D))
-    k = dec(p.k_f32).astype(np.float64)
-    v = dec(p.v_f32).astype(np.float64)
+    dec = lambda a, t: (orc.f16_bits_to_f32(orc.f32_to_f16_bits(a)) if t == orc.TYPE_F16 else
+                        orc.dequantize(encode_rows(a, t), t, D))
+    k = dec(p.k_f32, p.kv_type).astype(np.float64)
+    v = dec(p.v_f32, p.v_type).astype(np.float64)
     mask = orc.f16_bits_to_f32(p.mask_bits)[:, :N].astype(np.float64) if p.mask_bits is not None else 0
     out = np.zeros((p.S, NQ, H, D))
     r = H // p.Hkv
@@ -274,6 +274,14 @@ def test_oracle_ext_vs_fp64(kt, layout):
     p = make_problem(D=64, NQ=3, H=4, Hkv=2, N=96, kv_type=kt, layout=layout, mask="causal", seed=6)
     got = p.oracle(n_threads=2)
     assert attn_rel_err(got, _fp64_attention(p)) < 2e-3
+
+
+@pytest.mark.parametrize("kt,vt", [("q8_0", "f16"), ("f16", "q4_0"), ("q4_0", "q8_0")])
+def test_oracle_mixed_kv_types_vs_fp64(kt, vt):
+    """Separate K and V cache types (llama.cpp -ctk / -ctv): each tensor is read
+    by its own type."""
+    p = make_problem(D=64, NQ=3, H=4, Hkv=2, N=96, kv_type=kt, v_type=vt, layout="pos", mask="causal", seed=8)
+    assert attn_rel_err(p.oracle(n_threads=2), _fp64_attention(p)) < 2e-3
 
 
 def test_oracle_layouts_identical():
