@@ -697,8 +697,10 @@ int fattn_ext_f16_launch(const void* q, const void* k, const void* v, const void
                          int nb31, int nb01, int nb02, int nb03, int nb11, int nb12, int nb13, int ne0, int ne1,
                          int ne2, int ne3, int k_type, int v_type, void* workspace, size_t workspace_bytes,
                          void* stream) {
-    // flash-llama.h:120-125: V shares K's shape and strides.
+    // flash-llama.h:120-125: V shares K's shape and strides -- so one row size:
+    // mixed K / V types need the struct form (fattn_ext) with V's own strides
     (void)ne0; (void)ne1; (void)ne2; (void)ne3;
+    if (k_type != v_type) return FATTN_ERR_INVALID_ARG;
     fattn_params p;
     std::memset(&p, 0, sizeof(p));
     p.q = {q, FATTN_TYPE_F32, 0, {ne00, ne01, ne02, ne03}, {4, nb01, nb02, nb03}};

@@ -188,3 +188,13 @@ def test_cpy_rejects_bad_views():
               fattn.View(16, fattn.TYPE_Q8_0, (100, 8, 1, 1), (34, 136, 1088, 1088))) == -1  # not whole blocks
     assert rc(f32, fattn.View(16, fattn.TYPE_Q8_0, (128, 8, 1, 1), (18, 136, 1088, 1088))) == -4  # wrong nb0
     assert rc(fattn.View(18, fattn.TYPE_F32, (128, 8, 1, 1), (4, 512, 4096, 4096)), q8) == -7      # misaligned
+
+
+def test_positional_launch_rejects_mixed_types():
+    """fattn_ext_f16_launch shares K's row strides with V (src/flash-llama.h:123-125),
+    so a mixed K / V type pair cannot be described there: rejected before any launch."""
+    D, H, N, ptr = 128, 8, 256, 1 << 20
+    rc = fattn.lib().fattn_ext_f16_launch(
+        ptr, ptr, ptr, None, ptr, 0.088, D, 1, H, 1, D, N, H, 1, 1, N * 2, D * 4 * H, D * 4, D * H * 4,
+        136, 136 * N, 136 * N * H, D, H, 1, 1, fattn.TYPE_Q8_0, fattn.TYPE_F16, None, 0, None)
+    assert rc == -1
