@@ -440,7 +440,15 @@ int make_plan(const fattn_params* p, Plan& pl) {
     const bool mq_ok = !g_opt_mq_disable && !mixed && is_quant(k.type) && g16 && (D == 64 || D == 128) && NQ * a.rk2 >= 32 &&
                        a.rk2 <= 64 &&
                        (a.rk2 & (a.rk2 - 1)) == 0;
-    pl.mq = mq_ok && NQ * a.rk2 >= g_opt_mq_min_rows;
+    // Both 64-row-tile kernels (multi-query, batched decode) need every KV
+    // chunk to hold at least two 128-key tiles: a workgroup with one tile is all
+    // prologue and epilogue (config-5 shard, 4 heads x 64 rows: split kernel
+    // 9.4 + 4.3 us merge, multi-query 11.0 + 4.3, batched decode 10.9 + 4.4)
+    const int64_t qpt64 = mq_ok ? 64 / a.rk2 : 1;  // query rows per 64-row tile (rk2 <= 64)
+    const int64_t y64 = Hkv * ((NQ + qpt64 - 1) / qpt64);
+    const bool wide = N * y64 * S >= (int64_t)2 * kBdKeys * pl.cus;
+    pl.mq = mq_ok && NQ * a.rk2 >= g_opt_mq_min_rows &&
+            (wide || NQ * a.rk2 >= 256 || g_opt_mq_min_rows != kMqMinRowsDefault);  // (an explicit threshold wins)
     if (pl.mq) {
         // 256 rows per workgroup once that still gives one workgroup per CU
         const int64_t wg256 = Hkv * S * ((NQ * a.rk2 + 255) / 256);
@@ -472,9 +480,10 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // batched decode (config 5: 64 query rows per kv head): 64-row workgroups
     // over 128-key tiles, the KV split over workgroups to fill the chip, the
     // chunk partials merged in a second launch
+    // (from 64 rows, when the chunks hold two tiles or more: `wide` above)
     pl.bd = false;
     if (!pl.pf && g_opt_bd != 1 && mq_ok && D == 128 && N % kStep == 0 &&
-        (g_opt_bd == 2 || NQ * a.rk2 >= kBdRows)) {
+        (g_opt_bd == 2 || (NQ * a.rk2 >= kBdRows && wide))) {
         pl.bd = true;
         pl.mq = false;
         a.R = a.rk2;

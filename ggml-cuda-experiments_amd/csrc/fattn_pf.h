@@ -255,8 +255,9 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     }
     // live tiles whose mask block is +-0 everywhere (flag 2: the prefill of a
     // zero or causal mask, away from the diagonal): their mask DMA goes through
-    // an offset past the descriptor -- no traffic, zeros land in the slot, so
-    // the instruction count (vmcnt budget) and the arithmetic are unchanged.
+    // an offset past the descriptor -- no traffic, zeros land in the slot, the
+    // instruction count (vmcnt budget) is unchanged -- and the tile neither
+    // waits for nor reads the slot (zeros in registers instead).
     // Bit s of zb[s / 64]: tile t0 + s (the first 256 live tiles).
     uint64_t zb[4] = {0, 0, 0, 0};
     if (a.pf_flags) {
@@ -438,16 +439,28 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         // on): read it, refill the slot, and skip the tile when the whole 32 x 64
         // block is -inf (causal prefill: a fully masked block adds nothing to m,
         // l or O, so skipping it is exact -- the rows' state is left untouched)
+        // (a tile whose whole 256 x 64 mask block is +-0, flag 2, neither waits
+        // for nor reads its empty slot: its mask values are zeros in registers;
+        // the next DMA into the slot lands after the empty one, in issue order)
         u32x2 mk[2][4];
         bool live = true;
         if constexpr (HM) {
-            pf_vm_wait<KT, D>(wave, s + C::ahead < ntiles ? 1 : 0, 0);
+            const bool zero = s < 256 && ((zb[s >> 6] >> (s & 63)) & 1);  // workgroup-uniform
+            if (!zero) {
+                pf_vm_wait<KT, D>(wave, s + C::ahead < ntiles ? 1 : 0, 0);
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
+                for (int t = 0; t < 2; t++) {
 #pragma unroll
-                for (int uu = 0; uu < 4; uu++) mk[t][uu] = *(const u32x2*)(smem + maddr[t][uu]);
+                    for (int uu = 0; uu < 4; uu++) mk[t][uu] = *(const u32x2*)(smem + maddr[t][uu]);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            } else {
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+#pragma unroll
+                    for (int uu = 0; uu < 4; uu++) mk[t][uu] = u32x2{0u, 0u};
+                }
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (s + 1 < ntiles) mask_issue(s + 1);
             uint32_t open = 0;  // any key not at -inf (f16 0xFC00)
 #pragma unroll

@@ -69,10 +69,11 @@ def test_workspace_size_config3():
     (dict(N=2048, kt=fattn.TYPE_F16), ["f16,f16", "8waves>", "grid(8,32,1)"]),              # config 2
     (dict(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0), ["4waves> + fattn_merge_kernel", "grid(32,8,1)"]),  # config 4
     (dict(NQ=64), ["fattn_bd_kernel", "+ fattn_bd_merge_kernel", "grid(8,32,1)"]),         # config 5, one GPU
-    (dict(NQ=64, H=4, Hkv=4), ["fattn_bd_kernel", "+ fattn_bd_merge_kernel", "grid(32,4,1)"]),  # config 5, 8-rank shard
+    (dict(NQ=64, H=4, Hkv=4), ["fattn_split_kernel", "+ fattn_merge_kernel"]),             # config 5, 8-rank shard
+    (dict(NQ=64, H=16, Hkv=16), ["fattn_bd_kernel", "grid(16,16,1)"]),                     # config 5, 2-rank shard
     (dict(NQ=256), ["fattn_bd_kernel", "grid(2,128,1)"]),                                   # batched: 4 row tiles
     (dict(NQ=8, H=32, Hkv=8), ["fattn_split_kernel", "+ fattn_merge_kernel"]),              # < 64 rows per kv head
-], ids=["config3", "config2", "config4", "config5", "config5_shard", "mq_nq256", "split_nq8_gqa"])
+], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "split_nq8_gqa"])
 def test_planner_picks(kw, want):
     """The plans the round-2 measurements chose, at 256 CUs:
     one-row tiles take 8 waves with the fused row merge; multi-row tiles with
