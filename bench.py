@@ -293,6 +293,7 @@ def parse_args(argv=None):
     ap.add_argument("--pf-stagger", type=int, default=2)
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--no-mq", action="store_true", help="never pick the multi-query kernel (split-KV kernel only)")
+    ap.add_argument("--bd", type=int, default=0, help="batched-decode kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--split-prio", type=int, default=0,
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
     ap.add_argument("--waves", type=int, default=0, help="split kernel waves per workgroup (4, 8, 16; 0 = planner)")
@@ -320,7 +321,7 @@ def parse_args(argv=None):
 def apply_options(args):
     import fattn
     opts = [(args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT), (args.pf, fattn.OPT_PF),
-            (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO),
+            (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO), (args.bd, fattn.OPT_BD),
             (args.waves, fattn.OPT_SPLIT_WAVES)]
     fattn.set_option(fattn.OPT_SPLIT_SKIP, 1 if args.no_step_skip else 0)
     fattn.set_option(fattn.OPT_SPLIT_MERGE, 1 if args.fused_merge else 0)

@@ -3,10 +3,13 @@
 
   pmc_summary.py --kernel fattn_split_kernel a.csv [b.csv ...]
       per counter: dispatches, mean / min / max value per dispatch
-  --traffic OUT.json --workload W --alg-bytes B
+  --traffic OUT.json --bench-line BENCH.log
       HBM bytes per launch from FETCH_SIZE and WRITE_SIZE, corrected as
       MI355X_MICROARCH.md prescribes (FETCH_SIZE is KiB and reports 1/2 of
-      16-B/lane streaming reads on gfx950: x 1024 x 2; WRITE_SIZE x 1024)
+      16-B/lane streaming reads on gfx950: x 1024 x 2; WRITE_SIZE x 1024),
+      tagged with the workload, the plan (describe string) and the kernel
+      source hash of the bench.py JSON line of the same command (bench.py
+      reads a traffic file back only when all three match)
   --mfma
       MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMDs x CUs x cycles),
       cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums it over the 8 XCDs)
@@ -38,6 +41,7 @@ def main():
     ap.add_argument("--traffic")
     ap.add_argument("--workload", default="")
     ap.add_argument("--alg-bytes", type=float, default=0.0)
+    ap.add_argument("--bench-line", default="", help="log holding the bench.py JSON line of the profiled command")
     ap.add_argument("--command", default="")
     ap.add_argument("--mfma", action="store_true")
     ap.add_argument("--cus", type=int, default=256)
@@ -59,12 +63,22 @@ def main():
             print(f"MFMA busy / (4 x {a.cus} x GRBM_GUI_ACTIVE/8) = {util:.4f}  (kernel cycles {cyc:.0f})")
         if "SQ_INSTS_MFMA" in summ and "SQ_INSTS_VALU" in summ:
             print(f"VALU per MFMA instruction = {summ['SQ_INSTS_VALU']['mean'] / summ['SQ_INSTS_MFMA']['mean']:.3f}")
+    plan, shash = "", ""
+    if a.bench_line:
+        for ln in open(a.bench_line):
+            if ln.startswith('{"metric"'):
+                bl = json.loads(ln)
+                a.workload = a.workload or bl["config"]["workload"]
+                a.alg_bytes = a.alg_bytes or float(bl["config"]["bytes_per_step"])
+                plan, shash = bl["roofline"]["kernel"], bl["source_hash"]
     if a.traffic:
         fetch, write = summ["FETCH_SIZE"], summ["WRITE_SIZE"]
         fb = fetch["mean"] * 1024 * 2
         wb = write["mean"] * 1024
         out = {
             "workload": a.workload,
+            "plan": plan,
+            "source_hash": shash,
             "kernel": names[0] if len(names) == 1 else names,
             "command": a.command,
             "counters": {"FETCH_SIZE": {"dispatches": fetch["dispatches"], "mean_kb": fetch["mean"],
