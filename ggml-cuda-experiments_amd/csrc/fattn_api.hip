@@ -467,7 +467,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     pl.pf = false;
     const bool heads_ok = NQ * a.rk2 >= 32 && a.rk2 <= 64 && (a.rk2 & (a.rk2 - 1)) == 0;
     const bool pf_f16 = !g_opt_mq_disable && !mixed && k.type == FATTN_TYPE_F16 && !v_trans && g16 && heads_ok;
-    if ((mq_ok || pf_f16) && g_opt_pf != 1 && D == 128 && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
+    if ((mq_ok || pf_f16) && g_opt_pf != 1 && (D == 64 || D == 128) && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
         p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= pl.cus)) {
         pl.pf = true;
         pl.mq = false;
@@ -501,9 +501,13 @@ int make_plan(const fattn_params* p, Plan& pl) {
         a.n_chunks = 1;
         a.ncp = 1;
         pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
-        pl.lds = pl.kt == FATTN_TYPE_F16    ? PfCfg<FATTN_TYPE_F16, 128>::ldsBytes
-                 : pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
-                                            : PfCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
+        auto pf_lds = [&](auto d) {
+            constexpr int DD = decltype(d)::value;
+            return pl.kt == FATTN_TYPE_F16    ? PfCfg<FATTN_TYPE_F16, DD>::ldsBytes
+                   : pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, DD>::ldsBytes
+                                              : PfCfg<FATTN_TYPE_Q4_0, DD>::ldsBytes;
+        };
+        pl.lds = D == 64 ? pf_lds(std::integral_constant<int, 64>()) : pf_lds(std::integral_constant<int, 128>());
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
         // share the front of the workspace with the split-KV arrival words; a

@@ -163,9 +163,9 @@ int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
     return pl.a.has_mask ? launch_mq_hm<KT, D, 4, true>(pl, st, ev) : launch_mq_hm<KT, D, 4, false>(pl, st, ev);
 }
 
-template <int KT, bool HM>
+template <int KT, int D, bool HM>
 int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    auto kern = fattn_pf_kernel<KT, 128, HM>;
+    auto kern = fattn_pf_kernel<KT, D, HM>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         if (HM && pl.a.pf_flags)
             hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,
@@ -195,9 +195,9 @@ int launch_bd(const Plan& pl, hipStream_t st, const Events& ev) {
     return pl.a.has_mask ? launch_bd_hm<KT, true>(pl, st, ev) : launch_bd_hm<KT, false>(pl, st, ev);
 }
 
-template <int KT>
+template <int KT, int D>
 int launch_pf(const Plan& pl, hipStream_t st, const Events& ev) {
-    return pl.a.has_mask ? launch_pf_hm<KT, true>(pl, st, ev) : launch_pf_hm<KT, false>(pl, st, ev);
+    return pl.a.has_mask ? launch_pf_hm<KT, D, true>(pl, st, ev) : launch_pf_hm<KT, D, false>(pl, st, ev);
 }
 
 // split kernel over mixed K / V cache types (instantiated once per D in
@@ -224,13 +224,15 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
     if constexpr (D == 64 || D == 128 || D == 256) {
         if (pl.kt != pl.vt && pl.vt != VT_F16T) return launch_mixed<D>(pl, st, ev);
     }
-    if constexpr (D == 128) {
+    if constexpr (D == 64 || D == 128) {
         if (pl.pf) {
-            if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_pf<FATTN_TYPE_F16>(pl, st, ev);
-            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0>(pl, st, ev);
-            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_pf<FATTN_TYPE_F16, D>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0, D>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0, D>(pl, st, ev);
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
+    }
+    if constexpr (D == 128) {
         if (pl.bd) {
             if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_bd<FATTN_TYPE_Q8_0>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_bd<FATTN_TYPE_Q4_0>(pl, st, ev);

@@ -51,7 +51,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <int KT, int D>
 struct PfCfg {
-    static_assert(D == 128, "one half ggml block per wave and row");
+    static_assert(D == 64 || D == 128, "at most one half ggml block per wave and row");
     static constexpr int NT = kPfWaves * kWave;
     // f16 K/V: LDS-DMA straight into the images (no raw tiles, no dequantisation);
     // three image pairs: tile s in use, s+1 and s+2 in flight
@@ -91,20 +91,27 @@ __device__ __forceinline__ void pf_issue(const StepSrc& rs, int n0, uint32_t lds
 }
 
 // f16 K/V: this lane's source offsets (tile-relative; + n0 * nb1 per tile) of
-// its wave's DMA instructions j = wave + 8i, i = 0..3 (j < 16: K image bytes
-// [1024j, +1024); else V image bytes [1024(j-16), +1024)), laid out as the
-// image swizzles above.  Rows are addressed by nb1 (any 16-B aligned stride).
+// its wave's DMA instructions j = wave + 8i, i < NIW (j < NJ: K image bytes
+// [1024j, +1024); else V image bytes [1024(j-NJ), +1024); NJ = the image's
+// 1-KiB pieces), laid out as the image swizzles above.  Rows are addressed by nb1
+// (any 16-B aligned stride).
+template <int D>
+struct PfDirect {
+    static constexpr int NJ = kPfKeys * D * 2 / 1024;  // 1-KiB pieces per image
+    static constexpr int NIW = 2 * NJ / kPfWaves;      // DMA instructions per wave and tile
+    static_assert(kPfWaves == 8 && NIW * kPfWaves == 2 * NJ && NJ % kPfWaves == 0, "");
+};
 template <int D>
 __device__ __forceinline__ void pf_direct_offsets(const SplitArgs& a, int wave, int lane, uint32_t (&off)[4]) {
-    static_assert(kPfWaves == 8 && D == 128, "");
+    constexpr int NJ = PfDirect<D>::NJ;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < PfDirect<D>::NIW; i++) {
         const int j = wave + 8 * i;
-        if (i < 2) {  // K: slice kk = j / 2, rows 32 (j & 1) + lane / 2, stored half lane & 1
+        if (i < PfDirect<D>::NIW / 2) {  // K: slice kk = j / 2, rows 32 (j & 1) + lane / 2, stored half lane & 1
             const int kk = j >> 1, r = 32 * (j & 1) + (lane >> 1), hh = lane & 1;
             off[i] = (uint32_t)r * (uint32_t)a.k_nb1 + kk * 32 + ((hh ^ ((r >> 3) & 1)) * 16);
-        } else {      // V: dim block db = jj / 4, rows 16 (jj & 3) + lane / 4, stored chunk lane & 3
-            const int jj = j - 16, db = jj >> 2, r = 16 * (jj & 3) + (lane >> 2), pc = lane & 3;
+        } else {  // V: dim block db = jj / 4, rows 16 (jj & 3) + lane / 4, stored chunk lane & 3
+            const int jj = j - NJ, db = jj >> 2, r = 16 * (jj & 3) + (lane >> 2), pc = lane & 3;
             off[i] = (uint32_t)r * (uint32_t)a.v_nb1 + db * 64 + ((pc ^ ((r >> 2) & 3)) * 16);
         }
     }
@@ -117,13 +124,14 @@ __device__ __forceinline__ void pf_direct_issue(const SplitArgs& a, const StepSr
     return;  // diagnostic build only
 #endif
     const uint32_t nk = (uint32_t)n0 * (uint32_t)a.k_nb1, nv = (uint32_t)n0 * (uint32_t)a.v_nb1;
+    constexpr int NJ = PfDirect<D>::NJ;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < PfDirect<D>::NIW; i++) {
         const int j = wave + 8 * i;
-        if (i < 2)
+        if (i < PfDirect<D>::NIW / 2)
             dma<16>(rs.k, pair_lds + j * 1024, nk + off[i]);
         else
-            dma<16>(rs.v, pair_lds + PfCfg<FATTN_TYPE_F16, D>::img + (j - 16) * 1024, nv + off[i]);
+            dma<16>(rs.v, pair_lds + PfCfg<FATTN_TYPE_F16, D>::img + (j - NJ) * 1024, nv + off[i]);
     }
 }
 
@@ -159,6 +167,7 @@ __device__ __forceinline__ void pf_vm_wait(int wave, int nraw, int nmask) {
 
 // raw tile -> f16 images: wave w dequantises half h = w & 1 of block b = w >> 1
 // of row `lane`, for K (into dim slice 2b + h) and V (dim block b, chunks 2h, 2h+1)
+// (D = 64: two blocks, waves 0-3; waves 4-7 -- the prioritised half -- skip it)
 template <int KT, int D>
 __device__ __forceinline__ void pf_dequant(const uint8_t* rb, uint8_t* k16, uint8_t* v16, int wave, int lane) {
 #ifdef FATTN_MQ_NODEQ
@@ -166,6 +175,7 @@ __device__ __forceinline__ void pf_dequant(const uint8_t* rb, uint8_t* k16, uint
 #endif
     using C = PfCfg<KT, D>;
     const int b = wave >> 1, h = wave & 1;
+    if (b >= D / QK) return;  // wave-uniform
     u32x4 ck[2], cv[2];
     dequant_half<KT, D>(rb, lane, b, h, ck);
     dequant_half<KT, D>(rb + C::kvRaw, lane, b, h, cv);

@@ -420,6 +420,28 @@ def test_pf_sweep(dev, pf_force, case):
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
+PF64_CASES = [
+    dict(kv_type="q8_0", NQ=256, H=4, Hkv=4, N=512, mask="causal"),
+    dict(kv_type="q4_0", NQ=300, H=2, Hkv=2, N=256, mask="random"),           # two query tiles, ragged
+    dict(kv_type="q8_0", NQ=64, H=16, Hkv=4, N=192, mask="zero"),             # R = 4, odd tile count
+    dict(kv_type="f16", NQ=256, H=4, Hkv=4, N=256, mask="neginf_blocks"),
+    dict(kv_type="f16", NQ=100, H=8, Hkv=2, N=128, mask="none", layout="pos", S=2),
+]
+
+
+@pytest.mark.parametrize("case", PF64_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_pf_d64(dev, pf_force, case):
+    """The prefill kernel at D = 64: four K dim slices / two V dim blocks per
+    image, waves 0-3 dequantise (one half block each)."""
+    p = make_problem(D=64, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert "fattn_pf_kernel" in d and "D64" in d, d
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 @pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
 def test_pf_rescale(dev, pf_force, kt):
     """Large scores and scores rising along the sequence: deferred-max rescales."""
