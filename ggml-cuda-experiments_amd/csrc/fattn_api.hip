@@ -242,7 +242,12 @@ int mq_lds_bytes_r(int kt, int D) {
         return D == 128 ? MQCfg<FATTN_TYPE_Q8_0, 128, NW, RPW>::ldsBytes : MQCfg<FATTN_TYPE_Q8_0, 64, NW, RPW>::ldsBytes;
     return D == 128 ? MQCfg<FATTN_TYPE_Q4_0, 128, NW, RPW>::ldsBytes : MQCfg<FATTN_TYPE_Q4_0, 64, NW, RPW>::ldsBytes;
 }
-int mq_lds_bytes(int kt, int D, int nw) { return nw == 8 ? mq_lds_bytes_r<8, 32>(kt, D) : mq_lds_bytes_r<4, 16>(kt, D); }
+int mq_lds_bytes(int kt, int D, int nw) {
+    if (D == 256)  // 64-row workgroups only (256 rows' mask tiles do not fit beside the D = 256 images)
+        return kt == FATTN_TYPE_Q8_0 ? MQCfg<FATTN_TYPE_Q8_0, 256, 4, 16>::ldsBytes
+                                     : MQCfg<FATTN_TYPE_Q4_0, 256, 4, 16>::ldsBytes;
+    return nw == 8 ? mq_lds_bytes_r<8, 32>(kt, D) : mq_lds_bytes_r<4, 16>(kt, D);
+}
 
 // Multi-query sizing: 64 or 256 packed rows per workgroup, KV split only when the
 // (kv head x query tile x seq) workgroups cannot fill the chip (two per CU at
@@ -437,7 +442,8 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // are packed (R = rk2, a power of two <= 64).
     // (below 256 packed rows per kv head the split kernel measures faster:
     // config 5, 64 rows, 15.5 vs 37.6 us at 4 heads; FATTN_OPT_MQ_MIN_ROWS)
-    const bool mq_ok = !g_opt_mq_disable && !mixed && is_quant(k.type) && g16 && (D == 64 || D == 128) && NQ * a.rk2 >= 32 &&
+    const bool mq_ok = !g_opt_mq_disable && !mixed && is_quant(k.type) && g16 && (D == 64 || D == 128 || D == 256) &&
+                       NQ * a.rk2 >= 32 &&
                        a.rk2 <= 64 &&
                        (a.rk2 & (a.rk2 - 1)) == 0;
     // Both 64-row-tile kernels (multi-query, batched decode) need every KV
@@ -453,6 +459,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
         // 256 rows per workgroup once that still gives one workgroup per CU
         const int64_t wg256 = Hkv * S * ((NQ * a.rk2 + 255) / 256);
         pl.nw = g_opt_mq_rpw ? (g_opt_mq_rpw == 32 ? 8 : 4) : wg256 >= pl.cus ? 8 : 4;
+        if (D == 256) pl.nw = 4;  // (mq_lds_bytes)
     }
     if (pl.mq) {
         a.R = a.rk2;

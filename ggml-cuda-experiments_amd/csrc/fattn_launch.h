@@ -158,8 +158,10 @@ int launch_mq_hm(const Plan& pl, hipStream_t st, const Events& ev) {
 
 template <int KT, int D>
 int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
-    if (pl.nw == 8)
-        return pl.a.has_mask ? launch_mq_hm<KT, D, 8, true>(pl, st, ev) : launch_mq_hm<KT, D, 8, false>(pl, st, ev);
+    if constexpr (D != 256) {  // D = 256: 64-row workgroups only (LDS)
+        if (pl.nw == 8)
+            return pl.a.has_mask ? launch_mq_hm<KT, D, 8, true>(pl, st, ev) : launch_mq_hm<KT, D, 8, false>(pl, st, ev);
+    }
     return pl.a.has_mask ? launch_mq_hm<KT, D, 4, true>(pl, st, ev) : launch_mq_hm<KT, D, 4, false>(pl, st, ev);
 }
 
@@ -239,7 +241,7 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
     }
-    if constexpr (D == 64 || D == 128) {
+    if constexpr (D == 64 || D == 128 || D == 256) {
         if (pl.mq) {
             if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_mq<FATTN_TYPE_Q8_0, D>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_mq<FATTN_TYPE_Q4_0, D>(pl, st, ev);

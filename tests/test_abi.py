@@ -74,7 +74,8 @@ def test_workspace_size_config3():
     (dict(NQ=256), ["fattn_bd_kernel", "grid(2,128,1)"]),                                   # batched: 4 row tiles
     (dict(NQ=8, H=32, Hkv=8), ["fattn_split_kernel", "+ fattn_merge_kernel"]),              # < 64 rows per kv head
     (dict(D=64, NQ=4096, H=32, Hkv=32), ["fattn_pf_kernel<q8_0,D64"]),                       # D = 64 prefill
-], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "split_nq8_gqa", "pf_d64"])
+    (dict(D=256, NQ=4096, H=16, Hkv=16), ["fattn_mq_kernel<q8_0,D256,4waves"]),              # D = 256 prefill
+], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "split_nq8_gqa", "pf_d64", "mq_d256"])
 def test_planner_picks(kw, want):
     """The plans the round-2 measurements chose, at 256 CUs:
     one-row tiles take 8 waves with the fused row merge; multi-row tiles with

@@ -142,6 +142,27 @@ def test_mq_sweep(dev, mq_on, case):
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
+MQ256_CASES = [
+    dict(kv_type="q8_0", NQ=256, H=4, Hkv=4, N=256, mask="causal"),       # prefill-shaped, no split
+    dict(kv_type="q4_0", NQ=64, H=8, Hkv=2, N=1024, mask="random"),       # R = 4, KV split + merge launch
+    dict(kv_type="q8_0", NQ=50, H=2, Hkv=2, N=320, mask="neginf_blocks", S=2),  # ragged tile, 2 seqs
+    dict(kv_type="q8_0", NQ=300, H=2, Hkv=2, N=128, mask="none"),
+]
+
+
+@pytest.mark.parametrize("case", MQ256_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_mq_d256(dev, mq_on, case):
+    """The multi-query kernel at D = 256 (64-row workgroups: a 256-row tile's
+    mask rows do not fit beside the D = 256 images)."""
+    p = make_problem(D=256, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert "fattn_mq_kernel" in d and "D256,4waves" in d, d
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 @pytest.fixture
 def rpw64():
     """Force the 256-row workgroups (8 waves x 32 rows) on small problems."""
