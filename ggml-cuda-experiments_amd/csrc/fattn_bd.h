@@ -164,6 +164,94 @@ __device__ __forceinline__ void bd_dequant(const uint8_t* raw, uint8_t* k16, uin
     }
 }
 
+// ---- epilogue of the batched-decode kernels (all memory traffic of the tile
+// loop drained): merge the four key quarters of each row.  Every wave parks
+// its rows' (O, m, l) in LDS (accumulator layout -> [kq][row][D + 4]); then
+// each of the 512 threads merges 16 dims of one row (fixed order, kq = 0..3)
+// and stores them as 64 contiguous bytes, so every store instruction writes
+// whole rows (row-per-lane stores from the accumulator layout issue 32 lines
+// per instruction: MI355X_MICROARCH.md, epilogue store tail)
+template <int KT, int D>
+__device__ __forceinline__ void bd_finish(const SplitArgs& a, uint8_t* smem, const f32x16 (&o)[D / 32], float m_run,
+                                          f32x2 l2, int kq, int p, int h, int tid, int lane, int wave, int qt, int ik2,
+                                          int iq3, int y, int chunk) {
+    using C = BdCfg<KT, D>;
+    constexpr int NDB = D / 32;
+    constexpr float kNegInf = -__builtin_inff();
+    (void)lane; (void)wave;  // (stamps)
+    const float l_own = xor32_pair(l2.x + l2.y, false);
+    __syncthreads();  // every wave is done with the tiles' LDS
+    {
+        float* pk = (float*)smem + (kq * kBdRows + p) * C::parkStride + 4 * h;
+#pragma unroll
+        for (int db = 0; db < NDB; db++) {
+#pragma unroll
+            for (int uu = 0; uu < 4; uu++)
+                *(f32x4*)(pk + 32 * db + 8 * uu) = f32x4{o[db][4 * uu], o[db][4 * uu + 1], o[db][4 * uu + 2],
+                                                         o[db][4 * uu + 3]};
+        }
+        if (h == 0) ((f32x2*)(smem + C::parkMl))[kq * kBdRows + p] = f32x2{m_run, l_own};
+    }
+    __syncthreads();
+    FATTN_STAMP(12);
+    constexpr int kDpt = kBdRows * D / (kBdWaves * kWave);  // dims per thread: 16
+    const int pr = tid / (D / kDpt), c0 = (tid % (D / kDpt)) * kDpt;
+    const f32x2* pml = (const f32x2*)(smem + C::parkMl);
+    f32x2 mlk[4];
+    float M = kNegInf;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        mlk[k] = pml[k * kBdRows + pr];
+        M = fmaxf(M, mlk[k].x);
+    }
+    float L = 0.0f;
+    float acc[kDpt];
+#pragma unroll
+    for (int e = 0; e < kDpt; e++) acc[e] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float wk = (mlk[k].x == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mlk[k].x - M);
+        L += wk * mlk[k].y;
+        const float* src = (const float*)smem + (k * kBdRows + pr) * C::parkStride + c0;
+#pragma unroll
+        for (int e = 0; e < kDpt; e += 4) {
+            const f32x4 x = *(const f32x4*)(src + e);
+            acc[e] += wk * x.x;
+            acc[e + 1] += wk * x.y;
+            acc[e + 2] += wk * x.z;
+            acc[e + 3] += wk * x.w;
+        }
+    }
+    const int rq = div_R(a, pr);
+    const int q1 = qt * a.QPT + rq;
+    if (q1 >= a.NQ) return;
+    if (a.n_chunks == 1) {
+        const int q2 = ik2 * a.rk2 + (pr - rq * a.R);
+        float* out = a.dst + (((int64_t)iq3 * a.NQ + q1) * a.H + q2) * D + c0;
+        const float inv = 1.0f / L;  // fully masked row -> NaN like the reference
+#pragma unroll
+        for (int e = 0; e < kDpt; e += 4) {
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; r++) v[r] = L == 0.0f ? __builtin_nanf("") : acc[e + r] * inv;
+            *(f32x4*)(out + e) = v;
+        }
+        return;
+    }
+    // several chunks: the partial (O, m, l) of packed row pr for
+    // fattn_bd_merge_kernel, [tile][chunk][64 rows][D] and [..][64 rows][2] (the
+    // kernel boundary orders these stores before the merge's loads)
+    const int64_t slot = (((int64_t)iq3 * gridDim.y + y) * a.n_chunks + chunk) * kBdRows + pr;
+    float* po = a.ws_o + slot * D + c0;
+#pragma unroll
+    for (int e = 0; e < kDpt; e += 4) *(f32x4*)(po + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
+    if (c0 == 0) *(f32x2*)(a.ws_ml + 2 * slot) = f32x2{M, L};
+#ifdef FATTN_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FATTN_STAMP(13);
+#endif
+}
+
 template <int KT, int D, bool HM>
 __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const SplitArgs a) {
     using C = BdCfg<KT, D>;
@@ -441,84 +529,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     }
     FATTN_STAMP(11);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-
-    // ---- merge the four key quarters of each row.  Every wave parks its
-    // rows' (O, m, l) in LDS (accumulator layout -> [kq][row][D + 4]); then each
-    // of the 512 threads merges 16 dims of one row (fixed order, kq = 0..3) and
-    // stores them as 64 contiguous bytes, so every store instruction writes
-    // whole rows (row-per-lane stores from the accumulator layout issue 32
-    // lines per instruction: MI355X_MICROARCH.md, epilogue store tail)
-    const float l_own = xor32_pair(l2.x + l2.y, false);
-    __syncthreads();  // every wave is done with the tiles' LDS
-    {
-        float* pk = (float*)smem + (kq * kBdRows + p) * C::parkStride + 4 * h;
-#pragma unroll
-        for (int db = 0; db < NDB; db++) {
-#pragma unroll
-            for (int uu = 0; uu < 4; uu++)
-                *(f32x4*)(pk + 32 * db + 8 * uu) = f32x4{o[db][4 * uu], o[db][4 * uu + 1], o[db][4 * uu + 2],
-                                                         o[db][4 * uu + 3]};
-        }
-        if (h == 0) ((f32x2*)(smem + C::parkMl))[kq * kBdRows + p] = f32x2{m_run, l_own};
-    }
-    __syncthreads();
-    FATTN_STAMP(12);
-    constexpr int kDpt = kBdRows * D / (kBdWaves * kWave);  // dims per thread: 16
-    const int pr = tid / (D / kDpt), c0 = (tid % (D / kDpt)) * kDpt;
-    const f32x2* pml = (const f32x2*)(smem + C::parkMl);
-    f32x2 mlk[4];
-    float M = kNegInf;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        mlk[k] = pml[k * kBdRows + pr];
-        M = fmaxf(M, mlk[k].x);
-    }
-    float L = 0.0f;
-    float acc[kDpt];
-#pragma unroll
-    for (int e = 0; e < kDpt; e++) acc[e] = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const float wk = (mlk[k].x == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mlk[k].x - M);
-        L += wk * mlk[k].y;
-        const float* src = (const float*)smem + (k * kBdRows + pr) * C::parkStride + c0;
-#pragma unroll
-        for (int e = 0; e < kDpt; e += 4) {
-            const f32x4 x = *(const f32x4*)(src + e);
-            acc[e] += wk * x.x;
-            acc[e + 1] += wk * x.y;
-            acc[e + 2] += wk * x.z;
-            acc[e + 3] += wk * x.w;
-        }
-    }
-    const int rq = div_R(a, pr);
-    const int q1 = qt * a.QPT + rq;
-    if (q1 >= a.NQ) return;
-    if (a.n_chunks == 1) {
-        const int q2 = ik2 * a.rk2 + (pr - rq * a.R);
-        float* out = a.dst + (((int64_t)iq3 * a.NQ + q1) * a.H + q2) * D + c0;
-        const float inv = 1.0f / L;  // fully masked row -> NaN like the reference
-#pragma unroll
-        for (int e = 0; e < kDpt; e += 4) {
-            f32x4 v;
-#pragma unroll
-            for (int r = 0; r < 4; r++) v[r] = L == 0.0f ? __builtin_nanf("") : acc[e + r] * inv;
-            *(f32x4*)(out + e) = v;
-        }
-        return;
-    }
-    // several chunks: the partial (O, m, l) of packed row pr for
-    // fattn_bd_merge_kernel, [tile][chunk][64 rows][D] and [..][64 rows][2] (the
-    // kernel boundary orders these stores before the merge's loads)
-    const int64_t slot = (((int64_t)iq3 * gridDim.y + y) * a.n_chunks + chunk) * kBdRows + pr;
-    float* po = a.ws_o + slot * D + c0;
-#pragma unroll
-    for (int e = 0; e < kDpt; e += 4) *(f32x4*)(po + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
-    if (c0 == 0) *(f32x2*)(a.ws_ml + 2 * slot) = f32x2{M, L};
-#ifdef FATTN_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FATTN_STAMP(13);
-#endif
+    bd_finish<KT, D>(a, smem, o, m_run, l2, kq, p, h, tid, lane, wave, qt, ik2, iq3, y, chunk);
 }
 
 // Second launch of a split batched-decode plan: one wave per (tile, packed
