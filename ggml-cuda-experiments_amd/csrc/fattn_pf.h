@@ -136,32 +136,23 @@ __device__ __forceinline__ void pf_direct_issue(const SplitArgs& a, const StepSr
 }
 
 // counted wait: at most nraw (0..2) raw-tile DMA groups and nmask (0/1) mask
-// groups of this wave still in flight (vmcnt counts in issue order)
-template <int KT, int D, int W>
-__device__ __forceinline__ void pf_vm_wait_w(int nraw, int nmask) {
-    constexpr int NI = PfCfg<KT, D>::ni_wave(W);
-    constexpr int NM = PfCfg<KT, D>::NIM;
-    const int k = nraw * 4 + nmask;
-    switch (k) {
-        case 0: wait_vmcnt_c<0>(); break;
-        case 1: wait_vmcnt_c<NM>(); break;
-        case 4: wait_vmcnt_c<NI>(); break;
-        case 5: wait_vmcnt_c<NI + NM>(); break;
-        case 8: wait_vmcnt_c<2 * NI>(); break;
-        default: wait_vmcnt_c<2 * NI + NM>(); break;
-    }
-}
+// groups of this wave still in flight (vmcnt counts in issue order).  Counted
+// with the SMALLEST per-wave group (ni_wave of the last wave): a wave that
+// issues one more instruction per tile waits for that one too -- it belongs to
+// the youngest group, issued a tile earlier -- and no wave needs a switch over
+// its id (the branch trees cost ~300 SALU per wave and tile)
 template <int KT, int D>
-__device__ __forceinline__ void pf_vm_wait(int wave, int nraw, int nmask) {
-    switch (wave) {
-        case 0: pf_vm_wait_w<KT, D, 0>(nraw, nmask); break;
-        case 1: pf_vm_wait_w<KT, D, 1>(nraw, nmask); break;
-        case 2: pf_vm_wait_w<KT, D, 2>(nraw, nmask); break;
-        case 3: pf_vm_wait_w<KT, D, 3>(nraw, nmask); break;
-        case 4: pf_vm_wait_w<KT, D, 4>(nraw, nmask); break;
-        case 5: pf_vm_wait_w<KT, D, 5>(nraw, nmask); break;
-        case 6: pf_vm_wait_w<KT, D, 6>(nraw, nmask); break;
-        default: pf_vm_wait_w<KT, D, 7>(nraw, nmask); break;
+__device__ __forceinline__ void pf_vm_wait(int nraw, int nmask) {
+    constexpr int NI = PfCfg<KT, D>::ni_wave(kPfWaves - 1);
+    constexpr int NM = PfCfg<KT, D>::NIM;
+    if (nmask) {
+        if (nraw >= 2) wait_vmcnt_c<2 * NI + NM>();
+        else if (nraw == 1) wait_vmcnt_c<NI + NM>();
+        else wait_vmcnt_c<NM>();
+    } else {
+        if (nraw >= 2) wait_vmcnt_c<2 * NI>();
+        else if (nraw == 1) wait_vmcnt_c<NI>();
+        else wait_vmcnt_c<0>();
     }
 }
 
@@ -371,7 +362,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         for (int s = 0; s < 3 && s < ntiles; s++) pf_issue<KT, D>(rs, (t0 + s) * kPfKeys, raw_lds(s), wave, lane);
         if (ntiles > 0) mask_issue(0);
         // raw 0 landed (raw 1, 2 and mask 0 may fly on)
-        pf_vm_wait<KT, D>(wave, min(2, ntiles - 1), ntiles > 0 ? NM : 0);
+        pf_vm_wait<KT, D>(min(2, ntiles - 1), ntiles > 0 ? NM : 0);
         __syncthreads();
         if (ntiles > 0) pf_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, wave, lane);
     }
@@ -406,7 +397,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         // quantised: raw s+1 landed (raw s+2 and mask s may fly on);
         // f16: image pair of tile s landed (tile s+1 and mask s may fly on)
         PF_T(7);
-        pf_vm_wait<KT, D>(wave, s + C::ahead - 1 < ntiles ? 1 : 0, NM);
+        pf_vm_wait<KT, D>(s + C::ahead - 1 < ntiles ? 1 : 0, NM);
         __syncthreads();
         PF_T(0);
         if constexpr (C::kDirect) {
@@ -437,7 +428,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         }
 #ifdef FATTN_MQ_NOCOMPUTE
         if constexpr (HM) {
-            pf_vm_wait<KT, D>(wave, s + C::ahead < ntiles ? 1 : 0, 0);
+            pf_vm_wait<KT, D>(s + C::ahead < ntiles ? 1 : 0, 0);
             if (s + 1 < ntiles) mask_issue(s + 1);
         }
         if (late) dequant_next();
@@ -457,7 +448,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         if constexpr (HM) {
             const bool zero = s < 256 && ((zb[s >> 6] >> (s & 63)) & 1);  // workgroup-uniform
             if (!zero) {
-                pf_vm_wait<KT, D>(wave, s + C::ahead < ntiles ? 1 : 0, 0);
+                pf_vm_wait<KT, D>(s + C::ahead < ntiles ? 1 : 0, 0);
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
 #pragma unroll
