@@ -111,8 +111,9 @@ def test_config5_full_batch64(dev):
 
 @pytest.fixture
 def mq_on():
-    """The multi-query kernel from 32 packed rows per kv head (the planner's
-    default threshold is 256; below it the split kernel is faster)."""
+    """The multi-query kernel from 32 packed rows per kv head (the planner
+    takes it from 64 rows when every KV chunk holds two 128-key tiles, or
+    from 256 rows; an explicit threshold overrides both)."""
     fattn.set_option(fattn.OPT_MQ_MIN_ROWS, 32)
     fattn.set_option(fattn.OPT_BD, 1)  # (64+ rows at D = 128 would take the batched-decode kernel)
     yield
