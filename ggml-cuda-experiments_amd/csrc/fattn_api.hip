@@ -570,7 +570,7 @@ int fattn_set_option(int option, int value) {
             g_opt_pf = value;
             return FATTN_OK;
         case FATTN_OPT_PF_STAGGER:
-            if (value < 0 || value > 7) return FATTN_ERR_INVALID_ARG;
+            if (value < 0 || value > 7 || (value & 1)) return FATTN_ERR_INVALID_ARG;  // (bit 0: removed)
             g_opt_pf_stagger = value;
             return FATTN_OK;
         case FATTN_OPT_MQ_MIN_ROWS:

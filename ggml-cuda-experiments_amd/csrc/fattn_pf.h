@@ -404,16 +404,11 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             // into the pair every wave finished reading before the barrier
             if (s + 2 < ntiles)
                 pf_direct_issue<D>(a, rs, (t0 + s + 2) * kPfKeys, lds0 + ((P + 2) % 3) * C::pairBytes, wave, doff);
-        } else {
-            if (s + 3 < ntiles) pf_issue<KT, D>(rs, (t0 + s + 3) * kPfKeys, raw_lds(s + 3), wave, lane);
         }
         PF_T(1);
-        // SIMD partners (waves w and w + 4) run the tile's phases staggered:
-        // waves 0-3 dequantise first (VALU) while waves 4-7 run S^T (MFMA),
-        // then each one's softmax (VALU) meets the other's MFMA phase, and
-        // waves 4-7 dequantise last while waves 0-3 run O^T
-        // (MI355X_MICROARCH.md, two waves per SIMD)
-        const bool late = (a.pf_stagger & 1) && wave >= kPfWaves / 2;
+        // (the round-1 phase stagger -- waves 4-7 dequantising after their
+        // compute, FATTN_OPT_PF_STAGGER bit 0 -- measured neutral and was
+        // removed: it kept the dequantisation's state live across the compute)
         auto dequant_next = [&] {
             if constexpr (!C::kDirect) {
                 if (s + 1 < ntiles)
@@ -421,17 +416,25 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
                                       smem + (P ^ 1) * C::pairBytes + C::img, wave, lane);
             }
         };
-        if (!late) {
-            dequant_next();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            PF_T(2);
-        }
+        dequant_next();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PF_T(2);
+        // quantised: raw tile s + 3 is issued during this tile's first S^T chain
+        // (an issue that stalls on a full memory queue then waits beside the
+        // MFMAs, not in front of them), so it comes after mask s + 1; at the
+        // mask wait only raw s + 2 is younger than mask s (tile 0: nothing)
+        const int mask_younger = C::kDirect ? (s + C::ahead < ntiles ? 1 : 0) : s == 0 ? 0 : (s + 2 < ntiles ? 1 : 0);
+        auto issue_raw = [&] {
+            if constexpr (!C::kDirect) {
+                if (s + 3 < ntiles) pf_issue<KT, D>(rs, (t0 + s + 3) * kPfKeys, raw_lds(s + 3), wave, lane);
+            }
+        };
 #ifdef FATTN_MQ_NOCOMPUTE
         if constexpr (HM) {
-            pf_vm_wait<KT, D>(s + C::ahead < ntiles ? 1 : 0, 0);
+            pf_vm_wait<KT, D>(mask_younger, 0);
             if (s + 1 < ntiles) mask_issue(s + 1);
         }
-        if (late) dequant_next();
+        issue_raw();
         return;  // diagnostic build only: copies, dequant and barriers
 #endif
         const uint8_t* img = smem + P * C::pairBytes;  // K image; vbase includes + img
@@ -448,7 +451,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         if constexpr (HM) {
             const bool zero = s < 256 && ((zb[s >> 6] >> (s & 63)) & 1);  // workgroup-uniform
             if (!zero) {
-                pf_vm_wait<KT, D>(s + C::ahead < ntiles ? 1 : 0, 0);
+                pf_vm_wait<KT, D>(mask_younger, 0);
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
 #pragma unroll
@@ -471,33 +474,13 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             }
             live = __builtin_amdgcn_ballot_w64(open != 0) != 0;
         }
-        if (live) {
-        // -- one tile, phases overlapped within the wave (cdna_hip_programming.md
-        // T19): the two subtiles' S^T chains back to back, the scores of subtile 0
-        // (u = fma(s, scale, mask)) computed under subtile 1's MFMAs, subtile 0's
-        // exponentials under nothing but their own latency, then subtile 1's
-        // exponentials under subtile 0's P.V MFMAs.  Same arithmetic as before
-        // (one max over the tile's 64 keys, one deferred-rescale decision).
-        // K operands of both subtiles first (16 ds_read_b128): one LDS wait
+        // (state of the tile's first half, shared by the two live blocks below)
         f16x8 ka[2][NK];
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-#pragma unroll
-            for (int kk = 0; kk < NK; kk++) ka[t][kk] = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024);
-        }
-        __builtin_amdgcn_sched_barrier(0);
         f32x16 st0, st1;
-#pragma unroll
-        for (int j = 0; j < 16; j++) st0[j] = 0.0f;
-#pragma unroll
-        for (int kk = 0; kk < NK; kk++) st0 = mfma32(ka[0][kk], qop[kk], st0);
-#pragma unroll
-        for (int j = 0; j < 16; j++) st1[j] = 0.0f;
-#pragma unroll
-        for (int kk = 0; kk < NK; kk++) st1 = mfma32(ka[1][kk], qop[kk], st1);
+        float u0[16], u1[16];
+        float tmax0 = kNegInf;
         // scores (natural units) u = scale * s + mask; element j of subtile t is
-        // key 32t + 8(j/4) + 4h + (j%4) of this lane's row.  Subtile 0's depend
-        // only on st0: the scheduler places them between st1's MFMAs.
+        // key 32t + 8(j/4) + 4h + (j%4) of this lane's row
         auto scores = [&](const f32x16& stt, int t, float (&ut)[16]) {
             if constexpr (HM) {
 #pragma unroll
@@ -513,20 +496,46 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
                 for (int j = 0; j < 16; j++) ut[j] = stt[j];
             }
         };
-        float u0[16], u1[16];
+        if (live) {
+        // -- one tile, phases overlapped within the wave (cdna_hip_programming.md
+        // T19): the two subtiles' S^T chains back to back, the scores of subtile 0
+        // (u = fma(s, scale, mask)) computed under subtile 1's MFMAs, subtile 0's
+        // exponentials under nothing but their own latency, then subtile 1's
+        // exponentials under subtile 0's P.V MFMAs.  Same arithmetic as before
+        // (one max over the tile's 64 keys, one deferred-rescale decision).
+        // K operands of subtile 0 (8 ds_read_b128, one LDS wait); subtile 1's
+        // are read behind st0's chain (their latency under its MFMAs)
+#pragma unroll
+        for (int kk = 0; kk < NK; kk++) ka[0][kk] = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 16; j++) st0[j] = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < NK; kk++) st0 = mfma32(ka[0][kk], qop[kk], st0);
+#pragma unroll
+        for (int kk = 0; kk < NK; kk++) ka[1][kk] = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + 1024);
+#pragma unroll
+        for (int j = 0; j < 16; j++) st1[j] = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < NK; kk++) st1 = mfma32(ka[1][kk], qop[kk], st1);
+        // scores (natural units) u = scale * s + mask; element j of subtile t is
+        // key 32t + 8(j/4) + 4h + (j%4) of this lane's row.  Subtile 0's depend
+        // only on st0: the scheduler places them between st1's MFMAs.
         scores(st0, 0, u0);
-        float tmax0 = kNegInf;
 #pragma unroll
         for (int j = 0; j < 16; j++) tmax0 = fmaxf(tmax0, u0[j]);
-        // st0's chain alone, then one MFMA of st1's chain, then up to 4 of
-        // subtile 0's VALU
-        __builtin_amdgcn_sched_group_barrier(0x008, NK, 0);
+        // one MFMA of st1's chain, then up to 4 of subtile 0's VALU
 #pragma unroll
         for (int i = 0; i < NK; i++) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
+        }  // live, first half
+        // quantised: raw tile s + 3, issued while the S^T chains execute (a
+        // skipped tile issues it here too)
+        issue_raw();
+        if (live) {
         scores(st1, 1, u1);
         float tmax = tmax0;
 #pragma unroll
@@ -605,11 +614,6 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         }
         }  // live
         PF_T(5);
-        if (late) {
-            dequant_next();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            PF_T(2);
-        }
     };
     if constexpr (C::kDirect) {
         for (int s = 0; s < ntiles; s += 3) {

@@ -143,9 +143,9 @@ enum {
     FATTN_OPT_SPLIT_INFLIGHT = 4,   /* split kernel: steps in flight per wave (0 = auto, 1..4; LDS permitting) */
     FATTN_OPT_PF = 5,               /* prefill kernel: 0 = auto, 1 = never, 2 = whenever eligible (even if the
                                        workgroups do not fill the chip) */
-    FATTN_OPT_PF_STAGGER = 6,       /* prefill kernel, bit 0: SIMD partner waves staggered (default lockstep);
-                                       bit 1 (default on): waves 4-7 at s_setprio 1; bit 2: XCD-grouped
-                                       workgroup order (the query tiles of a kv head on one XCD) */
+    FATTN_OPT_PF_STAGGER = 6,       /* prefill kernel, bit 1 (default on): waves 4-7 at s_setprio 1; bit 2:
+                                       XCD-grouped workgroup order (the query tiles of a kv head on one XCD);
+                                       bit 0 (a phase stagger of SIMD partners) was removed and is rejected */
     FATTN_OPT_SPLIT_WAVE_MERGE = 10 /* split kernel, one-row tiles with <= 32 wave partials: 0 = every wave
                                        publishes and the last-arriving wave merges (default), 1 = the
                                        workgroup-level merge used for all other tiles */,

@@ -95,6 +95,17 @@ def test_split_merge_option_restores_fused_merge():
     assert "merge_kernel" not in d2, d2   # split kernel, 32 rows per kv head: fused merge
 
 
+def test_pf_stagger_option_range():
+    """FATTN_OPT_PF_STAGGER: bits 1-2 settable, the removed bit 0 and values
+    past 7 rejected (include/fattn.h)."""
+    for v in (0, 2, 4, 6):
+        fattn.set_option(fattn.OPT_PF_STAGGER, v)
+    fattn.set_option(fattn.OPT_PF_STAGGER, 2)
+    for v in (1, 3, 8, -1):
+        with pytest.raises(Exception):
+            fattn.set_option(fattn.OPT_PF_STAGGER, v)
+
+
 @pytest.mark.parametrize("kt,vt", [(fattn.TYPE_Q8_0, fattn.TYPE_F16), (fattn.TYPE_F16, fattn.TYPE_Q4_0),
                                    (fattn.TYPE_Q4_0, fattn.TYPE_Q8_0)])
 @pytest.mark.parametrize("D,NQ", [(128, 1), (64, 64), (256, 4096)])
