@@ -9,17 +9,21 @@ split-KV chunk merge is fused) over the whole problem.  Each step reads a
 different one of R independent KV caches (R * 35.7 MB > the 256 MiB Infinity
 Cache), so the number is HBM, not cache.
 
-N GPUs (`--gpus N`, or launched by torch.distributed.run): BASELINE.json
-configs[4] -- n_q = 64 query rows, 32 heads, N = 4096, Q8_0 -- head-sharded
-(SURVEY.md §8e): rank r owns kv heads [r*Hkv/N, (r+1)*Hkv/N) and their q heads
-(fattn.shard.shard_heads / head_views, zero-copy slices of the same global
-problem on every rank), runs the unchanged single-GPU kernel on its slice, and
-after the K timed steps the ranks' outputs meet in ONE RCCL all_gather over
-xGMI (inside the timed region) plus the permute into the ggml dst layout.
-Total work is fixed as N grows: "scaling": "strong".  The line also carries
-the per-step gather cost and kernel+gather per step, measured separately
-(kernel-only and kernel+gather reported apart).  `--gpus N` with
-no launcher starts N child ranks itself (before touching the GPU).
+N GPUs (`--gpus N`, or launched by torch.distributed.run): heads x batch
+sharding.  The value line is WEAK scaling: every rank decodes
+its own sequence of an N-sequence batch -- the config-3 problem above, its own
+KV caches, the unchanged single-GPU kernel, no collective on the data path --
+and after the K timed steps the ranks' outputs meet in ONE RCCL all_gather
+over xGMI (inside the timed region); value = N x the per-sequence bytes / the
+slowest rank's wall time, so value(N) / (N value(1)) is the scaling
+efficiency.  Beside it (`head_shard_config5`, strong scaling): BASELINE.json
+configs[4] -- n_q = 64 query rows, 32 heads, N = 4096, Q8_0 -- as one problem
+head-sharded over the ranks (rank r owns kv heads [r*Hkv/N, (r+1)*Hkv/N) and
+their q heads, zero-copy slices, fattn.shard), gathered and permuted into the
+ggml dst layout (`--multi head` makes that the value line).  Both report the
+per-step gather and kernel + gather per step apart from the kernel
+(BASELINE.md).  `--gpus N` with no launcher starts N child ranks itself
+(before touching the GPU).
 
 Prints ONE JSON line (rank 0).  `value` = whole-job algorithmic bytes / wall
 time (GB/s); `roofline` prices the dominant kernel from HIP events on its
@@ -276,7 +280,12 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="auto", choices=["auto", "config3", "config5"],
-                    help="auto: config3 on one GPU, config5 (head-sharded) on several")
+                    help="auto: config3 (on every rank with --multi batch), config5 with --multi head")
+    ap.add_argument("--multi", default="batch", choices=["batch", "head"],
+                    help="N > 1: batch = every rank decodes its own sequence (weak scaling, the value line); "
+                         "head = one problem head-sharded over the ranks (strong scaling)")
+    ap.add_argument("--no-head-shard", action="store_true",
+                    help="N > 1, --multi batch: skip the config-5 head-shard (strong-scaling) measurement")
     ap.add_argument("--rotate", type=int, default=0,
                     help="independent KV caches cycled through (0 = enough that one pass reads >= 512 MiB per rank)")
     ap.add_argument("--kv-type", default=None, choices=["q8_0", "q4_0", "f16"])
@@ -298,6 +307,8 @@ def parse_args(argv=None):
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
     ap.add_argument("--waves", type=int, default=0, help="split kernel waves per workgroup (4, 8, 16; 0 = planner)")
     ap.add_argument("--no-step-skip", action="store_true", help="split kernel: load and compute every step")
+    ap.add_argument("--handoff", type=int, default=0,
+                    help="split kernel, one-row workgroup partials: 0 data-tagged granules, 1 drain + counter")
     ap.add_argument("--fused-merge", action="store_true",
                     help="split kernel, multi-row tiles: last-arriving workgroup merges (no second launch)")
     ap.add_argument("--mask-live", type=float, default=1.0,
@@ -325,6 +336,7 @@ def apply_options(args):
             (args.waves, fattn.OPT_SPLIT_WAVES)]
     fattn.set_option(fattn.OPT_SPLIT_SKIP, 1 if args.no_step_skip else 0)
     fattn.set_option(fattn.OPT_SPLIT_MERGE, 1 if args.fused_merge else 0)
+    fattn.set_option(fattn.OPT_SPLIT_HANDOFF, args.handoff)
     for val, opt in opts:
         if val:
             fattn.set_option(opt, val)
@@ -349,15 +361,28 @@ def shape_of(args, workload):
 REHEARSE = os.environ.get("FATTN_BENCH_REHEARSE") == "1"
 
 
-def _gather(x):
+def _gather(x, mode="head"):
+    """head: the ranks' head slices -> the full [.., H, D] output (gather_heads);
+    batch: the ranks' own sequences stacked on a leading [world] axis."""
+    import torch
+    import torch.distributed as dist
     from fattn.shard import gather_heads
-    return gather_heads(x.cpu()).to(x.device) if REHEARSE else gather_heads(x)
+    y = x.cpu() if REHEARSE else x
+    if mode == "head":
+        out = gather_heads(y)
+    else:
+        world = dist.get_world_size()
+        out = torch.empty((world,) + tuple(y.shape), dtype=y.dtype, device=y.device)
+        dist.all_gather_into_tensor(out.view(world * y.shape[0], *y.shape[1:]), y.contiguous())
+    return out.to(x.device) if REHEARSE else out
 
 
-def run_decode(args, dev, shape, rank=0, world=1, tag=""):
-    """Time K steps of the decode workload `shape` (one FLASH_ATTN_EXT per step),
-    head-sharded over `world` ranks.  Returns the measurement dict (rank 0 holds
-    the max over ranks)."""
+def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
+    """Time K steps of the decode workload `shape` (one FLASH_ATTN_EXT per step)
+    over `world` ranks: mode "head" shards its heads (strong scaling, every rank
+    a slice of one global problem), mode "batch" gives every rank a whole
+    problem of its own -- its own sequence of the batch (weak scaling).
+    Returns the measurement dict (rank 0 holds the max over ranks)."""
     import torch
     import torch.distributed as dist
     import fattn
@@ -367,13 +392,15 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
     Hkv = shape["kv_heads"] or H
     typ = fattn.TYPE_NAMES[shape["kv_type"]]
     rb = fattn.row_size(typ, D)
-    sh = shard_heads(H, Hkv, world, rank)
+    sh = shard_heads(H, Hkv, world if mode == "head" else 1, rank if mode == "head" else 0)
     # rotation sized by bytes: the caches one rank reads over a
     # pass of the rotation exceed the 256 MiB Infinity Cache twice over, so a
     # step never finds its KV on-die from the previous pass
     R = args.rotate or max(16, -(-ROTATE_BYTES // (2 * sh.n_kv * N * rb)))
     g = torch.Generator(device=dev)
-    g.manual_seed(1234)  # the same global problem on every rank; each reads only its slice
+    # head: the same global problem on every rank, each reads only its slice;
+    # batch: every rank its own sequence
+    g.manual_seed(1234 + (rank if mode == "batch" else 0))
 
     # --- synthetic inputs, resident in HBM before timing
     kv_sets = []
@@ -455,7 +482,7 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
         graph.replay()   # untimed warm replay
     torch.cuda.synchronize()
     if world > 1:
-        _gather(outs)  # warm the communicator
+        _gather(outs, mode)  # warm the communicator
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = evs[0], evs[1]
@@ -466,7 +493,7 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
     hip.hipEventRecord(ev1, gs.cuda_stream)
     if world > 1:
         with torch.cuda.stream(gs):
-            full = _gather(outs)   # the single RCCL gather over xGMI + permute to [R][1][NQ][H][D]
+            full = _gather(outs, mode)  # the single RCCL gather over xGMI (head: + permute to [R][1][NQ][H][D])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -477,15 +504,21 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
     kern_ms_avg = f.value / K
 
     res = {"kernel": kname, "kernel_ms_avg": kern_ms_avg, "kernel_ms_median": kern_ms_median, "elapsed": elapsed}
-    if args.dump_out and rank == 0:
+    if args.dump_out and (rank == 0 or mode == "batch"):
         # rotation 0's inputs and the (gathered) output, for the multi-rank
-        # parity test (tests/test_rehearsal.py checks them against the oracle)
-        out0 = (full[0] if world > 1 else outs[0]).cpu().numpy()
-        np.savez(args.dump_out, q=q.cpu().numpy(), k=kv_sets[0][0].cpu().numpy(), v=kv_sets[0][1].cpu().numpy(),
+        # parity test (tests/test_rehearsal.py checks them against the oracle);
+        # batch mode: every rank its own inputs (<dump>.rank<r>.npz), rank 0
+        # the gathered outputs of all ranks
+        if mode == "head":
+            out0 = (full[0] if world > 1 else outs[0]).cpu().numpy()
+        else:
+            out0 = (full[:, 0] if world > 1 else outs[0][None]).cpu().numpy()
+        path = args.dump_out if rank == 0 else args.dump_out + f".rank{rank}.npz"
+        np.savez(path, q=q.cpu().numpy(), k=kv_sets[0][0].cpu().numpy(), v=kv_sets[0][1].cpu().numpy(),
                  mask=masks[0].cpu().view(torch.int16).numpy().view(np.uint16), out=out0,
-                 shape=np.array([D, NQ, H, Hkv, N, typ, world]), kernel=np.array(kname))
+                 shape=np.array([D, NQ, H, Hkv, N, typ, world]), kernel=np.array(kname), mode=np.array(mode))
     if world > 1:
-        assert tuple(full.shape) == (R, 1, NQ, H, D)
+        assert tuple(full.shape) == ((R, 1, NQ, H, D) if mode == "head" else (world, R, 1, NQ, H, D))
         # 3) per-step cost of the gather, and kernel + gather per step (eager),
         #    reported apart from the kernel (BASELINE.md multi-GPU rule)
         one = outs[0]
@@ -494,7 +527,7 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
             dist.barrier()
             torch.cuda.synchronize()
             t = time.perf_counter()
-            _gather(one)
+            _gather(one, mode)
             torch.cuda.synchronize()
             gts.append(time.perf_counter() - t)
         for i in range(25):
@@ -502,7 +535,7 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
             torch.cuda.synchronize()
             t = time.perf_counter()
             step(i, stream)
-            _gather(outs[i % R])
+            _gather(outs[i % R], mode)
             torch.cuda.synchronize()
             ets.append(time.perf_counter() - t)
         res["gather_ms_median"] = statistics.median(gts[5:]) * 1e3
@@ -521,8 +554,11 @@ def run_decode(args, dev, shape, rank=0, world=1, tag=""):
     mask_b = 0 if args.no_mask else NQ * N * 2
     job_bytes = (NQ * H * D * 4) * 2 + 2 * Hkv * N * rb + mask_b
     rank_bytes = (NQ * Hl * D * 4) * 2 + 2 * sh.n_kv * N * rb + mask_b
-    res.update(job_bytes=job_bytes, rank_bytes=rank_bytes, flops=4 * NQ * N * D * H, rank_flops=4 * NQ * N * D * Hl,
-               workload=f"decode_{shape['kv_type']}_h{H}_hkv{Hkv}_d{D}_n{N}_q{NQ}", shard=sh, R=R)
+    flops = 4 * NQ * N * D * H
+    if mode == "batch":  # the job: `world` sequences, one per rank
+        job_bytes, flops = world * job_bytes, world * flops
+    res.update(job_bytes=job_bytes, rank_bytes=rank_bytes, flops=flops, rank_flops=4 * NQ * N * D * Hl,
+               workload=f"decode_{shape['kv_type']}_h{H}_hkv{Hkv}_d{D}_n{N}_q{NQ}", shard=sh, R=R, mode=mode)
     return res
 
 
@@ -580,9 +616,15 @@ def main():
             dist.init_process_group("gloo", init_method="env://")
         else:
             dist.init_process_group("nccl", init_method="env://", device_id=dev)
-    workload = args.workload if args.workload != "auto" else ("config3" if world == 1 else "config5")
+    mode = args.multi if world > 1 else "head"
+    workload = args.workload if args.workload != "auto" else ("config5" if mode == "head" and world > 1 else "config3")
     shape = shape_of(args, workload)
-    res = run_decode(args, dev, shape, rank, world)
+    res = run_decode(args, dev, shape, rank, world, mode)
+    hs5 = None
+    if world > 1 and mode == "batch" and not args.no_head_shard:
+        # BASELINE config 5 head-sharded over the same ranks (strong scaling), beside the line
+        hs5 = run_decode(args, dev, shape_of(argparse.Namespace(**{k: None for k in WORKLOADS["config5"]}),
+                                             "config5"), rank, world, "head")
 
     if rank == 0:
         traffic = committed_traffic(res["workload"], res["kernel"]) if world == 1 else None
@@ -599,15 +641,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(res["elapsed"] / K * 1e3, 5),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if mode == "batch" else "strong",
             "vs_baseline": None,
             "dtype": "f16",
             "data": "synthetic (uniform [-1,1) Q/K/V, K/V quantised on device to ggml blocks; random f16 mask)",
             "config": {"workload": res["workload"], "heads": shape["heads"], "kv_heads": shape["kv_heads"],
                        "head_dim": shape["head_dim"], "kv_len": shape["kv_len"], "n_q": shape["n_q"],
                        "kv_type": shape["kv_type"], "kv_layout": args.layout, "kv_rotation": res["R"],
-                       "parallelism": (f"head_shard_{sh.n_heads}heads_per_rank_x{world}" if world > 1
-                                       else "single_gpu"),
+                       "parallelism": ("single_gpu" if world == 1 else
+                                       f"batch_shard_1seq_per_rank_x{world}" if mode == "batch" else
+                                       f"head_shard_{sh.n_heads}heads_per_rank_x{world}"),
                        "bytes_per_step": res["job_bytes"], "flops_per_step": res["flops"]},
             "tflops": round(res["flops"] * K / res["elapsed"] / 1e12, 4),
             "kernel_ms_avg": round(res["kernel_ms_avg"], 5),
@@ -620,10 +663,23 @@ def main():
         if world > 1:
             if REHEARSE:
                 line["rehearsal"] = "FATTN_BENCH_REHEARSE: all ranks on one GPU, gloo, not a measurement"
-            line["per_rank"] = {"heads": sh.n_heads, "kv_heads": sh.n_kv, "bytes": res["rank_bytes"]}
+            line["per_rank"] = {"heads": sh.n_heads, "kv_heads": sh.n_kv, "bytes": res["rank_bytes"],
+                                "sequences": 1 if mode == "batch" else f"1/{world} of the heads"}
             line["gather"] = {"collective": "all_gather_into_tensor (RCCL over xGMI), once after the K steps",
                               "per_step_gather_ms_median": round(res["gather_ms_median"], 4),
                               "per_step_kernel_plus_gather_ms_median": round(res["step_with_gather_ms_median"], 4)}
+            if hs5 is not None:
+                sh5 = hs5["shard"]
+                line["head_shard_config5"] = {
+                    "workload": hs5["workload"], "scaling": "strong",
+                    "parallelism": f"head_shard_{sh5.n_heads}heads_per_rank_x{world}",
+                    "value": round(hs5["job_bytes"] * K / hs5["elapsed"] / 1e9, 2), "unit": "GB/s",
+                    "ms_per_step": round(hs5["elapsed"] / K * 1e3, 5),
+                    "kernel_ms_avg": round(hs5["kernel_ms_avg"], 5), "kernel": hs5["kernel"],
+                    "per_step_gather_ms_median": round(hs5["gather_ms_median"], 4),
+                    "per_step_kernel_plus_gather_ms_median": round(hs5["step_with_gather_ms_median"], 4),
+                    "note": "one config-5 problem (n_q 64) sliced by kv heads over the ranks; strong-scaling "
+                            "efficiency = value / (N * the N=1 line's strong_scaling_ref value)"}
         if world > 1:
             print(json.dumps(line), flush=True)
 

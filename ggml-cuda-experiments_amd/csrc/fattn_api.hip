@@ -59,6 +59,7 @@ std::atomic<int> g_opt_split_waves{0};      // split kernel waves per workgroup 
 std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
+std::atomic<int> g_opt_split_handoff{0};    // one-row workgroup partials: 0 granules, 1 drain + counter (FATTN_OPT_SPLIT_HANDOFF)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
 std::atomic<uint32_t> g_epoch{0};
 
@@ -194,6 +195,7 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     a.step_skip = g_opt_split_no_skip ? 0 : 1;
     a.nbuf = nbuf;
     a.split_prio = g_opt_split_prio;
+    a.handoff = g_opt_split_handoff;
     a.wave_bytes = G.wave_bytes(nbuf);
     a.chunk_len = spw * quantum;
     a.n_chunks = (int)((N + a.chunk_len - 1) / a.chunk_len);
@@ -220,10 +222,11 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     if (a.n_chunks > 1 && a.wave_merge) {
         // [arrival counters][(m, l) per part][row-0 O per part]; parts = waves
         // (wave_merge 1) or workgroups (2)
+        // (wave_merge 2: room for either hand-off, D + 2 8-byte granules per part)
         const size_t parts = (size_t)S * Y * a.n_chunks * (a.wave_merge == 1 ? nwv : 1);
         pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
         pl.ml_bytes = (parts * 2 * sizeof(float) + 255) / 256 * 256;
-        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + parts * pl.D * 4;
+        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + parts * (a.wave_merge == 2 ? (pl.D + 2) * 8 : pl.D * 4);
     } else if (a.n_chunks > 1) {
         // [arrival words, one 256-B line per tile][(m, l) pairs][O partials];
         // no zeroing needed: each launch epoch-stamps its arrival words
@@ -609,6 +612,10 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_bd = value;
             return FATTN_OK;
+        case FATTN_OPT_SPLIT_HANDOFF:
+            if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_handoff = value;
+            return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:
             if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
             g_opt_split_nbuf = value;
@@ -694,7 +701,7 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
         pl.a.ws_cnt = (uint32_t*)w;
         uint32_t e = g_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
         if (e == 0) e = g_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
-        pl.a.arrival_stamp = kArrivalTag | (uint64_t)e << 16;
+        pl.a.arrival_stamp = kArrivalTag | (uint64_t)e << kArrivalEpochShift;
         pl.a.ws_ml = (float*)(w + pl.cnt_bytes);
         pl.a.ws_o = (float*)(w + pl.cnt_bytes + pl.ml_bytes);  // (prefill pre-pass: the f16 rows)
         if (pl.pf && pl.pf_flags) pl.a.pf_flags = w;

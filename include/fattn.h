@@ -102,9 +102,9 @@ typedef struct fattn_params {
                               allocation once (fattn_workspace_init): a launch stamps its
                               arrival words with a fresh epoch by atomic max, which
                               supersedes any word an earlier launch left (re-armed, or
-                              mid-count after an abort) and any word whose top 16 bits are
+                              mid-count after an abort) and any word whose top 8 bits are
                               not all ones -- but an uninitialised word that happens to
-                              read 0xFFFF in its top bits with an epoch field ahead of the
+                              read 0xFF in its top bits with an epoch field ahead of the
                               launch's would outrank the stamp.  No re-zeroing is needed
                               between launches.  Launches that share one workspace must be
                               ordered on one stream */
@@ -114,11 +114,13 @@ typedef struct fattn_params {
 size_t fattn_workspace_size(const fattn_params* p);
 /* Zero a workspace (hipMemsetAsync on `stream`); call once per allocation.  The
  * split-KV chunks of a tile meet through 64-bit arrival words kept at the front
- * of the workspace, [0xFFFF | epoch:32 | count:16]; each launch stamps them with
- * its own epoch (atomic max) before counting, so memory left by an earlier or an
- * aborted launch is superseded -- but not a never-initialised word whose top
- * 16 bits are all ones with an epoch above the current one (e.g. 0xFF fill),
- * which this call clears. */
+ * of the workspace, [0xFF | epoch:32 | generation:8 | count:16]; each launch
+ * stamps them with its own epoch (atomic max) before counting, so memory left by
+ * an earlier or an aborted launch is superseded -- but not a never-initialised
+ * word whose top 8 bits are all ones with an epoch above the current one (e.g.
+ * 0xFF fill), which this call clears.  The last arriver re-arms a word (count 0,
+ * generation + 1); one-row partials handed over as granules carry (epoch,
+ * generation) tags, so a replayed graph never reads a previous replay's. */
 int fattn_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 int fattn_ext(const fattn_params* p, void* stream);
 
@@ -167,7 +169,11 @@ enum {
                                        workgroup merges the whole tile (combine_tile) */
     FATTN_OPT_BD = 22               /* batched-decode kernel (64-row workgroups, D = 128 Q8_0 / Q4_0, contiguous
                                        rows): 0 = auto (from 64 packed rows per kv head, below the prefill
-                                       shapes), 1 = never, 2 = whenever eligible */
+                                       shapes), 1 = never, 2 = whenever eligible */,
+    FATTN_OPT_SPLIT_HANDOFF = 23    /* split kernel, one-row tiles merged per workgroup over several chunks: 0 =
+                                       each workgroup's row goes out as data-tagged granules with no drain and
+                                       the last arriver sweeps them (default), 1 = write-through row, drain,
+                                       then the arrival count */
 };
 int fattn_set_option(int option, int value);
 

@@ -222,9 +222,9 @@ def test_workspace_not_zeroed(dev, case, fill):
         ws = att.workspace
         if fill == "bytes5a":
             ws.fill_(0x5A)
-        else:  # every 256-B counter line: tag | epoch 1 | 5 arrivals already counted
+        else:  # every 256-B counter line: tag | epoch 1 | generation 0 | 5 arrivals already counted
             words = ws[: ws.numel() // 8 * 8].view(torch.int64)
-            words[::32] = (0xFFFF << 48 | 1 << 16 | 5) - (1 << 64)
+            words[::32] = (0xFF << 56 | 1 << 24 | 5) - (1 << 64)
         ref = p.oracle()
         for _ in range(2):
             t["dst"].zero_()
@@ -422,3 +422,80 @@ def test_cpy_into_kv_cache_view(dev, kt, layout, ntok):
             else:
                 w[p0 + t, h] = rows[t, h]
     assert np.array_equal(got, want)
+
+
+# ------------------------------------------------------------------ one-row hand-off forms (granules / drain)
+
+@pytest.mark.parametrize("handoff", [0, 1], ids=["granules", "drain"])
+@pytest.mark.parametrize("case", [
+    dict(D=128, H=32, N=4096, kv_type="q8_0"),                 # config 3 (8 waves, 8 chunks)
+    dict(D=128, H=8, N=8192, kv_type="q4_0", mask="tail"),      # whole chunks -inf
+    dict(D=64, H=16, N=4096, kv_type="q8_0"),
+    dict(D=80, H=16, N=2048, kv_type="f16"),
+    dict(D=96, H=16, N=4096, kv_type="q8_0"),
+    dict(D=256, H=16, N=2048, kv_type="f16"),
+], ids=["cfg3", "q4_tail", "d64", "d80", "d96", "d256"])
+def test_row_handoff_forms(dev, handoff, case):
+    """One-row tiles over several KV chunks (workgroup merge, wave_merge 2):
+    the partial rows reach the last arriver either as data-tagged granules
+    (default) or as write-through rows behind a drain; both against the oracle
+    at every head dim, with forced chunk counts up to 32."""
+    import torch
+    p = make_problem(seed=5 + case["D"], **case)
+    ref = p.oracle()
+    t = upload(p, dev)
+    fattn.set_option(fattn.OPT_SPLIT_HANDOFF, handoff)
+    try:
+        for chunk in (0, 256, 512):
+            att = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=chunk)
+            desc = att.describe()
+            t["dst"].fill_(float("nan"))
+            att()
+            torch.cuda.synchronize()
+            got = t["dst"].cpu().numpy()
+            assert attn_rel_err(got, ref) <= RTOL, desc
+    finally:
+        fattn.set_option(fattn.OPT_SPLIT_HANDOFF, 0)
+
+
+@pytest.mark.parametrize("handoff", [0, 1], ids=["granules", "drain"])
+def test_row_handoff_graph_replays_new_inputs(dev, handoff):
+    """A captured launch replays with the SAME epoch: the granule tags carry
+    the arrival word's generation, which every replay advances, so a replay
+    never merges a previous replay's partials.  K and V change between replays
+    (in place, as a KV cache does); every replay is checked against the oracle
+    of its own inputs, under uneven load from a copy stream."""
+    import torch
+    fattn.set_option(fattn.OPT_SPLIT_HANDOFF, handoff)
+    try:
+        probs = [make_problem(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", seed=400 + i) for i in range(3)]
+        refs = [p.oracle() for p in probs]
+        t = upload(probs[0], dev)
+        att = fattn.Attention(*views(probs[0], t), t["dst"], probs[0].scale)
+        assert int(att.describe().split("grid(")[1].split(",")[0]) > 1, att.describe()
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            att(s.cuda_stream)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            att(s.cuda_stream)
+        noise_src = torch.randn(1 << 25, device=dev)
+        noise_dst = torch.empty_like(noise_src)
+        side = torch.cuda.Stream()
+        for it in range(12):
+            p = probs[it % 3]
+            t["q"].copy_(torch.from_numpy(np.ascontiguousarray(p.q)))
+            t["k"].copy_(torch.from_numpy(p.k_bytes))
+            t["v"].copy_(torch.from_numpy(p.v_bytes))
+            t["mask"].copy_(torch.from_numpy(np.ascontiguousarray(p.mask_bits).view(np.int16)))
+            t["dst"].fill_(float("nan"))
+            torch.cuda.synchronize()
+            with torch.cuda.stream(side):
+                for _ in range(it % 3):
+                    noise_dst.copy_(noise_src)
+            g.replay()
+            torch.cuda.synchronize()
+            assert attn_rel_err(t["dst"].cpu().numpy(), refs[it % 3]) <= RTOL, f"replay {it}"
+    finally:
+        fattn.set_option(fattn.OPT_SPLIT_HANDOFF, 0)

@@ -757,4 +757,4 @@ def test_chunk_merge_handoff_stress(dev, hkv):
     # (plans whose partials merge in a second launch never touch the words)
     words = shared[: hkv * 256].view(torch.int64)[::32]
     assert int((words & 0xFFFF).abs().sum()) == 0
-    assert bool(((((words >> 48) & 0xFFFF) == 0xFFFF) | (words == 0)).all())
+    assert bool(((((words >> 56) & 0xFF) == 0xFF) | (words == 0)).all())

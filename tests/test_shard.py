@@ -138,3 +138,40 @@ def test_slice_problem_oracle_matches_full_heads():
         sh = shard_heads(prob.H, prob.Hkv, 2, r)
         parts.append(_slice_problem(prob, sh).oracle(n_threads=2))
     assert np.array_equal(assemble_heads(np.stack(parts)), ref)
+
+
+def _batch_worker(rank, world, port, q):
+    """bench.py's weak-scaling (--multi batch) gather on the CPU: every rank
+    solves its own sequence (seed 300 + rank) with the oracle and the outputs
+    meet in bench._gather(.., "batch") -- ONE all_gather_into_tensor."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        prob = make_problem(D=64, NQ=1, H=4, N=128, kv_type="q8_0", seed=300 + rank)
+        local = torch.from_numpy(prob.oracle(n_threads=2))[None]  # [R=1][S][NQ][H][D]
+        full = bench._gather(local, "batch")
+        if rank == 0:
+            q.put(full.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_batch_gather_stacks_sequences():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = q.get(timeout=120)
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert got.shape[:2] == (world, 1)
+    for w in range(world):
+        ref = make_problem(D=64, NQ=1, H=4, N=128, kv_type="q8_0", seed=300 + w).oracle(n_threads=2)
+        assert np.array_equal(got[w, 0], ref)
