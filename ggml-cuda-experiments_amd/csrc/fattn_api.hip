@@ -59,7 +59,7 @@ std::atomic<int> g_opt_split_waves{0};      // split kernel waves per workgroup 
 std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
-std::atomic<int> g_opt_split_handoff{0};    // one-row workgroup partials: 0 granules, 1 drain + counter (FATTN_OPT_SPLIT_HANDOFF)
+std::atomic<int> g_opt_merge_launch{0};  // 1: multi-row chunk partials always merge in a second launch (FATTN_OPT_MERGE_LAUNCH)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
 std::atomic<uint32_t> g_epoch{0};
 
@@ -195,7 +195,6 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     a.step_skip = g_opt_split_no_skip ? 0 : 1;
     a.nbuf = nbuf;
     a.split_prio = g_opt_split_prio;
-    a.handoff = g_opt_split_handoff;
     a.wave_bytes = G.wave_bytes(nbuf);
     a.chunk_len = spw * quantum;
     a.n_chunks = (int)((N + a.chunk_len - 1) / a.chunk_len);
@@ -216,17 +215,22 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     // 14.8 us, config 4: 10.0 vs 10.7; with 2 chunks per tile, config 5 on
     // one GPU, the extra launch costs more than it saves: 36.6 vs 35.6).
     // FATTN_OPT_SPLIT_MERGE = 1: always the last-arriving workgroup (combine_tile).
-    a.merge_launch = (a.n_chunks >= 4 && a.wave_merge == 0 && !g_opt_split_fused_merge) ? 1 : 0;
+    // ... or, with the whole grid co-resident, inside the launch: the tile's
+    // workgroups wait for each other and each merges a share of the rows
+    // (tile_arrive_wait; FATTN_OPT_MERGE_LAUNCH = 1 keeps the second launch)
     pl.lds = G.lds_bytes(nbuf, nwv);
+    const int64_t wgs_cu = std::max(1, std::min(4 * wps / nwv, kLdsPerCU / pl.lds));
+    const bool resident = (int64_t)a.n_chunks * Y * S <= (int64_t)pl.cus * wgs_cu;
+    a.merge_launch = (a.n_chunks >= 4 && a.wave_merge == 0 && !g_opt_split_fused_merge)
+                         ? ((resident && !g_opt_merge_launch) ? 2 : 1) : 0;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     if (a.n_chunks > 1 && a.wave_merge) {
         // [arrival counters][(m, l) per part][row-0 O per part]; parts = waves
         // (wave_merge 1) or workgroups (2)
-        // (wave_merge 2: room for either hand-off, D + 2 8-byte granules per part)
         const size_t parts = (size_t)S * Y * a.n_chunks * (a.wave_merge == 1 ? nwv : 1);
         pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
         pl.ml_bytes = (parts * 2 * sizeof(float) + 255) / 256 * 256;
-        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + parts * (a.wave_merge == 2 ? (pl.D + 2) * 8 : pl.D * 4);
+        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + parts * pl.D * 4;
     } else if (a.n_chunks > 1) {
         // [arrival words, one 256-B line per tile][(m, l) pairs][O partials];
         // no zeroing needed: each launch epoch-stamps its arrival words
@@ -322,17 +326,22 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     a.n_chunks = (int)nch;
     a.ncp = 1;
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
-    a.merge_launch = nch > 1 ? 1 : 0;
     a.nbuf = 0;
     a.wave_bytes = 0;
     pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? BdCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
+    // the chunk partials merge inside the launch (bd_tile_merge: the tile's
+    // workgroups wait for each other, so only when the whole grid is
+    // co-resident -- one workgroup per CU by LDS) or in a second launch
+    const int64_t per_cu = std::max<int64_t>(1, kLdsPerCU / pl.lds);
+    const bool resident = nch * Y * S <= (int64_t)pl.cus * per_cu;
+    a.merge_launch = nch == 1 ? 0 : (resident && !g_opt_merge_launch) ? 2 : 1;
     if (nch > 1) {
-        // [(m, l) pairs][O partials]: [S][Y][chunks][64 rows]
+        // [arrival words, in-kernel merge only][(m, l) pairs][O partials]: [S][Y][chunks][64 rows]
         const size_t slots = (size_t)S * Y * nch * kBdRows;
-        pl.cnt_bytes = 0;
+        pl.cnt_bytes = a.merge_launch == 2 ? (size_t)S * Y * kCntStride * sizeof(uint32_t) : 0;
         pl.ml_bytes = (slots * 2 * sizeof(float) + 255) / 256 * 256;
-        pl.ws_bytes = pl.ml_bytes + slots * pl.D * 4;
+        pl.ws_bytes = pl.cnt_bytes + pl.ml_bytes + slots * pl.D * 4;
     } else {
         pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
     }
@@ -612,9 +621,9 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_bd = value;
             return FATTN_OK;
-        case FATTN_OPT_SPLIT_HANDOFF:
+        case FATTN_OPT_MERGE_LAUNCH:
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
-            g_opt_split_handoff = value;
+            g_opt_merge_launch = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:
             if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
@@ -677,13 +686,14 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
                       tn(pl.kt), pl.D, hm);
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "fattn_bd_kernel<%s,D%d,%s>%s", tn(pl.kt), pl.D, hm,
-                      pl.a.merge_launch ? " + fattn_bd_merge_kernel" : "");
+                      pl.a.merge_launch == 1 ? " + fattn_bd_merge_kernel" : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     else if (pl.mq)
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,
                       pl.a.merge_launch ? " + fattn_mq_merge_kernel" : "");
     else
         std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>%s", tn(pl.kt), tn(pl.vt),
-                      pl.D, pl.gran, hm, pl.nwv, pl.a.merge_launch ? " + fattn_merge_kernel" : "");
+                      pl.D, pl.gran, hm, pl.nwv,
+                      pl.a.merge_launch == 1 ? " + fattn_merge_kernel" : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     const int n = std::snprintf(out, cap, "%s grid(%u,%u,%u) lds %d chunk %d steps/slots %d ws %zu", kern, pl.grid.x,
                                 pl.grid.y, pl.grid.z, pl.lds, pl.a.chunk_len, pl.a.nbuf, pl.ws_bytes);
     return n < 0 || (size_t)n >= cap ? FATTN_ERR_INVALID_ARG : FATTN_OK;

@@ -164,6 +164,54 @@ __device__ __forceinline__ void bd_dequant(const uint8_t* raw, uint8_t* k16, uin
     }
 }
 
+// ---- in-kernel chunk merge (SplitArgs::merge_launch == 2; every workgroup of
+// the grid co-resident, size_bd checks): the tile's workgroups publish their
+// partial rows write-through (sc1) and drain, one lane per workgroup counts on
+// the tile's arrival word (the prologue stamped it), and every workgroup then
+// merges its share of the tile's rows -- the workgroup whose add came last at
+// once, the others once their sc1 poll of the word sees the count complete
+// (or the last arriver's re-arm: generation + 1).  MI355X_MICROARCH.md,
+// inter-workgroup visibility, first row of the sc1 table: sc1 stores, every
+// storing wave drained, then the add; sc1 loads after the poll / add, the other
+// waves behind a barrier.  Row r of the tile goes to wave (r mod 8) of chunk
+// (r / 8) mod n, one merge_row_parts each: the fa_reduce LSE merge
+// (src/flash_row_float.h:415-472) in fp32, fixed order.  This replaces the
+// second launch (fattn_bd_merge_kernel) and its kernel boundary.
+template <int D>
+__device__ __forceinline__ void bd_tile_merge(const SplitArgs& a, uint8_t* smem, const float* acc, float M, float L,
+                                              int pr, int c0, bool row_valid, int tid, int lane, int wave, int qt,
+                                              int iq3, int y, int chunk) {
+    constexpr int kDpt = kBdRows * D / (kBdWaves * kWave);
+    const int64_t tile = (int64_t)iq3 * gridDim.y + y;
+    const int n = a.n_chunks;
+    const int64_t slot = (tile * n + chunk) * kBdRows + pr;
+    auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
+    if (row_valid) {
+        float* po = a.ws_o + slot * D + c0;
+#pragma unroll
+        for (int e = 0; e < kDpt; e += 4) st_sc1(po + e, u32x4{bits(acc[e]), bits(acc[e + 1]), bits(acc[e + 2]), bits(acc[e + 3])});
+        if (c0 == 0) st_sc1_x2(a.ws_ml + 2 * slot, u32x2{bits(M), bits(L)});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    __syncthreads();
+    int* flag = (int*)smem;  // (the park images were read before the barrier)
+    if (tid == 0) *flag = tile_arrive_wait(a, tile, n);
+    __syncthreads();
+    const bool ok = *flag != 0;
+    int qt_rows = min(a.QPT, a.NQ - qt * a.QPT) * a.R;
+    int ik2 = a.n_qt != 1 ? y / a.n_qt : y;
+    for (int r = chunk * kBdWaves + wave; r < qt_rows; r += kBdWaves * n) {  // wave-uniform
+        const int64_t s0 = tile * n * kBdRows + r;  // chunk 0's row r
+        const int rq = div_R(a, r);
+        float* out = a.dst + (((int64_t)iq3 * a.NQ + qt * a.QPT + rq) * a.H + ik2 * a.rk2 + (r - rq * a.R)) * D;
+        if (ok) {
+            merge_row_parts<D, 8>(a.ws_o + s0 * D, a.ws_ml + 2 * s0, n, out, lane, kBdRows * D, 2 * kBdRows);
+        } else if (lane < D / 4) {
+            *(f32x4*)(out + 4 * lane) = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+        }
+    }
+}
+
 // ---- epilogue of the batched-decode kernels (all memory traffic of the tile
 // loop drained): merge the four key quarters of each row.  Every wave parks
 // its rows' (O, m, l) in LDS (accumulator layout -> [kq][row][D + 4]); then
@@ -224,6 +272,10 @@ __device__ __forceinline__ void bd_finish(const SplitArgs& a, uint8_t* smem, con
     }
     const int rq = div_R(a, pr);
     const int q1 = qt * a.QPT + rq;
+    if (a.merge_launch == 2) {
+        bd_tile_merge<D>(a, smem, acc, M, L, pr, c0, q1 < a.NQ, tid, lane, wave, qt, iq3, y, chunk);
+        return;
+    }
     if (q1 >= a.NQ) return;
     if (a.n_chunks == 1) {
         const int q2 = ik2 * a.rk2 + (pr - rq * a.R);
@@ -275,6 +327,10 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     const int chunk = blockIdx.x;
     const int y = blockIdx.y;
     const int iq3 = blockIdx.z;
+    // in-kernel merge: stamp the tile's arrival word with this launch's epoch
+    // (no return; it is older than every counted DMA wait below, which it
+    // therefore only joins)
+    if (a.merge_launch == 2 && tid == 0) arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
     int qt = 0, ik2 = y, ik3 = iq3;
     if (a.n_qt != 1) {
         qt = y % a.n_qt;

@@ -84,8 +84,8 @@ int launch_split_e(const Plan& pl, hipStream_t st, const Events& ev) {
         if constexpr (EPI == 0) {
             // multi-row tiles: the chunk partials merge in a second launch, with
             // as few load slots per lane as the chunk count allows (the slots
-            // past it still cost issue cycles)
-            if (pl.a.merge_launch) {
+            // past it still cost issue cycles) -- unless they merge in-kernel (2)
+            if (pl.a.merge_launch == 1) {
                 const dim3 g(kRows / 4, pl.grid.y, pl.grid.z);
                 const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
                 if (need <= 2) hipLaunchKernelGGL((fattn_merge_kernel<D, 2>), g, dim3(256), 0, st, pl.a);
@@ -181,7 +181,7 @@ int launch_bd_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     auto kern = fattn_bd_kernel<KT, 128, HM>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         hipLaunchKernelGGL(kern, pl.grid, dim3(kBdWaves * kWave), pl.lds, st, pl.a);
-        if (pl.a.merge_launch) {
+        if (pl.a.merge_launch == 1) {
             const dim3 g(kBdRows / 4, pl.grid.y, pl.grid.z);
             const int need = (pl.a.n_chunks + merge_ppr<128>() - 1) / merge_ppr<128>();
             if (need <= 2) hipLaunchKernelGGL((fattn_bd_merge_kernel<128, 2>), g, dim3(256), 0, st, pl.a);

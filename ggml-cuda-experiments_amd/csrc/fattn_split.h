@@ -90,9 +90,8 @@ struct SplitArgs {
                         // 2 = one-row tiles: LDS merge, then one partial per workgroup
                         // (wg_row_merge)
     uint64_t arrival_stamp;  // kArrivalTag | launch epoch << kArrivalEpochShift (arrival_begin)
-    int handoff;        // one-row workgroup partials (wave_merge 2): 0 = data-tagged granules, no drain
-                        // (granule_handoff); 1 = write-through rows, drain, then the counter
-    int merge_launch;   // split kernel, multi-row tiles: 1 = partials merged by fattn_merge_kernel (second launch)
+    int merge_launch;   // chunk partials of multi-row tiles: 1 = merged by a second launch (fattn_merge_kernel,
+                        // fattn_bd_merge_kernel), 2 = inside the launch (tile_arrive_wait: grid co-resident)
     int step_skip;      // split kernel: 1 = skip steps whose mask is all -inf for the tile (FATTN_OPT_SPLIT_SKIP)
                         // flight beside the compute), 0 = refill a buffer once its step is computed
 };
@@ -285,8 +284,9 @@ struct StepSrc {
 // critical path): a word left by an earlier launch (re-armed or, after an
 // aborted launch, mid-count) or never zeroed (top 8 bits not all ones) is
 // superseded and the count restarts at 0.  The last arriver re-arms the word
-// (count 0, same epoch, generation + 1), so a replayed graph finds it clean
-// and its replays tell their partials apart (granule tags, wg_row_merge).
+// (count 0, same epoch, generation + 1), so a replayed graph finds it clean;
+// workgroups that wait for a tile's arrivals (bd_tile_merge) watch for the
+// count to complete or the generation to move.
 // Launches sharing one workspace must be stream-ordered.
 constexpr uint64_t kArrivalTag = 0xFFull << 56;
 constexpr int kArrivalEpochShift = 24;
@@ -313,13 +313,34 @@ __device__ __forceinline__ bool arrive_last(const SplitArgs& a, int64_t tile, in
     return last;
 }
 
-// Tag of this launch's granules (wg_row_merge): the launch epoch and the arrival
-// word's generation (which a graph replay of the same launch advances), top bit
-// set so that a zeroed workspace never matches.  `lo`: the word's low dword,
-// read after this workgroup's own stamp was performed.
-__device__ __forceinline__ uint32_t granule_tag(const SplitArgs& a, uint32_t lo) {
-    const uint32_t epoch = (uint32_t)(a.arrival_stamp >> kArrivalEpochShift);
-    return 0x80000000u | (epoch & 0x7FFFFFu) << 8 | ((lo >> 16) & 0xFFu);
+// In-kernel chunk merge (SplitArgs::merge_launch == 2, every workgroup of the
+// grid co-resident): one lane per workgroup, after every storing wave stored
+// its partials sc1 and drained and the workgroup met at a barrier, counts the
+// workgroup on the tile's arrival word (stamped in the prologue).  The last
+// arriver re-arms the word (count 0, generation + 1) and returns at once; the
+// others poll it (sc1 loads, relaxed) until the count is complete or the
+// generation has moved.  Then every workgroup of the tile may load the tile's
+// partials with sc1 loads, the other waves behind a barrier
+// (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1
+// table).  Returns 0 only when the bounded poll gave up (a fault: the caller
+// writes NaN rows instead of merging).
+__device__ __forceinline__ int tile_arrive_wait(const SplitArgs& a, int64_t tile, int n) {
+    uint64_t* w = arrival_word(a, tile);
+    const uint64_t old = __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t gen = (uint32_t)(old >> 16) & 0xFFu;
+    if ((int)(old & 0xFFFF) == n - 1) {
+        __hip_atomic_store(w, (old & ~0xFFFFFFull) | (uint64_t)((gen + 1) & 0xFFu) << 16, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        return 1;
+    }
+    for (uint32_t spins = 0; spins < (1u << 20); spins++) {
+        uint32_t lo = ld_sc1_u32((const uint32_t*)w);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        reg_fence(lo);
+        if (((lo >> 16) & 0xFFu) != gen || (int)(lo & 0xFFFF) >= n) return 1;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return 0;
 }
 
 // One step = [K rows | V rows | mask rows] for positions [n0, n0+32), copied
@@ -775,134 +796,6 @@ __device__ __forceinline__ void merge_row_parts(const float* parts_o, const floa
     *(f32x4*)(out + d4) = acc * inv;
 }
 
-// Cross-workgroup hand-off of one-row partials as data-tagged granules
-// (cdna_hip_programming.md Guideline 16, R2: the data is the flag).  Every
-// value of the workgroup's merged row -- D dims, then (m, l) -- is one aligned
-// 8-byte {value, tag} granule written by an sc1 store; no drain precedes the
-// arrival count, so the publish costs no round trip of its own.  The last
-// arriver (told by the counter) sweeps the other chunks' granules with sc1
-// loads until every tag is this launch's (a store still in flight shows an
-// older tag: re-read) and merges them with its own row, still in registers --
-// the fa_reduce LSE merge (src/flash_row_float.h:415-472) in fp32, in chunk
-// order.  Slot layout [tile][chunk][D + 2] granules; lane (h, j) owns DPL dims
-// at 4j + DPL h (the wave merge's own layout, so no lane moves).
-template <int D>
-__device__ __forceinline__ void granule_handoff(const SplitArgs& a, const f32x4& acc, float M, float L, int chunk,
-                                                int64_t tile, int lane, uint32_t tag, float* out) {
-    constexpr float kNegInf = -__builtin_inff();
-    constexpr int LPP = D / 4;
-    constexpr int PPR = merge_ppr<D>();
-    constexpr int DPL = PPR >= 2 ? 2 : 4;  // dims per lane: 2 (D = 64, 128) or 4 (D = 80, 96, 256)
-    constexpr int LPC = DPL / 2;           // 16-B granule pairs per chunk and lane
-    constexpr int GS = D + 2;              // granules per chunk slot
-    constexpr int CB = 16 / LPC;           // chunks per sweep pass
-    const int h = lane / LPP;
-    const bool act = h * DPL < 4;
-    const int dl = 4 * (lane % LPP) + DPL * h;
-    float own[4];
-    own[0] = (DPL == 2 && h == 1) ? acc.z : acc.x;
-    own[1] = (DPL == 2 && h == 1) ? acc.w : acc.y;
-    own[2] = acc.z;
-    own[3] = acc.w;
-    const int n = a.n_chunks;
-    uint64_t* gs = (uint64_t*)a.ws_o + tile * n * GS;
-    auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
-    {
-        uint64_t* mine = gs + chunk * GS;
-        if (act) {
-#pragma unroll
-            for (int j = 0; j < LPC; j++) st_sc1(mine + dl + 2 * j, u32x4{bits(own[2 * j]), tag, bits(own[2 * j + 1]), tag});
-        }
-        if (lane == 0) st_sc1(mine + D, u32x4{bits(M), tag, bits(L), tag});
-    }
-    int last = 0;
-    if (lane == 0) last = arrive_last(a, tile, n);  // (its wait also retires the stores: in flight together)
-    last = __builtin_amdgcn_readfirstlane(last);
-    FATTN_STAMP(14);
-    if (!last) return;
-
-    const uint32_t bytes = (uint32_t)(n * GS * 8);
-    const i32x4 srd = make_srd(gs, bytes);
-    const bool ml_ld = lane < n && lane != chunk;
-    const uint32_t ml_off = ml_ld ? (uint32_t)((lane * GS + D) * 8) : bytes;  // past the descriptor: zeros, no traffic
-    u32x4 mlv;
-    u32x4 v[CB * LPC];
-    auto valid = [&](int c) { return c < n && c != chunk && act; };
-    auto issue = [&](int c0) {
-#pragma unroll
-        for (int i = 0; i < CB; i++) {
-            const int c = c0 + i;
-#pragma unroll
-            for (int j = 0; j < LPC; j++)
-                v[i * LPC + j] = ld_sc1_buf(srd, valid(c) ? (uint32_t)((c * GS + dl + 2 * j) * 8) : bytes);
-        }
-    };
-    auto landed = [&](int c0) {
-        bool ok = true;
-#pragma unroll
-        for (int i = 0; i < CB; i++) {
-            const bool vc = valid(c0 + i);
-#pragma unroll
-            for (int j = 0; j < LPC; j++) {
-                reg_fence(v[i * LPC + j]);
-                ok &= !vc || (v[i * LPC + j].y == tag && v[i * LPC + j].w == tag);
-            }
-        }
-        return ok;
-    };
-    // bounded sweep: every arrival precedes the last one's count, so every
-    // granule is in flight or landed; the bound only turns a fault into NaNs
-    constexpr uint32_t kSpinMax = 1u << 20;
-    auto sweep = [&](int c0, bool with_ml) {
-        for (uint32_t spins = 0;; spins++) {
-            if (with_ml) mlv = ld_sc1_buf(srd, ml_off);
-            issue(c0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            bool ok = landed(c0);
-            if (with_ml) {
-                reg_fence(mlv);
-                ok &= !ml_ld || (mlv.y == tag && mlv.w == tag);
-            }
-            if (__builtin_amdgcn_ballot_w64(!ok) == 0) return true;
-            if (spins == kSpinMax) return false;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    };
-    bool fine = sweep(0, true);
-    const float mp = lane == chunk ? M : (lane < n ? __builtin_bit_cast(float, mlv.x) : kNegInf);
-    const float lp = lane == chunk ? L : (lane < n ? __builtin_bit_cast(float, mlv.z) : 0.0f);
-    const float Mx = seg_reduce<true>(mp, 64);
-    const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - Mx);
-    const float Lt = seg_reduce<false>(w * lp, 64);
-    const int wi = __builtin_bit_cast(int, w);
-    float r[DPL];
-#pragma unroll
-    for (int k = 0; k < DPL; k++) r[k] = 0.0f;
-    for (int c0 = 0; c0 < n; c0 += CB) {  // wave-uniform
-        if (c0 > 0) fine &= sweep(c0, false);
-#pragma unroll
-        for (int i = 0; i < CB; i++) {
-            const int c = c0 + i;
-            if (c >= n) break;
-            const float wc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(wi, c));
-#pragma unroll
-            for (int j = 0; j < LPC; j++) {
-                const float v0 = c == chunk ? own[2 * j] : __builtin_bit_cast(float, v[i * LPC + j].x);
-                const float v1 = c == chunk ? own[2 * j + 1] : __builtin_bit_cast(float, v[i * LPC + j].z);
-                r[2 * j] += wc * v0;
-                r[2 * j + 1] += wc * v1;
-            }
-        }
-    }
-    if (!act) return;
-    const float inv = (Lt == 0.0f || !fine) ? __builtin_nanf("") : 1.0f / Lt;  // L == 0 (row fully masked) -> NaN
-    if constexpr (DPL == 2) {
-        *(f32x2*)(out + dl) = f32x2{r[0] * inv, r[1] * inv};
-    } else {
-        *(f32x4*)(out + dl) = f32x4{r[0] * inv, r[1] * inv, r[2] * inv, r[3] * inv};
-    }
-}
-
 // One-row tiles, NW waves per workgroup: every wave writes its row-0 state
 // (O, m, l) into its own LDS region (its steps have all landed), one barrier,
 // then wave 0 merges the NW states (lane (h, dl): states p = h mod PPR, dims
@@ -921,13 +814,6 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
     constexpr int LPP = D / 4;
     constexpr int PPR = 64 % LPP == 0 ? 64 / LPP : 1;  // (D = 80 / 96: one part per lane row)
     const int g = lane >> 4, m = lane & 15;
-    const int64_t tile = (int64_t)iq3 * gridDim.y + blockIdx.y;
-    // granule hand-off: the arrival word's generation, read while the waves
-    // meet in LDS (this workgroup's stamp has been performed: the loop ended
-    // with vmcnt(0)); asm load, waited for before the granule stores
-    uint32_t word_lo = 0;
-    const bool granules = a.n_chunks > 1 && a.handoff == 0;
-    if (granules && wave == 0 && lane == 0) word_lo = ld_sc1_u32((const uint32_t*)arrival_word(a, tile));
     float* so = (float*)(smem + wave * region);  // [D] O row, then (m, l)
     if (m == 0) {  // column 0 = the tile's row; its dims sit on lanes 0, 16, 32, 48
         if constexpr (VQ8) {
@@ -997,14 +883,7 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
     if (acc.x == 12345.0f) a.dst[0] = L;  // diagnostic build only: stop after the workgroup merge
     return;
 #endif
-    if (granules) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        reg_fence(word_lo);
-        const uint32_t tag = granule_tag(a, __builtin_amdgcn_readfirstlane(word_lo));
-        granule_handoff<D>(a, acc, M, L, chunk, tile, lane, tag, out);
-        FATTN_STAMP(13);
-        return;
-    }
+    const int64_t tile = (int64_t)iq3 * gridDim.y + blockIdx.y;
     float* po = a.ws_o + (tile * a.n_chunks + chunk) * D;
     auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
     if (h == 0) st_sc1(po + d4, u32x4{bits(acc.x), bits(acc.y), bits(acc.z), bits(acc.w)});
@@ -1173,7 +1052,31 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
     }
     // second-launch merge (fattn_merge_kernel): the kernel boundary orders
     // these stores before its loads; no drain, no counter
-    if (a.merge_launch) return;
+    if (a.merge_launch == 1) return;
+    if (a.merge_launch == 2) {
+        // in-kernel: wait for the tile's chunks, then every workgroup merges a
+        // share of the tile's rows, one wave per row (row r: wave r mod NW of
+        // chunk (r / NW) mod n_chunks), as fattn_merge_kernel would
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+        __syncthreads();
+        int* flag = (int*)smem;  // (every wave is done reading the merge images)
+        if (threadIdx.x == 0) *flag = tile_arrive_wait(a, tile, a.n_chunks);
+        __syncthreads();
+        const bool ok = *flag != 0;
+        FATTN_STAMP(12);
+        for (int r = chunk * NW + wave; r < rv; r += NW * a.n_chunks) {  // wave-uniform
+            const int64_t s0 = tile * a.n_chunks * kRows + r;  // chunk 0's row r
+            float* out = dst_row(r);
+            if (ok) {
+                merge_row_parts<D, 8>(a.ws_o + s0 * D, a.ws_ml + 2 * s0, a.n_chunks, out, lane, kRows * D, 2 * kRows);
+            } else if (lane < D / 4) {
+                *(f32x4*)(out + 4 * lane) = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""),
+                                                  __builtin_nanf("")};
+            }
+        }
+        FATTN_STAMP(13);
+        return;
+    }
     // every storing wave drains: the merging workgroup reads its own partial back too
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef FATTN_DIAG_NOATOMIC
@@ -1492,7 +1395,7 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     // this launch's stamp on the tile's arrival word, by each lane that will
     // count an arrival: issued after the prologue's DMA, so no wait is spent
     // on it (at most one DMA instruction's worth in the counted waits below)
-    if (a.n_chunks > 1 && !a.merge_launch && lane == 0 && (EPI == 1 || wave == 0))
+    if (a.n_chunks > 1 && a.merge_launch != 1 && lane == 0 && (EPI == 1 || wave == 0))
         arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
 
     FATTN_STAMP(1);

@@ -119,8 +119,7 @@ size_t fattn_workspace_size(const fattn_params* p);
  * an earlier or an aborted launch is superseded -- but not a never-initialised
  * word whose top 8 bits are all ones with an epoch above the current one (e.g.
  * 0xFF fill), which this call clears.  The last arriver re-arms a word (count 0,
- * generation + 1); one-row partials handed over as granules carry (epoch,
- * generation) tags, so a replayed graph never reads a previous replay's. */
+ * generation + 1), so a replayed graph finds it clean. */
 int fattn_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 int fattn_ext(const fattn_params* p, void* stream);
 
@@ -164,16 +163,18 @@ enum {
     FATTN_OPT_SPLIT_SKIP = 20       /* split kernel, masked: 0 = steps whose mask is -inf for every key and row
                                        of the tile are neither loaded nor computed (default; the mask words are
                                        read beside Q), 1 = every step loaded and computed */,
-    FATTN_OPT_SPLIT_MERGE = 21,     /* split kernel, tiles of several packed rows: 0 = the chunk partials merge in
-                                       a second launch, one wave per (tile, row) (default), 1 = the last-arriving
-                                       workgroup merges the whole tile (combine_tile) */
+    FATTN_OPT_SPLIT_MERGE = 21,     /* split kernel, tiles of several packed rows: 0 = with 4+ chunks the partials
+                                       merge one wave per (tile, row), in-kernel or in a second launch
+                                       (FATTN_OPT_MERGE_LAUNCH) (default), 1 = the last-arriving workgroup merges
+                                       the whole tile (combine_tile) */
     FATTN_OPT_BD = 22               /* batched-decode kernel (64-row workgroups, D = 128 Q8_0 / Q4_0, contiguous
                                        rows): 0 = auto (from 64 packed rows per kv head, below the prefill
                                        shapes), 1 = never, 2 = whenever eligible */,
-    FATTN_OPT_SPLIT_HANDOFF = 23    /* split kernel, one-row tiles merged per workgroup over several chunks: 0 =
-                                       each workgroup's row goes out as data-tagged granules with no drain and
-                                       the last arriver sweeps them (default), 1 = write-through row, drain,
-                                       then the arrival count */
+    /* 23: a removed experiment (one-row partials as data-tagged granules), rejected */
+    FATTN_OPT_MERGE_LAUNCH = 24     /* chunk partials of multi-row tiles (split kernel with 4+ chunks, batched-
+                                       decode kernel): 0 = merged inside the launch when the whole grid is
+                                       co-resident -- the tile's workgroups wait for each other, then each merges
+                                       a share of the rows (default); 1 = always a second launch */
 };
 int fattn_set_option(int option, int value);
 

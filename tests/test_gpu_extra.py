@@ -424,9 +424,8 @@ def test_cpy_into_kv_cache_view(dev, kt, layout, ntok):
     assert np.array_equal(got, want)
 
 
-# ------------------------------------------------------------------ one-row hand-off forms (granules / drain)
+# ------------------------------------------------------------------ chunk merges: one-row tiles, batched decode in-kernel
 
-@pytest.mark.parametrize("handoff", [0, 1], ids=["granules", "drain"])
 @pytest.mark.parametrize("case", [
     dict(D=128, H=32, N=4096, kv_type="q8_0"),                 # config 3 (8 waves, 8 chunks)
     dict(D=128, H=8, N=8192, kv_type="q4_0", mask="tail"),      # whole chunks -inf
@@ -435,67 +434,144 @@ def test_cpy_into_kv_cache_view(dev, kt, layout, ntok):
     dict(D=96, H=16, N=4096, kv_type="q8_0"),
     dict(D=256, H=16, N=2048, kv_type="f16"),
 ], ids=["cfg3", "q4_tail", "d64", "d80", "d96", "d256"])
-def test_row_handoff_forms(dev, handoff, case):
-    """One-row tiles over several KV chunks (workgroup merge, wave_merge 2):
-    the partial rows reach the last arriver either as data-tagged granules
-    (default) or as write-through rows behind a drain; both against the oracle
-    at every head dim, with forced chunk counts up to 32."""
+def test_row_merge_head_dims(dev, case):
+    """One-row tiles over several KV chunks (workgroup merge + last-arriver
+    row merge) at every head dim, with forced chunk counts, against the oracle."""
     import torch
     p = make_problem(seed=5 + case["D"], **case)
     ref = p.oracle()
     t = upload(p, dev)
-    fattn.set_option(fattn.OPT_SPLIT_HANDOFF, handoff)
+    for chunk in (0, 256, 512):
+        att = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=chunk)
+        t["dst"].fill_(float("nan"))
+        att()
+        torch.cuda.synchronize()
+        assert attn_rel_err(t["dst"].cpu().numpy(), ref) <= RTOL, att.describe()
+
+
+def _replay_new_inputs(dev, shape, n_iter=12):
+    """Capture one launch, then replay it (same epoch every replay) over K/V/Q/
+    mask rewritten in place between replays, under uneven load from a copy
+    stream; every replay against the oracle of its own inputs."""
+    import torch
+    probs = [make_problem(seed=400 + i, **shape) for i in range(3)]
+    refs = [p.oracle() for p in probs]
+    t = upload(probs[0], dev)
+    att = fattn.Attention(*views(probs[0], t), t["dst"], probs[0].scale)
+    assert int(att.describe().split("grid(")[1].split(",")[0]) > 1, att.describe()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        att(s.cuda_stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        att(s.cuda_stream)
+    noise_src = torch.randn(1 << 25, device=dev)
+    noise_dst = torch.empty_like(noise_src)
+    side = torch.cuda.Stream()
+    for it in range(n_iter):
+        p = probs[it % 3]
+        t["q"].copy_(torch.from_numpy(np.ascontiguousarray(p.q)))
+        t["k"].copy_(torch.from_numpy(p.k_bytes))
+        t["v"].copy_(torch.from_numpy(p.v_bytes))
+        t["mask"].copy_(torch.from_numpy(np.ascontiguousarray(p.mask_bits).view(np.int16)))
+        t["dst"].fill_(float("nan"))
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            for _ in range(it % 3):
+                noise_dst.copy_(noise_src)
+        g.replay()
+        torch.cuda.synchronize()
+        assert attn_rel_err(t["dst"].cpu().numpy(), refs[it % 3]) <= RTOL, f"replay {it}: {att.describe()}"
+    return att.describe()
+
+
+def test_row_merge_graph_replays_new_inputs(dev):
+    """Config 3 (one-row tiles, last-arriver merge): a captured launch replays
+    with one epoch; the arrival words re-arm (count 0, generation + 1) so every
+    replay merges its own partials."""
+    _replay_new_inputs(dev, dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0"))
+
+
+@pytest.mark.parametrize("merge_launch", [0, 1], ids=["in_kernel", "second_launch"])
+@pytest.mark.parametrize("case", [
+    dict(D=128, NQ=64, H=32, N=4096, kv_type="q8_0"),                 # config 5 (8 chunks per kv head)
+    dict(D=128, NQ=64, H=16, N=4096, kv_type="q8_0"),                 # its 2-rank shard
+    dict(D=128, NQ=40, H=32, Hkv=8, N=4096, kv_type="q4_0", mask="causal"),  # GQA, partial row tile, causal
+    dict(D=128, NQ=64, H=8, N=8192, kv_type="q8_0", mask="tail"),     # whole chunks -inf
+], ids=["cfg5", "cfg5_h16", "gqa_causal", "tail"])
+def test_bd_chunk_merge_forms(dev, merge_launch, case):
+    """The batched-decode kernel over several KV chunks: the tile's workgroups
+    merge the partials inside the launch (every workgroup co-resident: each
+    waits for the tile's count, then merges its share of the rows) or in the
+    second launch; both against the oracle, forced chunk counts included."""
+    import torch
+    p = make_problem(seed=90 + case["H"], **case)
+    ref = p.oracle()
+    t = upload(p, dev)
+    fattn.set_option(fattn.OPT_MERGE_LAUNCH, merge_launch)
     try:
-        for chunk in (0, 256, 512):
+        for chunk in (0, 1024):
+            att = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=chunk)
+            desc = att.describe()
+            assert "fattn_bd_kernel" in desc, desc
+            assert ("in-kernel" in desc) == (merge_launch == 0), desc
+            t["dst"].fill_(float("nan"))
+            att()
+            torch.cuda.synchronize()
+            assert attn_rel_err(t["dst"].cpu().numpy(), ref) <= RTOL, desc
+    finally:
+        fattn.set_option(fattn.OPT_MERGE_LAUNCH, 0)
+
+
+def test_bd_in_kernel_merge_graph_replays_new_inputs(dev):
+    """Config 5 through the batched-decode kernel with the in-kernel merge: the
+    waiting workgroups watch the arrival word for a complete count or the last
+    arriver's re-arm (generation + 1), which must hold replay after replay of
+    one captured launch (one epoch)."""
+    desc = _replay_new_inputs(dev, dict(D=128, NQ=64, H=32, N=4096, kv_type="q8_0"), n_iter=9)
+    assert "in-kernel" in desc, desc
+
+
+@pytest.mark.parametrize("merge_launch", [0, 1], ids=["in_kernel", "second_launch"])
+@pytest.mark.parametrize("case", [
+    dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0"),           # config 4
+    dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0"),                  # config 5, 8-rank shard
+    dict(D=128, NQ=16, H=4, N=4096, kv_type="q8_0", mask="tail"),     # whole chunks -inf
+    dict(D=64, NQ=8, H=16, Hkv=4, N=4096, kv_type="q8_0"),
+    dict(D=96, NQ=4, H=16, Hkv=4, N=4096, kv_type="q8_0"),
+    dict(D=256, NQ=4, H=8, Hkv=2, N=2048, kv_type="f16"),
+], ids=["cfg4", "cfg5_shard", "tail", "d64", "d96", "d256"])
+def test_split_multirow_merge_forms(dev, merge_launch, case):
+    """Multi-row split tiles over 4+ KV chunks: the partials merge one wave per
+    (tile, row), inside the launch (the tile's workgroups wait for each other)
+    or in the second launch; both against the oracle at several head dims."""
+    import torch
+    p = make_problem(seed=70 + case["D"], **case)
+    ref = p.oracle()
+    t = upload(p, dev)
+    fattn.set_option(fattn.OPT_MERGE_LAUNCH, merge_launch)
+    fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
+    try:
+        for chunk in (0, 256):
             att = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=chunk)
             desc = att.describe()
             t["dst"].fill_(float("nan"))
             att()
             torch.cuda.synchronize()
-            got = t["dst"].cpu().numpy()
-            assert attn_rel_err(got, ref) <= RTOL, desc
+            assert attn_rel_err(t["dst"].cpu().numpy(), ref) <= RTOL, desc
     finally:
-        fattn.set_option(fattn.OPT_SPLIT_HANDOFF, 0)
+        fattn.set_option(fattn.OPT_MERGE_LAUNCH, 0)
+        fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
 
 
-@pytest.mark.parametrize("handoff", [0, 1], ids=["granules", "drain"])
-def test_row_handoff_graph_replays_new_inputs(dev, handoff):
-    """A captured launch replays with the SAME epoch: the granule tags carry
-    the arrival word's generation, which every replay advances, so a replay
-    never merges a previous replay's partials.  K and V change between replays
-    (in place, as a KV cache does); every replay is checked against the oracle
-    of its own inputs, under uneven load from a copy stream."""
-    import torch
-    fattn.set_option(fattn.OPT_SPLIT_HANDOFF, handoff)
+def test_split_in_kernel_merge_graph_replays_new_inputs(dev):
+    """Config 4 (multi-row split tiles, in-kernel merge) replayed from one
+    captured launch over changing inputs: the waiting workgroups see each
+    replay's own count / generation."""
+    fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
     try:
-        probs = [make_problem(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", seed=400 + i) for i in range(3)]
-        refs = [p.oracle() for p in probs]
-        t = upload(probs[0], dev)
-        att = fattn.Attention(*views(probs[0], t), t["dst"], probs[0].scale)
-        assert int(att.describe().split("grid(")[1].split(",")[0]) > 1, att.describe()
-        s = torch.cuda.Stream()
-        with torch.cuda.stream(s):
-            att(s.cuda_stream)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            att(s.cuda_stream)
-        noise_src = torch.randn(1 << 25, device=dev)
-        noise_dst = torch.empty_like(noise_src)
-        side = torch.cuda.Stream()
-        for it in range(12):
-            p = probs[it % 3]
-            t["q"].copy_(torch.from_numpy(np.ascontiguousarray(p.q)))
-            t["k"].copy_(torch.from_numpy(p.k_bytes))
-            t["v"].copy_(torch.from_numpy(p.v_bytes))
-            t["mask"].copy_(torch.from_numpy(np.ascontiguousarray(p.mask_bits).view(np.int16)))
-            t["dst"].fill_(float("nan"))
-            torch.cuda.synchronize()
-            with torch.cuda.stream(side):
-                for _ in range(it % 3):
-                    noise_dst.copy_(noise_src)
-            g.replay()
-            torch.cuda.synchronize()
-            assert attn_rel_err(t["dst"].cpu().numpy(), refs[it % 3]) <= RTOL, f"replay {it}"
+        desc = _replay_new_inputs(dev, dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0"), n_iter=9)
     finally:
-        fattn.set_option(fattn.OPT_SPLIT_HANDOFF, 0)
+        fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
+    assert "in-kernel" in desc, desc
