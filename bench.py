@@ -303,8 +303,8 @@ def parse_args(argv=None):
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--no-mq", action="store_true", help="never pick the multi-query kernel (split-KV kernel only)")
     ap.add_argument("--bd", type=int, default=0, help="batched-decode kernel: 0 auto, 1 never, 2 whenever eligible")
-    ap.add_argument("--merge-launch", type=int, default=0,
-                    help="multi-row chunk merge: 0 in-kernel when the grid is co-resident, 1 second launch")
+    ap.add_argument("--merge-in-kernel", type=int, default=0,
+                    help="multi-row chunk merge: 0 second launch, 1 in-kernel when the grid is co-resident")
     ap.add_argument("--split-prio", type=int, default=0,
                     help="split kernel wave priorities: 0 staggered, 1 none, 2 staggered while issuing")
     ap.add_argument("--waves", type=int, default=0, help="split kernel waves per workgroup (4, 8, 16; 0 = planner)")
@@ -336,7 +336,7 @@ def apply_options(args):
             (args.waves, fattn.OPT_SPLIT_WAVES)]
     fattn.set_option(fattn.OPT_SPLIT_SKIP, 1 if args.no_step_skip else 0)
     fattn.set_option(fattn.OPT_SPLIT_MERGE, 1 if args.fused_merge else 0)
-    fattn.set_option(fattn.OPT_MERGE_LAUNCH, args.merge_launch)
+    fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, args.merge_in_kernel)
     for val, opt in opts:
         if val:
             fattn.set_option(opt, val)

@@ -59,7 +59,7 @@ std::atomic<int> g_opt_split_waves{0};      // split kernel waves per workgroup 
 std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
-std::atomic<int> g_opt_merge_launch{0};  // 1: multi-row chunk partials always merge in a second launch (FATTN_OPT_MERGE_LAUNCH)
+std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
 std::atomic<uint32_t> g_epoch{0};
 
@@ -215,14 +215,16 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     // 14.8 us, config 4: 10.0 vs 10.7; with 2 chunks per tile, config 5 on
     // one GPU, the extra launch costs more than it saves: 36.6 vs 35.6).
     // FATTN_OPT_SPLIT_MERGE = 1: always the last-arriving workgroup (combine_tile).
-    // ... or, with the whole grid co-resident, inside the launch: the tile's
-    // workgroups wait for each other and each merges a share of the rows
-    // (tile_arrive_wait; FATTN_OPT_MERGE_LAUNCH = 1 keeps the second launch)
+    // FATTN_OPT_MERGE_IN_KERNEL = 1, with the whole grid co-resident: inside
+    // the launch instead, the tile's workgroups waiting for each other and each
+    // merging a share of the rows (tile_arrive_wait): measured 0.6-1.1 us
+    // slower than the second launch (config 4 10.7-10.9 vs 10.0-10.3 us, the
+    // config-5 8-rank shard 12.2 vs 11.6-11.7; profiles/r03_merge)
     pl.lds = G.lds_bytes(nbuf, nwv);
     const int64_t wgs_cu = std::max(1, std::min(4 * wps / nwv, kLdsPerCU / pl.lds));
     const bool resident = (int64_t)a.n_chunks * Y * S <= (int64_t)pl.cus * wgs_cu;
     a.merge_launch = (a.n_chunks >= 4 && a.wave_merge == 0 && !g_opt_split_fused_merge)
-                         ? ((resident && !g_opt_merge_launch) ? 2 : 1) : 0;
+                         ? ((resident && g_opt_merge_in_kernel) ? 2 : 1) : 0;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     if (a.n_chunks > 1 && a.wave_merge) {
         // [arrival counters][(m, l) per part][row-0 O per part]; parts = waves
@@ -335,7 +337,7 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     // co-resident -- one workgroup per CU by LDS) or in a second launch
     const int64_t per_cu = std::max<int64_t>(1, kLdsPerCU / pl.lds);
     const bool resident = nch * Y * S <= (int64_t)pl.cus * per_cu;
-    a.merge_launch = nch == 1 ? 0 : (resident && !g_opt_merge_launch) ? 2 : 1;
+    a.merge_launch = nch == 1 ? 0 : (resident && g_opt_merge_in_kernel) ? 2 : 1;
     if (nch > 1) {
         // [arrival words, in-kernel merge only][(m, l) pairs][O partials]: [S][Y][chunks][64 rows]
         const size_t slots = (size_t)S * Y * nch * kBdRows;
@@ -621,9 +623,9 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_bd = value;
             return FATTN_OK;
-        case FATTN_OPT_MERGE_LAUNCH:
+        case FATTN_OPT_MERGE_IN_KERNEL:
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
-            g_opt_merge_launch = value;
+            g_opt_merge_in_kernel = value;
             return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:
             if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;

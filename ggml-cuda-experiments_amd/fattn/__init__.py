@@ -50,7 +50,7 @@ OPT_SPLIT_WAVES = 19
 OPT_SPLIT_SKIP = 20
 OPT_SPLIT_MERGE = 21
 OPT_BD = 22
-OPT_MERGE_LAUNCH = 24
+OPT_MERGE_IN_KERNEL = 24
 
 
 class FattnError(RuntimeError):

@@ -164,17 +164,17 @@ enum {
                                        of the tile are neither loaded nor computed (default; the mask words are
                                        read beside Q), 1 = every step loaded and computed */,
     FATTN_OPT_SPLIT_MERGE = 21,     /* split kernel, tiles of several packed rows: 0 = with 4+ chunks the partials
-                                       merge one wave per (tile, row), in-kernel or in a second launch
-                                       (FATTN_OPT_MERGE_LAUNCH) (default), 1 = the last-arriving workgroup merges
+                                       merge one wave per (tile, row), in a second launch or in-kernel
+                                       (FATTN_OPT_MERGE_IN_KERNEL) (default), 1 = the last-arriving workgroup merges
                                        the whole tile (combine_tile) */
     FATTN_OPT_BD = 22               /* batched-decode kernel (64-row workgroups, D = 128 Q8_0 / Q4_0, contiguous
                                        rows): 0 = auto (from 64 packed rows per kv head, below the prefill
                                        shapes), 1 = never, 2 = whenever eligible */,
     /* 23: a removed experiment (one-row partials as data-tagged granules), rejected */
-    FATTN_OPT_MERGE_LAUNCH = 24     /* chunk partials of multi-row tiles (split kernel with 4+ chunks, batched-
-                                       decode kernel): 0 = merged inside the launch when the whole grid is
-                                       co-resident -- the tile's workgroups wait for each other, then each merges
-                                       a share of the rows (default); 1 = always a second launch */
+    FATTN_OPT_MERGE_IN_KERNEL = 24  /* chunk partials of multi-row tiles (split kernel with 4+ chunks, batched-
+                                       decode kernel): 0 = merged in a second launch (default); 1 = inside the
+                                       launch when the whole grid is co-resident -- the tile's workgroups wait
+                                       for each other, then each merges a share of the rows (0.6-1.5 us slower) */
 };
 int fattn_set_option(int option, int value);
 

@@ -67,38 +67,39 @@ def test_workspace_size_config3():
 @pytest.mark.parametrize("kw,want", [
     (dict(), ["8waves>", "grid(8,32,1)", "steps/slots 1"]),                                 # config 3
     (dict(N=2048, kt=fattn.TYPE_F16), ["f16,f16", "8waves>", "grid(8,32,1)"]),              # config 2
-    (dict(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0), ["4waves> (in-kernel merge)", "grid(32,8,1)"]),  # config 4
-    (dict(NQ=64), ["fattn_bd_kernel", "(in-kernel merge)", "grid(8,32,1)"]),               # config 5, one GPU
-    (dict(NQ=64, H=4, Hkv=4), ["fattn_split_kernel", "(in-kernel merge)"]),               # config 5, 8-rank shard
-    (dict(NQ=64, H=16, Hkv=16), ["fattn_bd_kernel", "(in-kernel merge)", "grid(16,16,1)"]),  # config 5, 2-rank shard
+    (dict(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0), ["4waves> + fattn_merge_kernel", "grid(32,8,1)"]),  # config 4
+    (dict(NQ=64), ["fattn_bd_kernel", "+ fattn_bd_merge_kernel", "grid(8,32,1)"]),         # config 5, one GPU
+    (dict(NQ=64, H=4, Hkv=4), ["fattn_split_kernel", "+ fattn_merge_kernel"]),             # config 5, 8-rank shard
+    (dict(NQ=64, H=16, Hkv=16), ["fattn_bd_kernel", "+ fattn_bd_merge_kernel", "grid(16,16,1)"]),  # config 5, 2-rank shard
     (dict(NQ=256), ["fattn_bd_kernel", "grid(2,128,1)"]),                                   # batched: 4 row tiles
-    (dict(NQ=8, H=32, Hkv=8), ["fattn_split_kernel", "(in-kernel merge)"]),                # < 64 rows per kv head
+    (dict(NQ=8, H=32, Hkv=8), ["fattn_split_kernel", "+ fattn_merge_kernel"]),              # < 64 rows per kv head
     (dict(D=64, NQ=4096, H=32, Hkv=32), ["fattn_pf_kernel<q8_0,D64"]),                       # D = 64 prefill
     (dict(D=256, NQ=4096, H=16, Hkv=16), ["fattn_mq_kernel<q8_0,D256,4waves"]),              # D = 256 prefill
 ], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "split_nq8_gqa", "pf_d64", "mq_d256"])
 def test_planner_picks(kw, want):
     """The plans the round-2 measurements chose, at 256 CUs:
     one-row tiles take 8 waves with the fused row merge; multi-row split tiles
-    with 4+ chunks merge in a second launch; batched-decode tiles merge inside
-    the launch (grid co-resident); long multi-row slices take twice the chunks."""
+    with 4+ chunks and batched-decode tiles merge in a second launch; long
+    multi-row slices take twice the chunks."""
     d = fattn.describe(_params(**kw))
     for w in want:
         assert w in d, d
 
 
-def test_bd_merge_option_restores_second_launch():
-    fattn.set_option(fattn.OPT_MERGE_LAUNCH, 1)
+def test_merge_in_kernel_option():
+    fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 1)
     try:
         d = fattn.describe(_params(NQ=64))
-        assert "+ fattn_bd_merge_kernel" in d, d
-        # the second launch needs no arrival words: a smaller workspace
+        assert "(in-kernel merge)" in d, d
+        d4 = fattn.describe(_params(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0))
+        assert "4waves> (in-kernel merge)" in d4, d4
         ws1 = fattn.workspace_size(_params(NQ=64))
     finally:
-        fattn.set_option(fattn.OPT_MERGE_LAUNCH, 0)
+        fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 0)
     ws0 = fattn.workspace_size(_params(NQ=64))
-    assert ws0 == ws1 + 32 * 256  # one 256-B arrival line per tile for the in-kernel merge
+    assert ws1 == ws0 + 32 * 256  # one 256-B arrival line per tile for the in-kernel merge
     with pytest.raises(Exception):
-        fattn.set_option(fattn.OPT_MERGE_LAUNCH, 2)  # rejected (FATTN_ERR_INVALID_ARG)
+        fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 2)  # rejected (FATTN_ERR_INVALID_ARG)
 
 
 def test_split_merge_option_restores_fused_merge():

@@ -493,35 +493,36 @@ def test_row_merge_graph_replays_new_inputs(dev):
     _replay_new_inputs(dev, dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0"))
 
 
-@pytest.mark.parametrize("merge_launch", [0, 1], ids=["in_kernel", "second_launch"])
+@pytest.mark.parametrize("in_kernel", [1, 0], ids=["in_kernel", "second_launch"])
 @pytest.mark.parametrize("case", [
     dict(D=128, NQ=64, H=32, N=4096, kv_type="q8_0"),                 # config 5 (8 chunks per kv head)
     dict(D=128, NQ=64, H=16, N=4096, kv_type="q8_0"),                 # its 2-rank shard
     dict(D=128, NQ=40, H=32, Hkv=8, N=4096, kv_type="q4_0", mask="causal"),  # GQA, partial row tile, causal
     dict(D=128, NQ=64, H=8, N=8192, kv_type="q8_0", mask="tail"),     # whole chunks -inf
 ], ids=["cfg5", "cfg5_h16", "gqa_causal", "tail"])
-def test_bd_chunk_merge_forms(dev, merge_launch, case):
-    """The batched-decode kernel over several KV chunks: the tile's workgroups
-    merge the partials inside the launch (every workgroup co-resident: each
-    waits for the tile's count, then merges its share of the rows) or in the
-    second launch; both against the oracle, forced chunk counts included."""
+def test_bd_chunk_merge_forms(dev, in_kernel, case):
+    """The batched-decode kernel over several KV chunks: the partials merge in
+    the second launch (default) or inside the launch (FATTN_OPT_MERGE_IN_KERNEL:
+    every workgroup co-resident, each waits for the tile's count, then merges
+    its share of the rows); both against the oracle, forced chunk counts
+    included."""
     import torch
     p = make_problem(seed=90 + case["H"], **case)
     ref = p.oracle()
     t = upload(p, dev)
-    fattn.set_option(fattn.OPT_MERGE_LAUNCH, merge_launch)
+    fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, in_kernel)
     try:
         for chunk in (0, 1024):
             att = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=chunk)
             desc = att.describe()
             assert "fattn_bd_kernel" in desc, desc
-            assert ("in-kernel" in desc) == (merge_launch == 0), desc
+            assert ("in-kernel" in desc) == (in_kernel == 1), desc
             t["dst"].fill_(float("nan"))
             att()
             torch.cuda.synchronize()
             assert attn_rel_err(t["dst"].cpu().numpy(), ref) <= RTOL, desc
     finally:
-        fattn.set_option(fattn.OPT_MERGE_LAUNCH, 0)
+        fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 0)
 
 
 def test_bd_in_kernel_merge_graph_replays_new_inputs(dev):
@@ -529,11 +530,15 @@ def test_bd_in_kernel_merge_graph_replays_new_inputs(dev):
     waiting workgroups watch the arrival word for a complete count or the last
     arriver's re-arm (generation + 1), which must hold replay after replay of
     one captured launch (one epoch)."""
-    desc = _replay_new_inputs(dev, dict(D=128, NQ=64, H=32, N=4096, kv_type="q8_0"), n_iter=9)
+    fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 1)
+    try:
+        desc = _replay_new_inputs(dev, dict(D=128, NQ=64, H=32, N=4096, kv_type="q8_0"), n_iter=9)
+    finally:
+        fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 0)
     assert "in-kernel" in desc, desc
 
 
-@pytest.mark.parametrize("merge_launch", [0, 1], ids=["in_kernel", "second_launch"])
+@pytest.mark.parametrize("in_kernel", [1, 0], ids=["in_kernel", "second_launch"])
 @pytest.mark.parametrize("case", [
     dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0"),           # config 4
     dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0"),                  # config 5, 8-rank shard
@@ -542,7 +547,7 @@ def test_bd_in_kernel_merge_graph_replays_new_inputs(dev):
     dict(D=96, NQ=4, H=16, Hkv=4, N=4096, kv_type="q8_0"),
     dict(D=256, NQ=4, H=8, Hkv=2, N=2048, kv_type="f16"),
 ], ids=["cfg4", "cfg5_shard", "tail", "d64", "d96", "d256"])
-def test_split_multirow_merge_forms(dev, merge_launch, case):
+def test_split_multirow_merge_forms(dev, in_kernel, case):
     """Multi-row split tiles over 4+ KV chunks: the partials merge one wave per
     (tile, row), inside the launch (the tile's workgroups wait for each other)
     or in the second launch; both against the oracle at several head dims."""
@@ -550,7 +555,7 @@ def test_split_multirow_merge_forms(dev, merge_launch, case):
     p = make_problem(seed=70 + case["D"], **case)
     ref = p.oracle()
     t = upload(p, dev)
-    fattn.set_option(fattn.OPT_MERGE_LAUNCH, merge_launch)
+    fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, in_kernel)
     fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
     try:
         for chunk in (0, 256):
@@ -561,7 +566,7 @@ def test_split_multirow_merge_forms(dev, merge_launch, case):
             torch.cuda.synchronize()
             assert attn_rel_err(t["dst"].cpu().numpy(), ref) <= RTOL, desc
     finally:
-        fattn.set_option(fattn.OPT_MERGE_LAUNCH, 0)
+        fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 0)
         fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
 
 
@@ -570,8 +575,10 @@ def test_split_in_kernel_merge_graph_replays_new_inputs(dev):
     captured launch over changing inputs: the waiting workgroups see each
     replay's own count / generation."""
     fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
+    fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 1)
     try:
         desc = _replay_new_inputs(dev, dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0"), n_iter=9)
     finally:
         fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
+        fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 0)
     assert "in-kernel" in desc, desc
