@@ -481,8 +481,9 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
     with torch.cuda.stream(gs):
         graph.replay()   # untimed warm replay
     torch.cuda.synchronize()
+    last = (K - 1) % R  # the output buffer of the last timed step
     if world > 1:
-        _gather(outs, mode)  # warm the communicator
+        _gather(outs[last], mode)  # warm the communicator
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = evs[0], evs[1]
@@ -493,7 +494,9 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
     hip.hipEventRecord(ev1, gs.cuda_stream)
     if world > 1:
         with torch.cuda.stream(gs):
-            full = _gather(outs, mode)  # the single RCCL gather over xGMI (head: + permute to [R][1][NQ][H][D])
+            # the single RCCL gather over xGMI of the last step's outputs (head:
+            # + permute to [1][NQ][H][D]; batch: [world][1][NQ][H][D])
+            full = _gather(outs[last], mode)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -505,20 +508,20 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
 
     res = {"kernel": kname, "kernel_ms_avg": kern_ms_avg, "kernel_ms_median": kern_ms_median, "elapsed": elapsed}
     if args.dump_out and (rank == 0 or mode == "batch"):
-        # rotation 0's inputs and the (gathered) output, for the multi-rank
-        # parity test (tests/test_rehearsal.py checks them against the oracle);
-        # batch mode: every rank its own inputs (<dump>.rank<r>.npz), rank 0
-        # the gathered outputs of all ranks
+        # the last step's inputs (rotation `last`) and the (gathered) output,
+        # for the multi-rank parity test (tests/test_rehearsal.py checks them
+        # against the oracle); batch mode: every rank its own inputs
+        # (<dump>.rank<r>.npz), rank 0 the gathered outputs of all ranks
         if mode == "head":
-            out0 = (full[0] if world > 1 else outs[0]).cpu().numpy()
+            out0 = (full if world > 1 else outs[last]).cpu().numpy()
         else:
-            out0 = (full[:, 0] if world > 1 else outs[0][None]).cpu().numpy()
+            out0 = (full if world > 1 else outs[last][None]).cpu().numpy()
         path = args.dump_out if rank == 0 else args.dump_out + f".rank{rank}.npz"
-        np.savez(path, q=q.cpu().numpy(), k=kv_sets[0][0].cpu().numpy(), v=kv_sets[0][1].cpu().numpy(),
-                 mask=masks[0].cpu().view(torch.int16).numpy().view(np.uint16), out=out0,
+        np.savez(path, q=q.cpu().numpy(), k=kv_sets[last][0].cpu().numpy(), v=kv_sets[last][1].cpu().numpy(),
+                 mask=masks[last].cpu().view(torch.int16).numpy().view(np.uint16), out=out0,
                  shape=np.array([D, NQ, H, Hkv, N, typ, world]), kernel=np.array(kname), mode=np.array(mode))
     if world > 1:
-        assert tuple(full.shape) == ((R, 1, NQ, H, D) if mode == "head" else (world, R, 1, NQ, H, D))
+        assert tuple(full.shape) == ((1, NQ, H, D) if mode == "head" else (world, 1, NQ, H, D))
         # 3) per-step cost of the gather, and kernel + gather per step (eager),
         #    reported apart from the kernel (BASELINE.md multi-GPU rule)
         one = outs[0]
@@ -665,7 +668,8 @@ def main():
                 line["rehearsal"] = "FATTN_BENCH_REHEARSE: all ranks on one GPU, gloo, not a measurement"
             line["per_rank"] = {"heads": sh.n_heads, "kv_heads": sh.n_kv, "bytes": res["rank_bytes"],
                                 "sequences": 1 if mode == "batch" else f"1/{world} of the heads"}
-            line["gather"] = {"collective": "all_gather_into_tensor (RCCL over xGMI), once after the K steps",
+            line["gather"] = {"collective": "all_gather_into_tensor (RCCL over xGMI) of the last step's outputs, "
+                                            "once after the K steps, inside the timed region",
                               "per_step_gather_ms_median": round(res["gather_ms_median"], 4),
                               "per_step_kernel_plus_gather_ms_median": round(res["step_with_gather_ms_median"], 4)}
             if hs5 is not None:

@@ -58,7 +58,7 @@ def test_bench_rehearsal_batch_shard_matches_oracle(tmp_path):
     assert line["config"]["bytes_per_step"] == 2 * 35692544  # two config-3 sequences
     d0 = np.load(out)
     d1 = np.load(str(out) + ".rank1.npz")
-    got = d0["out"]  # [world][1][NQ][H][D]
+    got = d0["out"]  # [world][1][NQ][H][D]: the last step's outputs of every rank
     assert got.shape[0] == 2
     for w, d in enumerate((d0, d1)):
         D, NQ, H, Hkv, N, typ, world = (int(x) for x in d["shape"])
