@@ -898,7 +898,14 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
     last = __builtin_amdgcn_readfirstlane(last);
     FATTN_STAMP(14);
     if (!last) return;
-    merge_row_parts<D>(a.ws_o + tile * a.n_chunks * D, a.ws_ml + 2 * tile * a.n_chunks, a.n_chunks, out, lane);
+    // as few load slots per lane as the chunk count needs (a slot past it is
+    // still an issued instruction; config 3: 8 chunks = 4 slots)
+    const float* po_all = a.ws_o + tile * a.n_chunks * D;
+    const float* pml_all = a.ws_ml + 2 * tile * a.n_chunks;
+    const int need = (a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
+    if (need <= 4) merge_row_parts<D, 4>(po_all, pml_all, a.n_chunks, out, lane);
+    else if (need <= 8) merge_row_parts<D, 8>(po_all, pml_all, a.n_chunks, out, lane);
+    else merge_row_parts<D>(po_all, pml_all, a.n_chunks, out, lane);
     FATTN_STAMP(13);
 }
 
