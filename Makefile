@@ -13,9 +13,9 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-functi
 CSRC := $(wildcard $(PKG)/csrc/*.hip)
 CHDR := $(wildcard $(PKG)/csrc/*.h) include/fattn.h
 
-.PHONY: all lib harness oracle clean asm stamps tests-hip probe
+.PHONY: all lib harness oracle clean asm stamps tests-hip probe isa
 
-all: lib harness oracle tests-hip probe
+all: lib harness oracle tests-hip probe isa
 
 lib: $(LIB)
 
@@ -57,6 +57,18 @@ probe: $(PROBE)
 $(PROBE): tools/hbm_copy.hip
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared $< -o $@
+
+# The -save-temps ISA of every translation unit of libfattn.so, same flags as
+# the library (tools/isa_hazard_check.py audits it and checks that it equals
+# the shipped code objects; tests/test_isa_hazards.py)
+ISADIR := build/isa
+ISAS := $(patsubst $(PKG)/csrc/%.hip,$(ISADIR)/%.s,$(CSRC))
+isa: $(ISAS)
+$(ISADIR)/%.s: $(PKG)/csrc/%.hip $(CHDR)
+	@mkdir -p $(ISADIR)/$*.tmp
+	cd $(ISADIR)/$*.tmp && $(HIPCC) $(subst -Iinclude,-I$(CURDIR)/include,$(HIPFLAGS)) -c $(CURDIR)/$< -save-temps -o $*.o
+	mv $(ISADIR)/$*.tmp/$*-hip-amdgcn-amd-amdhsa-$(ARCH).s $@
+	rm -rf $(ISADIR)/$*.tmp
 
 # ISA dump for inspection (not part of the build): make asm ASMSRC=fattn_launch_d128
 ASMSRC ?= fattn_launch_d128

@@ -10,20 +10,19 @@ different one of R independent KV caches (R * 35.7 MB > the 256 MiB Infinity
 Cache), so the number is HBM, not cache.
 
 N GPUs (`--gpus N`, or launched by torch.distributed.run): heads x batch
-sharding.  The value line is WEAK scaling: every rank decodes
-its own sequence of an N-sequence batch -- the config-3 problem above, its own
-KV caches, the unchanged single-GPU kernel, no collective on the data path --
-and after the K timed steps the ranks' outputs meet in ONE RCCL all_gather
-over xGMI (inside the timed region); value = N x the per-sequence bytes / the
-slowest rank's wall time, so value(N) / (N value(1)) is the scaling
-efficiency.  Beside it (`head_shard_config5`, strong scaling): BASELINE.json
-configs[4] -- n_q = 64 query rows, 32 heads, N = 4096, Q8_0 -- as one problem
-head-sharded over the ranks (rank r owns kv heads [r*Hkv/N, (r+1)*Hkv/N) and
-their q heads, zero-copy slices, fattn.shard), gathered and permuted into the
-ggml dst layout (`--multi head` makes that the value line).  Both report the
-per-step gather and kernel + gather per step apart from the kernel
-(BASELINE.md).  `--gpus N` with no launcher starts N child ranks itself
-(before touching the GPU).
+sharding.  The value line is BASELINE.json configs[4] --
+n_q = 64 query rows, 32 heads, N = 4096, Q8_0 -- as ONE problem head-sharded
+over the ranks (strong scaling; rank r owns kv heads [r*Hkv/N, (r+1)*Hkv/N)
+and their q heads, zero-copy slices, fattn.shard): every timed step is the
+rank's FLASH_ATTN_EXT followed by the RCCL all_gather over xGMI of that step's
+output and its permute into the ggml dst layout, K gathers inside the timed
+region.  value = the config-5 bytes x K / the slowest rank's wall time.  The
+N = 1 line carries `strong_scaling_ref` (config 5 on one GPU) as the
+denominator.  Beside the value line: `kernel_only` (the same launches with no
+gather, graph-replayed: SURVEY's "near-linear applies to the kernel part") and
+`weak_scaling_config3` (every rank decodes its own config-3 sequence, one
+gather per step; `--multi batch` makes that the value line).  `--gpus N` with
+no launcher starts N child ranks itself (before touching the GPU).
 
 Prints ONE JSON line (rank 0).  `value` = whole-job algorithmic bytes / wall
 time (GB/s); `roofline` prices the dominant kernel from HIP events on its
@@ -281,11 +280,12 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="auto", choices=["auto", "config3", "config5"],
                     help="auto: config3 (on every rank with --multi batch), config5 with --multi head")
-    ap.add_argument("--multi", default="batch", choices=["batch", "head"],
-                    help="N > 1: batch = every rank decodes its own sequence (weak scaling, the value line); "
-                         "head = one problem head-sharded over the ranks (strong scaling)")
-    ap.add_argument("--no-head-shard", action="store_true",
-                    help="N > 1, --multi batch: skip the config-5 head-shard (strong-scaling) measurement")
+    ap.add_argument("--multi", default="head", choices=["batch", "head"],
+                    help="N > 1: head = BASELINE config 5 as one problem head-sharded over the ranks, one gather "
+                         "per step (strong scaling, the value line); batch = every rank decodes its own config-3 "
+                         "sequence (weak scaling)")
+    ap.add_argument("--no-side-line", action="store_true",
+                    help="N > 1: skip the other mode's measurement reported beside the value line")
     ap.add_argument("--rotate", type=int, default=0,
                     help="independent KV caches cycled through (0 = enough that one pass reads >= 512 MiB per rank)")
     ap.add_argument("--kv-type", default=None, choices=["q8_0", "q4_0", "f16"])
@@ -462,11 +462,10 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
         kms.append(f.value)
     kern_ms_median = statistics.median(kms)
 
-    # 2) the timed job: the K steps (step i reads KV cache i % R) captured
-    #    back-to-back into one HIP graph and replayed once inside the timed
-    #    region; at world > 1 the ranks' outputs then meet in ONE all_gather.
-    #    HIP events around the replay on the launch stream give the kernel's
-    #    average in-stream duration over the timed region.
+    # 2) the kernel alone: the K steps (step i reads KV cache i % R) captured
+    #    back-to-back into one HIP graph and replayed; HIP events around the
+    #    replay on the launch stream give the kernel's average in-stream
+    #    duration.  At world 1 this replay IS the timed job (no collective).
     K = args.steps
     gs = torch.cuda.Stream(dev)
     gs.wait_stream(torch.cuda.current_stream(dev))
@@ -492,21 +491,32 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
     with torch.cuda.stream(gs):
         graph.replay()
     hip.hipEventRecord(ev1, gs.cuda_stream)
-    if world > 1:
-        with torch.cuda.stream(gs):
-            # the single RCCL gather over xGMI of the last step's outputs (head:
-            # + permute to [1][NQ][H][D]; batch: [world][1][NQ][H][D])
-            full = _gather(outs[last], mode)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     hip.hipEventSynchronize(ev1)
     hip.hipEventElapsedTime(C.byref(f), ev0, ev1)
     kern_ms_avg = f.value / K
+    kernel_only_elapsed = elapsed
+    if world > 1:
+        # 3) the timed job at world > 1: every step is one FLASH_ATTN_EXT on the
+        #    rank's slice followed by the RCCL gather over xGMI of THAT step's
+        #    output (head: + the permute into [1][NQ][H][D]; batch: stacked
+        #    [world][1][NQ][H][D]) -- a decode layer cannot start its next
+        #    step before the gathered output exists.  K gathers are timed.
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(gs):
+            for i in range(K):
+                step(i, gs.cuda_stream)
+                full = _gather(outs[i % R], mode)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
 
-    res = {"kernel": kname, "kernel_ms_avg": kern_ms_avg, "kernel_ms_median": kern_ms_median, "elapsed": elapsed}
+    res = {"kernel": kname, "kernel_ms_avg": kern_ms_avg, "kernel_ms_median": kern_ms_median, "elapsed": elapsed,
+           "kernel_only_elapsed": kernel_only_elapsed}
     if args.dump_out and (rank == 0 or mode == "batch"):
         # the last step's inputs (rotation `last`) and the (gathered) output,
         # for the multi-rank parity test (tests/test_rehearsal.py checks them
@@ -544,11 +554,11 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
         res["gather_ms_median"] = statistics.median(gts[5:]) * 1e3
         res["step_with_gather_ms_median"] = statistics.median(ets[5:]) * 1e3
         t = torch.tensor([elapsed, kern_ms_avg, kern_ms_median, res["gather_ms_median"],
-                          res["step_with_gather_ms_median"]], dtype=torch.float64,
+                          res["step_with_gather_ms_median"], kernel_only_elapsed], dtype=torch.float64,
                          device="cpu" if REHEARSE else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         (res["elapsed"], res["kernel_ms_avg"], res["kernel_ms_median"], res["gather_ms_median"],
-         res["step_with_gather_ms_median"]) = (float(x) for x in t.tolist())
+         res["step_with_gather_ms_median"], res["kernel_only_elapsed"]) = (float(x) for x in t.tolist())
     for e in evs:
         hip.hipEventDestroy(e)
 
@@ -623,11 +633,14 @@ def main():
     workload = args.workload if args.workload != "auto" else ("config5" if mode == "head" and world > 1 else "config3")
     shape = shape_of(args, workload)
     res = run_decode(args, dev, shape, rank, world, mode)
-    hs5 = None
-    if world > 1 and mode == "batch" and not args.no_head_shard:
-        # BASELINE config 5 head-sharded over the same ranks (strong scaling), beside the line
-        hs5 = run_decode(args, dev, shape_of(argparse.Namespace(**{k: None for k in WORKLOADS["config5"]}),
-                                             "config5"), rank, world, "head")
+    side = None
+    if world > 1 and not args.no_side_line:
+        # the other multi-GPU reading beside the value line: head mode (the line)
+        # -> the weak-scaling batch of config-3 sequences; batch -> the config-5 head shard
+        other = "batch" if mode == "head" else "head"
+        wl = "config3" if other == "batch" else "config5"
+        side = run_decode(args, dev, shape_of(argparse.Namespace(**{k: None for k in WORKLOADS[wl]}), wl),
+                          rank, world, other)
 
     if rank == 0:
         traffic = committed_traffic(res["workload"], res["kernel"]) if world == 1 else None
@@ -668,22 +681,36 @@ def main():
                 line["rehearsal"] = "FATTN_BENCH_REHEARSE: all ranks on one GPU, gloo, not a measurement"
             line["per_rank"] = {"heads": sh.n_heads, "kv_heads": sh.n_kv, "bytes": res["rank_bytes"],
                                 "sequences": 1 if mode == "batch" else f"1/{world} of the heads"}
-            line["gather"] = {"collective": "all_gather_into_tensor (RCCL over xGMI) of the last step's outputs, "
-                                            "once after the K steps, inside the timed region",
+            line["gather"] = {"collective": "all_gather_into_tensor (RCCL over xGMI) of every step's output"
+                                            + (" + permute into the ggml dst layout" if mode == "head" else "")
+                                            + ", K gathers inside the timed region (eager: kernel, gather, ...)",
+                              "gathers_timed": K,
                               "per_step_gather_ms_median": round(res["gather_ms_median"], 4),
                               "per_step_kernel_plus_gather_ms_median": round(res["step_with_gather_ms_median"], 4)}
-            if hs5 is not None:
-                sh5 = hs5["shard"]
-                line["head_shard_config5"] = {
-                    "workload": hs5["workload"], "scaling": "strong",
-                    "parallelism": f"head_shard_{sh5.n_heads}heads_per_rank_x{world}",
-                    "value": round(hs5["job_bytes"] * K / hs5["elapsed"] / 1e9, 2), "unit": "GB/s",
-                    "ms_per_step": round(hs5["elapsed"] / K * 1e3, 5),
-                    "kernel_ms_avg": round(hs5["kernel_ms_avg"], 5), "kernel": hs5["kernel"],
-                    "per_step_gather_ms_median": round(hs5["gather_ms_median"], 4),
-                    "per_step_kernel_plus_gather_ms_median": round(hs5["step_with_gather_ms_median"], 4),
-                    "note": "one config-5 problem (n_q 64) sliced by kv heads over the ranks; strong-scaling "
-                            "efficiency = value / (N * the N=1 line's strong_scaling_ref value)"}
+            # kernel-only scaling ("near-linear" applies to the kernel
+            # part): the same K launches as one graph replay, no collective
+            line["kernel_only"] = {
+                "value": round(res["job_bytes"] * K / res["kernel_only_elapsed"] / 1e9, 2), "unit": "GB/s",
+                "ms_per_step": round(res["kernel_only_elapsed"] / K * 1e3, 5),
+                "timing": "the K launches captured in one HIP graph, replayed, wall clock max over ranks; "
+                          "no gather"}
+            if side is not None:
+                shs = side["shard"]
+                key = "weak_scaling_config3" if side["mode"] == "batch" else "head_shard_config5"
+                line[key] = {
+                    "workload": side["workload"], "scaling": "weak" if side["mode"] == "batch" else "strong",
+                    "parallelism": (f"batch_shard_1seq_per_rank_x{world}" if side["mode"] == "batch" else
+                                    f"head_shard_{shs.n_heads}heads_per_rank_x{world}"),
+                    "value": round(side["job_bytes"] * K / side["elapsed"] / 1e9, 2), "unit": "GB/s",
+                    "ms_per_step": round(side["elapsed"] / K * 1e3, 5),
+                    "kernel_only_value": round(side["job_bytes"] * K / side["kernel_only_elapsed"] / 1e9, 2),
+                    "kernel_ms_avg": round(side["kernel_ms_avg"], 5), "kernel": side["kernel"],
+                    "per_step_gather_ms_median": round(side["gather_ms_median"], 4),
+                    "per_step_kernel_plus_gather_ms_median": round(side["step_with_gather_ms_median"], 4),
+                    "note": ("every rank decodes its own config-3 sequence (the N=1 line's workload), one gather of "
+                             "the ranks' outputs per step; weak-scaling efficiency = value / (N * the N=1 value)"
+                             if side["mode"] == "batch" else
+                             "one config-5 problem (n_q 64) sliced by kv heads over the ranks, one gather per step")}
         if world > 1:
             print(json.dumps(line), flush=True)
 

@@ -52,6 +52,7 @@ std::atomic<int> g_opt_pf{0};  // 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_pf_stagger{2};
 constexpr int kMqMinRowsDefault = 64;
 std::atomic<int> g_opt_mq_min_rows{kMqMinRowsDefault};  // multi-query kernel from this many packed rows per kv head (>= 32)
+std::atomic<int> g_opt_mq_min_rows_set{0};  // 1: FATTN_OPT_MQ_MIN_ROWS was given explicitly (bypasses the `wide` gate)
 std::atomic<int> g_opt_pf_no_skip{0};     // 1: masked prefill without the live-block pre-pass (FATTN_OPT_PF_SKIP)
 std::atomic<int> g_opt_split_prio{0};     // split kernel wave priorities (FATTN_OPT_SPLIT_PRIO)
 std::atomic<int> g_opt_no_wave_merge{0};  // 1: one-row split tiles merge through LDS + combine_tile as other tiles
@@ -287,6 +288,9 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     a.chunk_len = (int)(tpc * kStep);
     a.n_chunks = (int)nch;
     a.merge_launch = (nch > 1 && !fused) ? 1 : 0;
+    // the merge launch's grid.y is Y x the 16-row subtiles per tile: refuse a
+    // plan whose merge could not launch (nothing is launched on an error)
+    if (a.merge_launch && Y * (pl.nw == 8 ? 16 : 4) > 65535) return FATTN_ERR_INVALID_ARG;
     a.ncp = 1;
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     a.nbuf = 0;
@@ -383,6 +387,8 @@ int make_plan(const fattn_params* p, Plan& pl) {
         if (v.nb[1] != 2) return FATTN_ERR_BAD_STRIDE;
         v_trans = true;
         if (N % kStep || v.nb[0] % 16 || (uintptr_t)v.data % 16) return FATTN_ERR_BAD_STRIDE;
+        // the transposed-V kernels exist for f16 K only (flash_row_float.h's layout)
+        if (k.type != FATTN_TYPE_F16) return FATTN_ERR_UNSUPPORTED_TYPE;
     }
     if (is_quant(v.type) && v.nb[0] != (int64_t)fattn_row_size(v.type, 32)) return FATTN_ERR_BAD_STRIDE;
     if (k.nb[1] % 2 || k.nb[2] % 4 || k.nb[3] % 4 || (uintptr_t)k.data % 4) return FATTN_ERR_ALIGNMENT;
@@ -468,7 +474,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     const int64_t y64 = Hkv * ((NQ + qpt64 - 1) / qpt64);
     const bool wide = N * y64 * S >= (int64_t)2 * kBdKeys * pl.cus;
     pl.mq = mq_ok && NQ * a.rk2 >= g_opt_mq_min_rows &&
-            (wide || NQ * a.rk2 >= 256 || g_opt_mq_min_rows != kMqMinRowsDefault);  // (an explicit threshold wins)
+            (wide || NQ * a.rk2 >= 256 || g_opt_mq_min_rows_set);  // (an explicit threshold wins)
     if (pl.mq) {
         // 256 rows per workgroup once that still gives one workgroup per CU
         const int64_t wg256 = Hkv * S * ((NQ * a.rk2 + 255) / 256);
@@ -590,6 +596,7 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_MQ_MIN_ROWS:
             if (value != 0 && value < 32) return FATTN_ERR_INVALID_ARG;
             g_opt_mq_min_rows = value ? value : kMqMinRowsDefault;
+            g_opt_mq_min_rows_set = value ? 1 : 0;
             return FATTN_OK;
         case FATTN_OPT_PF_SKIP:
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;

@@ -178,11 +178,10 @@ __device__ __forceinline__ float wave_sum(float x) {
 
 // ---------------------------------------------------------------- sc1 memory ops
 // Write-through stores / L1-bypassing loads for data handed between workgroups
-// of one launch (MI355X_MICROARCH.md, inter-workgroup visibility).  Issued as
-// inline asm, so the compiler does not track them: callers drain with an
-// explicit s_waitcnt vmcnt(0) and pass every loaded value through reg_fence()
-// after that wait, so no use can be scheduled above it.
-// The trailing s_nop covers the VMEM-store-data hazard (a store of more than 8
+// of one launch (MI355X_MICROARCH.md, inter-workgroup visibility).
+// Stores: inline asm with no destination register (nothing for the compiler
+// to misplace); callers drain them with an explicit s_waitcnt vmcnt(0).  The
+// trailing s_nop covers the VMEM-store-data hazard (a store of more than 8
 // bytes must not have its data VGPRs overwritten by the next VALU instruction):
 // hipcc's hazard recognizer does not see inside inline asm, and with the
 // multi-query kernel's register pressure it reused the data registers of one
@@ -193,30 +192,28 @@ __device__ __forceinline__ void st_sc1(void* p, u32x4 v) {
 __device__ __forceinline__ void st_sc1_x2(void* p, u32x2 v) {
     asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
-// Integer vector operands only: with a float-vector "+v"/"=v" operand hipcc
-// (ROCm 7.2) mis-assigned the elements of the result (a bit_cast of .y read
-// the register of .x), caught by the chunk-merge stress test.
-__device__ __forceinline__ u32x4 ld_sc1(const void* p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
+// Loads of handed-off words: compiler-tracked (relaxed agent-scope atomic
+// loads lower to global_load_dword(x2) ... sc1), so hipcc places every wait
+// itself -- no register is live before its data has landed.
 __device__ __forceinline__ u32x2 ld_sc1_x2(const void* p) {
-    u32x2 v;
-    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-    return v;
+    const uint64_t x = __hip_atomic_load((const uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return u32x2{(uint32_t)x, (uint32_t)(x >> 32)};
 }
 __device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
-    uint32_t v;
-    asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-    return v;
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// keeps uses of an asm-loaded value below the preceding explicit wait
-// (integer scalars / vectors only, see ld_sc1)
-template <typename T>
+// Keeps uses of a value loaded by an UNTRACKED inline-asm load below the
+// explicit wait that retires it (the split kernel's Q and mask-word prefetch,
+// the only such loads left; tools/isa_hazard_check.py audits the ISA).
+// Integer scalars / vectors only: with a float-vector "+v"/"=v" operand hipcc
+// (ROCm 7.2) mis-assigned the elements (a bit_cast of .y read .x's register).
+// The comment "RETIRED(tag) <registers>" marks, for tools/isa_hazard_check.py,
+// the point from which the loads of `tag` have landed (the caller's wait sits
+// just before it; volatile asm statements keep their source order).
+template <int TAG, typename T>
 __device__ __forceinline__ void reg_fence(T& v) {
     static_assert(!__is_same(T, f32x4) && !__is_same(T, f32x2), "float vector asm operands are miscompiled");
-    asm volatile("" : "+v"(v));
+    asm volatile("; RETIRED(%1) %0" : "+v"(v) : "n"(TAG));
 }
 
 __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {

@@ -198,12 +198,46 @@ __device__ __forceinline__ i32x4 make_srd(const void* base, uint32_t bytes) {
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(const lds_void*)p; }
 
-// L1-bypassing (sc1) 16-B load through a buffer descriptor; offsets at or past
-// num_records return zeros without memory traffic.  Inline asm like ld_sc1
-// (fattn_common.h): explicit wait + reg_fence before use.
-__device__ __forceinline__ u32x4 ld_sc1_buf(const i32x4& srd, uint32_t off) {
+// Buffer resource for compiler-tracked buffer loads (the hand-off reads of the
+// chunk merges): built from readfirstlane'd inputs, so it is provably
+// wave-uniform and no waterfall loop wraps the loads (cdna_hip_programming.md
+// T20).  Offsets at or past num_records return zeros without memory traffic.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t p = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, (int)n, 0x00020000);
+}
+constexpr int kAuxSc1 = 16;  // buffer-load cache policy: sc1 (L1 bypass; MI355X_MICROARCH.md sc1 table)
+
+// L1-bypassing (sc1) 16-B / 4-B loads of handed-off partials.  Compiler-tracked
+// builtins: hipcc inserts the waits and never reads a register before its data
+// landed (round 3's asm forms had three such miscompiles).
+__device__ __forceinline__ u32x4 ld_sc1_buf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSc1));
+}
+__device__ __forceinline__ uint32_t ld_sc1_buf_b32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kAuxSc1);
+}
+
+// 16-B load into registers through a buffer descriptor, as asm: UNTRACKED --
+// hipcc inserts no wait for it, so waiting for it leaves the LDS-DMA issued
+// after it in flight (a tracked load would make hipcc drain every DMA with
+// vmcnt(0) at its first use, cdna_hip_programming.md §5 trap (b)).  The caller
+// retires it with a counted wait and then passes every result through
+// reg_fence<TAG>() before any use.  The asm comments "UNTRACKED(tag)" on the
+// load and "RETIRED(tag)" on the fence let tools/isa_hazard_check.py prove on
+// the ISA that no instruction touches the destination registers between the
+// load and its fence on any path (tests/test_isa_hazards.py).
+enum : int { kTagQ = 1, kTagMaskWords = 2 };  // bit masks
+template <int TAG>
+__device__ __forceinline__ u32x4 ld_buf_untracked(const i32x4& srd, uint32_t off) {
     u32x4 v;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(srd) : "memory");
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen ; UNTRACKED(%3)"
+                 : "=v"(v)
+                 : "v"(off), "s"(srd), "i"(TAG)
+                 : "memory");
     return v;
 }
 
@@ -217,22 +251,6 @@ __device__ __forceinline__ u32x4 ld_sc1_buf(const i32x4& srd, uint32_t off) {
 // consumer waits with an explicit vmcnt.
 // NT: non-temporal policy for bytes one CU reads once (the decode KV stream,
 // MI355X_MICROARCH.md 'nt-weights'); never for tiles other workgroups re-read.
-// (one dword: hipcc mis-tracked the .y half of a u32x2 asm output here --
-// it reused that register as a temporary before the value's last use)
-__device__ __forceinline__ uint32_t ld_sc1_buf_b32(const i32x4& srd, uint32_t off) {
-    uint32_t v;
-    asm volatile("buffer_load_dword %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(srd) : "memory");
-    return v;
-}
-
-// 16-B load through a buffer descriptor, as asm: the compiler inserts no wait
-// for it; the caller retires it with a counted wait and reg_fence
-__device__ __forceinline__ u32x4 ld_buf(const i32x4& srd, uint32_t off) {
-    u32x4 v;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(srd) : "memory");
-    return v;
-}
-
 template <int BYTES, bool NT = false>
 __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds_any, uint32_t off) {
     // wave-uniform by construction; readfirstlane keeps it an SGPR operand even
@@ -334,9 +352,7 @@ __device__ __forceinline__ int tile_arrive_wait(const SplitArgs& a, int64_t tile
         return 1;
     }
     for (uint32_t spins = 0; spins < (1u << 20); spins++) {
-        uint32_t lo = ld_sc1_u32((const uint32_t*)w);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        reg_fence(lo);
+        const uint32_t lo = ld_sc1_u32((const uint32_t*)w);
         if (((lo >> 16) & 0xFFu) != gen || (int)(lo & 0xFFFF) >= n) return 1;
         __builtin_amdgcn_s_sleep(2);
     }
@@ -665,37 +681,26 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     // the descriptor: zeros, no traffic, weight 0); the halves meet by one
     // permlane32 swap.  Every load of a batch is issued before one wait.
     const int h = lane >> 5, d4 = 4 * (lane & 31);
-    const i32x4 osrd = make_srd(a.ws_o + tile * NP * D, (uint32_t)(NP * D * 4));
-    const i32x4 msrd = make_srd(a.ws_ml + 2 * tile * NP, (uint32_t)(NP * 8));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the count)
+    const __amdgpu_buffer_rsrc_t osrd = make_rsrc(a.ws_o + tile * NP * D, (uint32_t)(NP * D * 4));
+    const __amdgpu_buffer_rsrc_t msrd = make_rsrc(a.ws_ml + 2 * tile * NP, (uint32_t)(NP * 8));
     constexpr int kIt = kWaveMergeBatch / 2;  // part pairs per round trip
     u32x4 v[kIt];
     auto issue = [&](int p0) {
 #pragma unroll
         for (int i = 0; i < kIt; i++) v[i] = ld_sc1_buf(osrd, (uint32_t)(((p0 + 2 * i + h) * D + d4) * 4));
     };
-    auto fence = [&] {
-#pragma unroll
-        for (int i = 0; i < kIt; i++) reg_fence(v[i]);
-    };
     issue(0);
-    uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
-    uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8 + 4));  //          l of part p
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
+    const uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8 + 4));  //          l of part p
     FATTN_STAMP(15);
-    reg_fence(mlm);
-    reg_fence(mll);
-    fence();
     const float mp = lane < NP ? __builtin_bit_cast(float, mlm) : kNegInf;
     const float M = seg_reduce<true>(mp, 64);
     const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M);
     const float L = seg_reduce<false>(lane < NP ? w * __builtin_bit_cast(float, mll) : 0.0f, 64);
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int p0 = 0; p0 < NP; p0 += kWaveMergeBatch) {  // wave-uniform
-        if (p0 > 0) {
-            issue(p0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            fence();
-        }
+        if (p0 > 0) issue(p0);
 #pragma unroll
         for (int i = 0; i < kIt; i++) {
             const int wi = __builtin_bit_cast(int, w);
@@ -738,24 +743,17 @@ __device__ __forceinline__ void merge_row_parts(const float* parts_o, const floa
     constexpr int PPR = merge_ppr<D>();     // D = 80 / 96: 1
     const int h = lane / LPP, d4 = 4 * (lane % LPP);
     // (part p's O row at p * ostride floats, its (m, l) at p * mstride)
-    const i32x4 osrd = make_srd(parts_o, (uint32_t)(NP * ostride * 4));
-    const i32x4 msrd = make_srd(parts_ml, (uint32_t)(NP * mstride * 4));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the count)
+    const __amdgpu_buffer_rsrc_t osrd = make_rsrc(parts_o, (uint32_t)(NP * ostride * 4));
+    const __amdgpu_buffer_rsrc_t msrd = make_rsrc(parts_ml, (uint32_t)(NP * mstride * 4));
     u32x4 v[kIt];
     auto issue = [&](int p0) {
 #pragma unroll
         for (int i = 0; i < kIt; i++) v[i] = ld_sc1_buf(osrd, (uint32_t)(((p0 + PPR * i + h) * ostride + d4) * 4));
     };
-    auto fence = [&] {
-#pragma unroll
-        for (int i = 0; i < kIt; i++) reg_fence(v[i]);
-    };
     issue(0);
-    uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * mstride * 4));      // lane p: m of part p
-    uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * mstride * 4 + 4));  //          l of part p
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    reg_fence(mlm);
-    reg_fence(mll);
-    fence();
+    const uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * mstride * 4));      // lane p: m of part p
+    const uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * mstride * 4 + 4));  //          l of part p
     const float mp = lane < NP ? __builtin_bit_cast(float, mlm) : kNegInf;
     const float M = seg_reduce<true>(mp, 64);
     const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M);
@@ -763,11 +761,7 @@ __device__ __forceinline__ void merge_row_parts(const float* parts_o, const floa
     const int wi = __builtin_bit_cast(int, w);
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int p0 = 0; p0 < NP; p0 += kIt * PPR) {  // wave-uniform
-        if (p0 > 0) {
-            issue(p0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            fence();
-        }
+        if (p0 > 0) issue(p0);
 #pragma unroll
         for (int i = 0; i < kIt; i++) {
             float wp = 0.0f;
@@ -1367,8 +1361,8 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
         for (int b = 0; b < NB; b++) {
             // (D = 80: dims past D come from past the descriptor, as zeros)
             const uint32_t qb = (D % QK == 0 || 32 * b + 8 * g < D) ? qoff + 128 * b : a.q_span;
-            qraw[b][0] = ld_buf(qs, qb);
-            qraw[b][1] = ld_buf(qs, qb + 16);
+            qraw[b][0] = ld_buf_untracked<kTagQ>(qs, qb);
+            qraw[b][1] = ld_buf_untracked<kTagQ>(qs, qb + 16);
         }
     }
     // ---- -inf steps (src/flash-llama.h:275-278 skips their compute): a step
@@ -1394,7 +1388,7 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
         const uint32_t moff = r < n_rows ? (uint32_t)(mrow0 + r) * (uint32_t)a.m_nb1 + (uint32_t)(w_lo + st * kStep) * 2
                                          : a.m_span;  // past the descriptor: no traffic
 #pragma unroll
-        for (int j = 0; j < 4; j++) mraw[j] = ld_buf(rs.m, moff + 16 * j);
+        for (int j = 0; j < 4; j++) mraw[j] = ld_buf_untracked<kTagMaskWords>(rs.m, moff + 16 * j);
     }
     for (int s = 0; s < pro; s++) {
         issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + s * kStep, mrow0, wbuf + s * C::stepBytes, lane);
@@ -1408,11 +1402,18 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     FATTN_STAMP(1);
     if (a.split_prio == 2) __builtin_amdgcn_s_setprio(0);
     wait_steps<NI>(pro);  // Q and the mask words landed (the steps issued after them may fly on)
+    // every untracked result, on every path, passes its fence right behind
+    // that wait (nothing reads or moves those registers before it)
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        reg_fence<kTagQ>(qraw[b][0]);
+        reg_fence<kTagQ>(qraw[b][1]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) reg_fence<kTagMaskWords>(mraw[j]);
     f16x8 qop[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) {
-        reg_fence(qraw[b][0]);
-        reg_fence(qraw[b][1]);
         const f32x4 x0 = __builtin_bit_cast(f32x4, qraw[b][0]), x1 = __builtin_bit_cast(f32x4, qraw[b][1]);
         f16x8 h;
         h.s0 = (f16)x0.x; h.s1 = (f16)x0.y; h.s2 = (f16)x0.z; h.s3 = (f16)x0.w;
@@ -1426,7 +1427,6 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
         bool lv = false;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            reg_fence(mraw[j]);
             lv |= (mraw[j].x != kNegInf2) | (mraw[j].y != kNegInf2) | (mraw[j].z != kNegInf2) | (mraw[j].w != kNegInf2);
         }
         const uint64_t bl = __builtin_amdgcn_ballot_w64(lv && lane < n_rows * nsteps);
@@ -1555,7 +1555,8 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
     // load -- an asm load under a branch would leave a register copy (phi)
     // reading the destination before its wait.
     const uint32_t obytes = (uint32_t)(NCH * kRows * D * 4);
-    const i32x4 osrd = make_srd(a.ws_o + sb * kRows * D, obytes);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the count)
+    const __amdgpu_buffer_rsrc_t osrd = make_rsrc(a.ws_o + sb * kRows * D, obytes);
     auto issue = [&](u32x4 (&v)[CB][EPT / 4], int k0) {
 #pragma unroll
         for (int kk = 0; kk < CB; kk++) {
@@ -1566,13 +1567,6 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
             for (int e = 0; e < EPT / 4; e++) v[kk][e] = ld_sc1_buf(osrd, off + 16 * e);
         }
     };
-    auto fence_all = [&](u32x4 (&v)[CB][EPT / 4]) {
-#pragma unroll
-        for (int kk = 0; kk < CB; kk++) {
-#pragma unroll
-            for (int e = 0; e < EPT / 4; e++) reg_fence(v[kk][e]);
-        }
-    };
     u32x4 v[CB][EPT / 4];
     issue(v, 0);
     // (m, l) of chunk c of row r in thread r * NCP + c (NCP = next power of
@@ -1580,10 +1574,7 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
     const int NCP = a.ncp;
     const int mr = threadIdx.x / NCP, mc = threadIdx.x % NCP;
     const bool has_ml = mr < rv && mc < NCH;
-    u32x2 mlb = ld_sc1_x2(a.ws_ml + 2 * ((sb + min(mc, NCH - 1)) * kRows + (has_ml ? mr : 0)));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    reg_fence(mlb);
-    fence_all(v);
+    const u32x2 mlb = ld_sc1_x2(a.ws_ml + 2 * ((sb + min(mc, NCH - 1)) * kRows + (has_ml ? mr : 0)));
     const float mlm = has_ml ? fl(mlb.x) : kNegInf;
     const float Mr = seg_reduce<true>(mlm, NCP);
     const float wt = (mlm == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mlm - Mr);
@@ -1600,11 +1591,7 @@ __device__ __forceinline__ void combine_tile(const SplitArgs& a, int64_t tile, i
 #pragma unroll
         for (int e = 0; e < EPT; e++) s8[e] = 0.0f;
         for (int k0 = 0; k0 < kmax; k0 += CB) {
-            if (k0 > 0) {
-                issue(v, k0);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                fence_all(v);
-            }
+            if (k0 > 0) issue(v, k0);
 #pragma unroll
             for (int kk = 0; kk < CB; kk++) {
                 const int c = cg + (k0 + kk) * G;

@@ -51,6 +51,12 @@ OPT_SPLIT_SKIP = 20
 OPT_SPLIT_MERGE = 21
 OPT_BD = 22
 OPT_MERGE_IN_KERNEL = 24
+# every option's default (include/fattn.h): reset_options() restores them
+OPTION_DEFAULTS = {
+    OPT_MQ_ROWS_PER_WAVE: 0, OPT_MQ_DISABLE: 0, OPT_SPLIT_STEPS: 0, OPT_SPLIT_INFLIGHT: 0, OPT_PF: 0,
+    OPT_PF_STAGGER: 2, OPT_SPLIT_WAVE_MERGE: 0, OPT_SPLIT_PRIO: 0, OPT_PF_SKIP: 0, OPT_MQ_MIN_ROWS: 0,
+    OPT_SPLIT_WAVES: 0, OPT_SPLIT_SKIP: 0, OPT_SPLIT_MERGE: 0, OPT_BD: 0, OPT_MERGE_IN_KERNEL: 0,
+}
 
 
 class FattnError(RuntimeError):
@@ -131,6 +137,35 @@ def set_option(option: int, value: int):
     (0 auto, 16, 32), OPT_MQ_DISABLE (1 = split-KV kernel only), OPT_SPLIT_STEPS
     (32-position steps per wave, 0 auto) or OPT_SPLIT_INFLIGHT (steps in flight, 0 auto)."""
     _check(lib().fattn_set_option(option, value), "fattn_set_option")
+
+
+def reset_options():
+    """Every planner override back to its default (the process-wide state of
+    fattn_set_option; tests reset it after each case so a failing one cannot
+    leak an override into the next)."""
+    for opt, val in OPTION_DEFAULTS.items():
+        set_option(opt, val)
+
+
+class options:
+    """Context manager: set planner overrides for a block, restore the defaults
+    on exit (also when the block raises).  `with fattn.options({OPT_BD: 2}): ...`"""
+
+    def __init__(self, opts: dict):
+        self.opts = dict(opts)
+
+    def __enter__(self):
+        try:
+            for opt, val in self.opts.items():
+                set_option(opt, val)
+        except Exception:
+            reset_options()
+            raise
+        return self
+
+    def __exit__(self, *exc):
+        reset_options()
+        return False
 
 
 def row_size(typ: int, k: int) -> int:

@@ -157,7 +157,9 @@ enum {
                                        first (default; the workspace holds n_qt * N/64 flag bytes),
                                        1 = no pre-pass (every tile fetched; all -inf wave blocks still skipped) */,
     FATTN_OPT_MQ_MIN_ROWS = 13,     /* multi-query kernel only from this many packed (query x head) rows per kv
-                                       head (0 = the default, 64; minimum 32); fewer rows take the split-KV kernel */
+                                       head (0 = the default, 64; minimum 32); fewer rows take the split-KV kernel.
+                                       An explicit value (64 included) also lifts the default's rule that every
+                                       KV chunk hold two 128-key tiles */
     FATTN_OPT_SPLIT_WAVES = 19,     /* split kernel waves per workgroup: 0 = auto, 4, 8 or 16 (16-B row path;
                                        16 needs the Q8_0/Q4_0 register budget, else clamped to 8) */
     FATTN_OPT_SPLIT_SKIP = 20       /* split kernel, masked: 0 = steps whose mask is -inf for every key and row
@@ -174,7 +176,11 @@ enum {
     FATTN_OPT_MERGE_IN_KERNEL = 24  /* chunk partials of multi-row tiles (split kernel with 4+ chunks, batched-
                                        decode kernel): 0 = merged in a second launch (default); 1 = inside the
                                        launch when the whole grid is co-resident -- the tile's workgroups wait
-                                       for each other, then each merges a share of the rows (0.6-1.5 us slower) */
+                                       for each other, then each merges a share of the rows (0.6-1.5 us slower).
+                                       Co-residency is judged from CU count, LDS and launch bounds only: on a
+                                       device shared with other streams or processes (or CU-masked) a waiting
+                                       workgroup's bounded poll can give up, and it then writes NaN rows while
+                                       fattn_ext has returned FATTN_OK.  Diagnostics only; keep 0 in production */
 };
 int fattn_set_option(int option, int value);
 

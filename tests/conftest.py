@@ -28,3 +28,15 @@ def dev():
     if not torch.cuda.is_available():
         pytest.fail("GPU test selected but no GPU visible (torch.cuda.is_available() is False)")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _reset_planner_options():
+    """fattn_set_option state is process-wide: whatever a test sets (and however
+    it ends), the next test starts from the defaults."""
+    yield
+    try:
+        import fattn
+        fattn.reset_options()
+    except Exception:
+        pass  # library not built / not loadable: nothing was set

@@ -1,0 +1,39 @@
+// Test-only probe for tools/isa_hazard_check.py (tests/test_isa_hazards.py):
+// the product's untracked register load (ld_buf_untracked) and fence
+// (reg_fence) used correctly once, and twice with a deliberately injected
+// early touch of the destination registers -- the miscompile class the audit
+// exists to catch.  Compiled to ISA only; never launched.
+#include "../../ggml-cuda-experiments_amd/csrc/fattn_split.h"
+
+using namespace fattn;
+
+// correct: load, wait, fence, use
+__global__ void probe_clean(const uint8_t* p, uint32_t* out, uint32_t bytes) {
+    const i32x4 srd = make_srd(p, bytes);
+    u32x4 v = ld_buf_untracked<kTagQ>(srd, threadIdx.x * 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    reg_fence<kTagQ>(v);
+    out[threadIdx.x] = v.x + v.y + v.z + v.w;
+}
+
+// injected: the value is stored before its wait (a read of a pending register)
+__global__ void probe_early_store(const uint8_t* p, uint32_t* out, uint32_t bytes) {
+    const i32x4 srd = make_srd(p, bytes);
+    u32x4 v = ld_buf_untracked<kTagQ>(srd, threadIdx.x * 16);
+    out[threadIdx.x + 256] = v.y;  // before the wait: stale register contents
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    reg_fence<kTagQ>(v);
+    out[threadIdx.x] = v.x;
+}
+
+// injected: an early register copy, as hipcc made them in round 3, with a
+// counted (not vmcnt(0)) wait -- only the fence retires the load
+__global__ void probe_early_copy(const uint8_t* p, uint32_t* out, uint32_t bytes) {
+    const i32x4 srd = make_srd(p, bytes);
+    u32x4 v = ld_buf_untracked<kTagMaskWords>(srd, threadIdx.x * 16);
+    uint32_t c;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(c) : "v"(v.z));  // the copy, before the wait
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    reg_fence<kTagMaskWords>(v);
+    out[threadIdx.x] = v.x + c;
+}

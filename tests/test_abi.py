@@ -138,6 +138,40 @@ def test_mixed_kv_types_other_head_dims_rejected():
     assert fattn.workspace_size(p) == 0
 
 
+@pytest.mark.parametrize("kt", [fattn.TYPE_Q8_0, fattn.TYPE_Q4_0])
+def test_quant_k_with_transposed_f16_v_rejected(kt):
+    """The transposed-V (flash_row_float.h) kernels exist for f16 K only: the
+    planner refuses the pair instead of planning a launch that cannot run."""
+    D, N, H = 128, 2048, 8
+    p = _params(D=D, N=N, H=H, Hkv=H, kt=kt)
+    # V f16 [Hkv][D][N]: nb0 = N * 2 (along D), nb1 = 2 (along N)
+    vt = fattn.View(1 << 20, fattn.TYPE_F16, (D, N, H, 1), (N * 2, 2, D * N * 2, D * N * 2 * H))
+    p.v = vt.c()
+    assert fattn.workspace_size(p) == 0
+    with pytest.raises(fattn.FattnError) as e:
+        fattn.describe(p)
+    assert e.value.code == -2  # FATTN_ERR_UNSUPPORTED_TYPE
+
+
+def test_mq_min_rows_explicit_default_lifts_the_wide_gate():
+    """An explicit FATTN_OPT_MQ_MIN_ROWS = 64 (the default's value) bypasses the
+    rule that every chunk hold two 128-key tiles, as the header says."""
+    p = _params(NQ=64, H=4, Hkv=4)  # config-5 8-rank shard: the split kernel by default
+    assert fattn.describe(p).startswith("fattn_split_kernel"), fattn.describe(p)
+    with fattn.options({fattn.OPT_MQ_MIN_ROWS: 64, fattn.OPT_BD: 1}):
+        d = fattn.describe(p)
+    assert d.startswith("fattn_mq_kernel"), d
+    assert fattn.describe(p).startswith("fattn_split_kernel")  # restored
+
+
+def test_mq_merge_launch_grid_limit():
+    """A forced small KV chunk with many 64-row query tiles: the merge launch's
+    grid.y (tiles x 4 subtiles) would pass 65535 -- refused at planning."""
+    p = _params(NQ=64 * 20000, H=1, Hkv=1, N=1024, kv_chunk=256)
+    with fattn.options({fattn.OPT_PF: 1, fattn.OPT_BD: 1}):
+        assert fattn.workspace_size(p) == 0
+
+
 def test_single_chunk_needs_no_workspace():
     assert fattn.workspace_size(_params(N=128)) == 0
 

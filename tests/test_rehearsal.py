@@ -5,8 +5,9 @@ otherwise: rank spawn, the unchanged kernel per rank, the gather).  Two modes:
 --multi head (one config-5 problem, n_q 64, 32 heads, N 4096, Q8_0, sliced by
 kv heads into zero-copy views, gathered and permuted into the ggml dst layout:
 rank 0 dumps rotation 0's inputs and the gathered output) and --multi batch
-(the default value line: every rank decodes its own config-3 sequence; every
-rank dumps its inputs, rank 0 the gathered outputs).  Each output is checked
+(every rank decodes its own config-3 sequence; every rank dumps its inputs,
+rank 0 the gathered outputs).  --multi head is the default value line at N > 1
+(BASELINE configs[4]), with one gather per timed step.  Each output is checked
 against the CPU oracle at full size -- SURVEY.md §8(e): sharding must
 reproduce the one-GPU result."""
 import json
@@ -23,7 +24,6 @@ from problems import attn_rel_err
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.gpu
 def _oracle_of(d):
     D, NQ, H, Hkv, N, typ, world = (int(x) for x in d["shape"])
     rb = D // 32 * orc.BLOCK_BYTES[typ]
@@ -41,7 +41,7 @@ def _rehearse(tmp_path, mode):
     out = tmp_path / "rank0.npz"
     env = dict(os.environ, FATTN_BENCH_REHEARSE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "4", "--warmup", "2", "--rotate", "2",
-           "--multi", mode, "--no-head-shard", "--dump-out", str(out)]
+           "--no-side-line", "--dump-out", str(out)] + (["--multi", mode] if mode else [])
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -56,6 +56,7 @@ def test_bench_rehearsal_batch_shard_matches_oracle(tmp_path):
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["config"]["parallelism"] == "batch_shard_1seq_per_rank_x2"
     assert line["config"]["bytes_per_step"] == 2 * 35692544  # two config-3 sequences
+    assert line["gather"]["gathers_timed"] == line["steps"]
     d0 = np.load(out)
     d1 = np.load(str(out) + ".rank1.npz")
     got = d0["out"]  # [world][1][NQ][H][D]: the last step's outputs of every rank
@@ -70,10 +71,13 @@ def test_bench_rehearsal_batch_shard_matches_oracle(tmp_path):
 
 @pytest.mark.gpu
 def test_bench_rehearsal_two_ranks_matches_oracle(tmp_path):
-    line, out = _rehearse(tmp_path, "head")
+    line, out = _rehearse(tmp_path, None)  # the default N > 1 value line
     assert line["scaling"] == "strong"
     assert line["n_gpus"] == 2
     assert line["config"]["parallelism"] == "head_shard_16heads_per_rank_x2"
+    assert line["config"]["bytes_per_step"] == 38273024  # BASELINE config 5
+    assert line["gather"]["gathers_timed"] == line["steps"]  # one gather per timed step
+    assert line["kernel_only"]["value"] > 0
     assert "gather" in line and line["gather"]["per_step_gather_ms_median"] > 0
     d = np.load(out)
     D, NQ, H, Hkv, N, typ, world = (int(x) for x in d["shape"])

@@ -1,0 +1,362 @@
+#!/usr/bin/env python3
+"""ISA audit of the untracked inline-asm register loads (round-3 verdict item 7).
+
+hipcc does not model the memory operations inside an `asm volatile` statement:
+the VGPR destination of an asm VMEM load counts as written at `;;#ASMEND`, so
+the compiler may read, copy, spill or reuse that register before the data has
+landed -- silently wrong results.  The product keeps exactly one kind of such
+load (ggml-cuda-experiments_amd/csrc/fattn_split.h `ld_buf_untracked<TAG>`:
+the split kernel's Q and mask-word prefetch, left untracked so that waiting for
+it does not drain the LDS-DMA issued behind it); every other hand-off load is a
+compiler-tracked builtin.  Each untracked load carries the asm comment
+`UNTRACKED(tag)`; the caller waits for it with a counted `s_waitcnt` and then
+passes every result through `reg_fence<TAG>` (fattn_common.h), whose asm
+comment `RETIRED(tag) <registers>` marks the point from which it may be used.
+
+This tool proves, on the compiler's own output (the `-save-temps` ISA of every
+shipped translation unit, `make isa`), that on EVERY control-flow path from an
+untracked load no instruction names any of its destination VGPRs -- as source
+or destination, VALU, copy, spill or address -- before its RETIRED marker (or
+an `s_waitcnt vmcnt(0)`).  The wait itself precedes the fence in the source,
+and volatile asm statements keep their order.
+May-analysis over the CFG of each kernel (labels and s_branch / s_cbranch_*
+edges), union at joins, to a fixpoint.  It also rejects any asm VMEM load with
+a VGPR destination that carries no UNTRACKED tag.
+
+`--same-as LIB.so` additionally checks that the audited ISA is the shipped
+code: every function's instruction sequence (alignment nops aside) equals the
+disassembly of the gfx950 code objects inside the library.
+
+Usage: isa_hazard_check.py [--same-as lib.so] file.s [file.s ...]
+Exit 0 = clean; 1 = hazards (listed); 2 = usage / parse problem.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import re
+import struct
+import subprocess
+import sys
+from collections import defaultdict
+
+VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+VMEM_PREFIX = ("buffer_", "global_", "flat_", "scratch_", "tbuffer_")
+BRANCH_RE = re.compile(r"^s_(c?branch\w*)\s+(\.L\w+|\S+)")
+
+
+def vregs(text: str) -> set[int]:
+    out = set()
+    for m in VREG.finditer(text):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+class Insn:
+    __slots__ = ("line", "mnem", "ops", "comment", "in_asm", "text")
+
+    def __init__(self, line, mnem, ops, comment, in_asm, text):
+        self.line, self.mnem, self.ops, self.comment, self.in_asm, self.text = line, mnem, ops, comment, in_asm, text
+
+
+def parse_functions(path: str):
+    """{function name: (list of ('label', name) | ('insn', Insn))} from a .s file."""
+    funcs = {}
+    cur = None
+    body = None
+    in_asm = False
+    prev_type = None
+    with open(path) as f:
+        for ln, raw in enumerate(f, 1):
+            line = raw.rstrip("\n")
+            st = line.strip()
+            if not st:
+                continue
+            if cur is None:
+                m = re.match(r"^([A-Za-z_][\w.$]*):\s*(;.*)?$", line)
+                if m and not m.group(1).startswith(".") and prev_type == m.group(1):
+                    cur, body = m.group(1), []
+                    in_asm = False
+                    continue
+                mt = re.match(r"^\s*\.type\s+([\w.$]+),@function", line)
+                if mt:
+                    prev_type = mt.group(1)
+                continue
+            if st.startswith(".Lfunc_end"):
+                funcs[cur] = body
+                cur = None
+                prev_type = None
+                continue
+            if st == ";;#ASMSTART":
+                in_asm = True
+                continue
+            if st == ";;#ASMEND":
+                in_asm = False
+                continue
+            if st.startswith(";") or st.startswith("//"):
+                if in_asm and "RETIRED(" in st:  # reg_fence<TAG>'s marker: a pseudo-instruction
+                    body.append(("insn", Insn(ln, "RETIRED", st.split(")", 1)[1], st, True, st)))
+                continue
+            m = re.match(r"^(\.L\w+):", st)
+            if m:
+                body.append(("label", m.group(1)))
+                continue
+            if st.startswith("."):
+                continue  # directives
+            code, _, comment = st.partition(";")
+            code = code.strip()
+            if not code:
+                continue
+            parts = code.split(None, 1)
+            body.append(("insn", Insn(ln, parts[0], parts[1] if len(parts) > 1 else "", comment, in_asm, code)))
+    return funcs
+
+
+def is_vmem(mn: str) -> bool:
+    return mn.startswith(VMEM_PREFIX)
+
+
+def vgpr_dest_load(ins: Insn) -> bool:
+    """A VMEM instruction that writes VGPRs: a load (not LDS-DMA) or a returning atomic."""
+    mn = ins.mnem
+    if not is_vmem(mn):
+        return False
+    if "_load_lds" in mn or re.search(r"\blds\b", ins.ops):
+        return False
+    if "_load" in mn:
+        return True
+    if "_atomic" in mn and re.search(r"\b(sc0|glc)\b", ins.ops):
+        return True
+    return False
+
+
+def dest_and_rest(ins: Insn):
+    """(dest vregs, the other vregs named) of a VGPR-destination VMEM instruction."""
+    first, _, rest = ins.ops.partition(",")
+    return vregs(first), vregs(rest)
+
+
+def build_blocks(body):
+    """Basic blocks: list of (label or None, [Insn]), successor indices."""
+    blocks = []
+    cur_label, cur = None, []
+    for kind, x in body:
+        if kind == "label":
+            if cur or cur_label is not None:
+                blocks.append((cur_label, cur))
+            cur_label, cur = x, []
+        else:
+            cur.append(x)
+            if x.mnem in ("s_endpgm", "s_setpc_b64") or x.mnem.startswith("s_branch") or \
+                    x.mnem.startswith("s_cbranch"):
+                blocks.append((cur_label, cur))
+                cur_label, cur = None, []
+    if cur or cur_label is not None:
+        blocks.append((cur_label, cur))
+    index = {lab: i for i, (lab, _) in enumerate(blocks) if lab is not None}
+    succ = []
+    for i, (_, insns) in enumerate(blocks):
+        s = []
+        last = insns[-1] if insns else None
+        if last is not None and last.mnem in ("s_endpgm", "s_setpc_b64"):
+            pass
+        elif last is not None and (last.mnem.startswith("s_branch") or last.mnem.startswith("s_cbranch")):
+            tgt = last.ops.split()[0].rstrip(",") if last.ops else ""
+            if tgt not in index:
+                raise ValueError(f"branch target {tgt!r} not found (line {last.line})")
+            s.append(index[tgt])
+            if last.mnem.startswith("s_cbranch") and i + 1 < len(blocks):
+                s.append(i + 1)
+        elif i + 1 < len(blocks):
+            s.append(i + 1)
+        succ.append(s)
+    return blocks, succ
+
+
+def transfer(insns, state, report):
+    """Run a block: state = {vreg: (tag, load line)} of pending untracked loads."""
+    st = dict(state)
+    for ins in insns:
+        mn = ins.mnem
+        untracked = ins.in_asm and vgpr_dest_load(ins)
+        if untracked:
+            dst, rest = dest_and_rest(ins)
+            for r in rest & st.keys():
+                report(ins, r, st[r])
+            m = re.search(r"UNTRACKED\((\d+)\)", ins.comment)
+            if not m:
+                report(ins, None, ("untagged asm load", ins.line))
+                tag = -1
+            else:
+                tag = int(m.group(1))
+            for r in dst:
+                st[r] = (tag, ins.line)
+            continue
+        if mn == "RETIRED":
+            mask = int(re.search(r"RETIRED\((\d+)\)", ins.comment).group(1))
+            st = {k: v for k, v in st.items() if not (v[0] > 0 and v[0] & mask)}
+            continue
+        named = vregs(ins.ops)
+        hit = named & st.keys()
+        for r in sorted(hit):
+            report(ins, r, st[r])
+        if mn == "s_waitcnt":
+            m = re.search(r"vmcnt\((\d+)\)", ins.ops)
+            if m and int(m.group(1)) == 0:
+                st.clear()
+        elif mn in ("s_swappc_b64", "s_call_b64"):
+            report(ins, None, ("call inside a kernel with untracked state", ins.line)) if st else None
+    return st
+
+
+def check_function(name, body):
+    blocks, succ = build_blocks(body)
+    n = len(blocks)
+    inp = [None] * n
+    inp[0] = {}
+    findings = {}
+
+    def report(ins, reg, info):
+        key = (ins.line, reg)
+        if key not in findings:
+            findings[key] = (ins, reg, info)
+
+    work = [0]
+    seen_out = [None] * n
+    while work:
+        i = work.pop()
+        out = transfer(blocks[i][1], inp[i], report)
+        if seen_out[i] == out:
+            continue
+        seen_out[i] = out
+        for j in succ[i]:
+            merged = dict(inp[j]) if inp[j] is not None else {}
+            changed = inp[j] is None
+            for r, v in out.items():
+                if r not in merged:
+                    merged[r] = v
+                    changed = True
+            if changed:
+                inp[j] = merged
+                work.append(j)
+    loads = sum(1 for _, b in blocks for ins in b if ins.in_asm and vgpr_dest_load(ins))
+    retires = sum(1 for _, b in blocks for ins in b if ins.mnem == "RETIRED")
+    return list(findings.values()), loads, retires
+
+
+# ------------------------------------------------------------------ shipped-library comparison
+
+def code_objects(lib_path):
+    data = open(lib_path, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    pos, objs = 0, []
+    while True:
+        i = data.find(magic, pos)
+        if i < 0:
+            break
+        ne, = struct.unpack_from("<Q", data, i + 24)
+        off = i + 32
+        for _ in range(ne):
+            o, sz, tl = struct.unpack_from("<QQQ", data, off)
+            off += 24
+            triple = data[off:off + tl].decode()
+            off += tl
+            if "gfx950" in triple and sz:
+                objs.append(data[i + o:i + o + sz])
+        pos = i + 1
+    return objs
+
+
+def disasm_mnemonics(lib_path, tmpdir):
+    """{symbol: [list of mnemonic sequences, one per code object holding it]}"""
+    objdump = "/opt/rocm/llvm/bin/llvm-objdump"
+    out = defaultdict(list)
+    for k, co in enumerate(code_objects(lib_path)):
+        p = os.path.join(tmpdir, f"co{k}.elf")
+        with open(p, "wb") as f:
+            f.write(co)
+        txt = subprocess.run([objdump, "-d", "--mcpu=gfx950", p], capture_output=True, text=True, check=True).stdout
+        cur, seq = None, []
+        for line in txt.splitlines():
+            m = re.match(r"^[0-9a-f]+ <([^>]+)>:$", line)
+            if m:
+                if cur:
+                    out[cur].append(seq)
+                cur, seq = m.group(1), []
+                continue
+            if cur and line.startswith("\t"):
+                mn = line.strip().split(None, 1)[0]
+                if not mn.startswith("."):  # ("..." = objdump skipping zero padding)
+                    seq.append(mn)
+        if cur:
+            out[cur].append(seq)
+    return out
+
+
+def norm(seq):
+    """Mnemonics as both printers agree on them: no alignment nops, no encoding
+    suffix (the disassembler spells v_permlane*_swap_b32 with _e32)."""
+    return [re.sub(r"_e(32|64)$", "", m) for m in seq if m not in ("s_nop", "s_code_end", "RETIRED")]
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("files", nargs="+")
+    ap.add_argument("--same-as", default="", help="shipped library whose code objects the ISA must equal")
+    ap.add_argument("-q", action="store_true")
+    args = ap.parse_args(argv)
+    bad = 0
+    total_loads = total_ret = nfunc = 0
+    asm_seqs = {}
+    for path in args.files:
+        try:
+            funcs = parse_functions(path)
+        except Exception as e:  # noqa: BLE001
+            print(f"{path}: parse error: {e}", file=sys.stderr)
+            return 2
+        for name, body in funcs.items():
+            nfunc += 1
+            asm_seqs.setdefault(name, []).append(norm([x.mnem for k, x in body if k == "insn"]))
+            try:
+                findings, loads, rets = check_function(name, body)
+            except ValueError as e:
+                print(f"{path}: {name}: {e}", file=sys.stderr)
+                return 2
+            total_loads += loads
+            total_ret += rets
+            for ins, reg, info in findings:
+                bad += 1
+                what = f"v{reg}" if reg is not None else info[0]
+                print(f"HAZARD {os.path.basename(path)}:{ins.line} {name}: `{ins.text}` touches {what} "
+                      f"(untracked load at line {info[1]}, tag {info[0]})")
+    if not args.q:
+        print(f"audited {nfunc} functions in {len(args.files)} files: {total_loads} untracked asm register loads, "
+              f"{total_ret} retiring waits, {bad} hazards")
+    if args.same_as:
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            dis = disasm_mnemonics(args.same_as, td)
+        mism = 0
+        for name, seqs in asm_seqs.items():
+            if name not in dis:
+                print(f"MISMATCH {name}: in the ISA files, not in {args.same_as}")
+                mism += 1
+                continue
+            def same(d, s):  # (zero padding after a function decodes as v_cndmask_b32)
+                d = norm(d)
+                return d[:len(s)] == s and all(x == "v_cndmask_b32" for x in d[len(s):])
+            for s in seqs:
+                if not any(same(d, s) for d in dis[name]):
+                    print(f"MISMATCH {name}: instruction sequence differs from the shipped code object")
+                    mism += 1
+        if not args.q:
+            print(f"compared {len(asm_seqs)} functions with {args.same_as}: {mism} mismatches")
+        bad += mism
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
