@@ -267,10 +267,18 @@ def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5):
     pairs = NQ * (NQ + 1) // 2 if causal else NQ * N
     flops = 4 * pairs * D * H
     tf = flops / (ms * 1e-3) / 1e12
-    return {"workload": f"prefill_{kvn}_h{H}_d{D}_n{N}_q{NQ}_{mask_kind}_mask",
-            "kernel": att.describe(), "kernel_ms_avg": round(ms, 5), "flops_per_step": flops,
+    # algorithmic bytes: Q + K + V + mask + O at stored precision, once each
+    alg_bytes = 2 * NQ * H * D * 4 + 2 * H * N * fattn.row_size(typ, D) + (0 if mask_kind == "none" else NQ * N * 2)
+    workload = f"prefill_{kvn}_h{H}_d{D}_n{N}_q{NQ}_{mask_kind}_mask"
+    kname = att.describe()
+    # HBM bytes per launch from the committed FETCH_SIZE / WRITE_SIZE passes of
+    # this exact plan and source (tools/pmc_summary.py --traffic), else None
+    traffic = committed_traffic(workload, kname)
+    return {"workload": workload, "kernel": kname, "kernel_ms_avg": round(ms, 5), "flops_per_step": flops,
+            "bytes_per_step": alg_bytes,
             "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None}}
+                         "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "traffic_over_algorithmic": round(traffic / alg_bytes, 4) if traffic else None}}
 
 
 def parse_args(argv=None):
@@ -319,6 +327,8 @@ def parse_args(argv=None):
                          "reported beside it")
     ap.add_argument("--prefill-kv", default="q8_0", choices=["q8_0", "q4_0", "f16"],
                     help="K/V type of the prefill measurement (the metric's is q8_0)")
+    ap.add_argument("--prefill-only", action="store_true",
+                    help="N=1: only the prefill measurement, as a line tools/pmc_summary.py can tag traffic with")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS, else os.cpu_count()")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -629,6 +639,17 @@ def main():
             dist.init_process_group("gloo", init_method="env://")
         else:
             dist.init_process_group("nccl", init_method="env://", device_id=dev)
+    if args.prefill_only and world == 1:
+        # (profiling passes: the prefill launches alone)
+        hip, evs = hip_events(2)
+        r = prefill_measure(dev, hip, evs, args.prefill_kv, args.prefill_mask)
+        print(json.dumps({"metric": METRIC + " (prefill shape)", "value": r["roofline"]["achieved"], "unit": "TFLOP/s",
+                          "n_gpus": 1, "kernel_ms_avg": r["kernel_ms_avg"],
+                          "config": {"workload": r["workload"], "bytes_per_step": r["bytes_per_step"],
+                                     "flops_per_step": r["flops_per_step"]},
+                          "roofline": {**r["roofline"], "kernel": r["kernel"]}, "source_hash": source_hash()}),
+              flush=True)
+        return
     mode = args.multi if world > 1 else "head"
     workload = args.workload if args.workload != "auto" else ("config5" if mode == "head" and world > 1 else "config3")
     shape = shape_of(args, workload)

@@ -334,7 +334,11 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     a.nbuf = 0;
     a.wave_bytes = 0;
-    pl.lds = pl.kt == FATTN_TYPE_Q8_0 ? BdCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes;
+    pl.lds = pl.bdp ? (pl.kt == FATTN_TYPE_Q8_0 ? BdpCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
+                                                : BdpCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes)
+             : pl.kt == FATTN_TYPE_Q8_0 ? BdCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
+             : pl.kt == FATTN_TYPE_Q4_0 ? BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes
+                                        : BdCfg<FATTN_TYPE_F16, 128>::ldsBytes;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     // the chunk partials merge inside the launch (bd_tile_merge: the tile's
     // workgroups wait for each other, so only when the whole grid is
@@ -462,15 +466,19 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // are packed (R = rk2, a power of two <= 64).
     // (below 256 packed rows per kv head the split kernel measures faster:
     // config 5, 64 rows, 15.5 vs 37.6 us at 4 heads; FATTN_OPT_MQ_MIN_ROWS)
+    // (any rk2 <= 64: with R = rk2 not a power of two a tile packs
+    // floor(rows / R) whole head groups and its last rows stay empty)
     const bool mq_ok = !g_opt_mq_disable && !mixed && is_quant(k.type) && g16 && (D == 64 || D == 128 || D == 256) &&
-                       NQ * a.rk2 >= 32 &&
-                       a.rk2 <= 64 &&
-                       (a.rk2 & (a.rk2 - 1)) == 0;
+                       NQ * a.rk2 >= 32 && a.rk2 <= 64;
+    // the same packing for f16 K/V rows (not transposed V): the prefill and
+    // batched-decode kernels fill their f16 images by LDS-DMA straight from the rows
+    const bool heads_ok = NQ * a.rk2 >= 32 && a.rk2 <= 64;
+    const bool f16_ok = !g_opt_mq_disable && !mixed && k.type == FATTN_TYPE_F16 && !v_trans && g16 && heads_ok;
     // Both 64-row-tile kernels (multi-query, batched decode) need every KV
     // chunk to hold at least two 128-key tiles: a workgroup with one tile is all
     // prologue and epilogue (config-5 shard, 4 heads x 64 rows: split kernel
     // 9.4 + 4.3 us merge, multi-query 11.0 + 4.3, batched decode 10.9 + 4.4)
-    const int64_t qpt64 = mq_ok ? 64 / a.rk2 : 1;  // query rows per 64-row tile (rk2 <= 64)
+    const int64_t qpt64 = (mq_ok || f16_ok) ? 64 / a.rk2 : 1;  // query rows per 64-row tile (rk2 <= 64)
     const int64_t y64 = Hkv * ((NQ + qpt64 - 1) / qpt64);
     const bool wide = N * y64 * S >= (int64_t)2 * kBdKeys * pl.cus;
     pl.mq = mq_ok && NQ * a.rk2 >= g_opt_mq_min_rows &&
@@ -492,9 +500,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // the (kv head x query tile x seq) workgroups alone fill the chip
     // (f16 K/V rows, not transposed V: the same kernel, images filled by DMA)
     pl.pf = false;
-    const bool heads_ok = NQ * a.rk2 >= 32 && a.rk2 <= 64 && (a.rk2 & (a.rk2 - 1)) == 0;
-    const bool pf_f16 = !g_opt_mq_disable && !mixed && k.type == FATTN_TYPE_F16 && !v_trans && g16 && heads_ok;
-    if ((mq_ok || pf_f16) && g_opt_pf != 1 && (D == 64 || D == 128) && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
+    if ((mq_ok || f16_ok) && g_opt_pf != 1 && (D == 64 || D == 128) && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
         p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= pl.cus)) {
         pl.pf = true;
         pl.mq = false;
@@ -506,12 +512,15 @@ int make_plan(const fattn_params* p, Plan& pl) {
     }
     // batched decode (config 5: 64 query rows per kv head): 64-row workgroups
     // over 128-key tiles, the KV split over workgroups to fill the chip, the
-    // chunk partials merged in a second launch
+    // chunk partials merged in a second launch; Q8_0 / Q4_0 and f16 K/V
     // (from 64 rows, when the chunks hold two tiles or more: `wide` above)
-    pl.bd = false;
-    if (!pl.pf && g_opt_bd != 1 && mq_ok && D == 128 && N % kStep == 0 &&
-        (g_opt_bd == 2 || (NQ * a.rk2 >= kBdRows && wide))) {
+    // Q8_0 / Q4_0 take the compute / build-role form (fattn_bdp.h) unless
+    // FATTN_OPT_BD = 2 asks for the all-waves form
+    pl.bd = pl.bdp = false;
+    if (!pl.pf && g_opt_bd != 1 && (mq_ok || f16_ok) && D == 128 && N % kStep == 0 &&
+        (g_opt_bd >= 2 || (NQ * a.rk2 >= kBdRows && wide))) {
         pl.bd = true;
+        pl.bdp = mq_ok && g_opt_bd != 2;
         pl.mq = false;
         a.R = a.rk2;
         a.R_inv = 1.0f / (float)a.R;
@@ -627,7 +636,7 @@ int fattn_set_option(int option, int value) {
             g_opt_split_waves = value;
             return FATTN_OK;
         case FATTN_OPT_BD:
-            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            if (value < 0 || value > 3) return FATTN_ERR_INVALID_ARG;
             g_opt_bd = value;
             return FATTN_OK;
         case FATTN_OPT_MERGE_IN_KERNEL:
@@ -694,7 +703,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
         std::snprintf(kern, sizeof kern, "%sfattn_pf_kernel<%s,D%d,%s>", pl.pf_flags ? "pf_mask_flags_kernel + " : "",
                       tn(pl.kt), pl.D, hm);
     else if (pl.bd)
-        std::snprintf(kern, sizeof kern, "fattn_bd_kernel<%s,D%d,%s>%s", tn(pl.kt), pl.D, hm,
+        std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D, hm,
                       pl.a.merge_launch == 1 ? " + fattn_bd_merge_kernel" : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     else if (pl.mq)
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,

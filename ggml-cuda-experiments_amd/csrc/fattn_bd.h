@@ -56,13 +56,21 @@ constexpr int kBdKeys = 128;                   // keys per tile (four 32-key qua
 template <int KT, int D>
 struct BdCfg {
     static_assert(D == 128, "four 32-dim blocks: one ggml block per V image block");
+    // f16 K/V (the reference's own cache type): no raw tiles and no
+    // dequantisation -- the LDS-DMA writes the images straight from the rows,
+    // into a ring of two image pairs (tile s computes while s + 1 lands)
+    static constexpr bool kF16 = KT == FATTN_TYPE_F16;
     static constexpr int rowB = row_bytes<KT, D>();
     static constexpr int kvRaw = kBdKeys * rowB;                 // raw K (or V) bytes per tile
     static constexpr int rawBytes = (2 * kvRaw + 15) / 16 * 16;  // [K rows | V rows]
-    static constexpr int nRaw = 2;
+    static constexpr int nRaw = kF16 ? 0 : 2;
     static constexpr int img = kBdKeys * D * 2;                  // one f16 image (K, then V)
-    static constexpr int rawOff = 2 * img;
+    static constexpr int nPair = kF16 ? 2 : 1;                   // [K image | V image] pairs
+    static constexpr int rawOff = nPair * 2 * img;
     static constexpr int ringEnd = rawOff + nRaw * rawBytes;
+    // where Q's f32 rows are staged before the first tile: the K image of the
+    // pair tile 0 does not use (f16: pair 1, whose tile is issued once Q is read)
+    static constexpr int qOff = kF16 ? 2 * img : 0;
     static constexpr int NI = (kvRaw + 1023) / 1024;             // 1-KiB DMA instructions per K (or V) tile
     // instructions j = 0 .. 2 NI - 1 (K then V) go to wave j % 8
     static constexpr int ni_wave(int w) { return (2 * NI - w + kBdWaves - 1) / kBdWaves; }
@@ -72,12 +80,9 @@ struct BdCfg {
     static constexpr int maskSlot = 2048;
     static constexpr int maskOff = ringEnd;
     static constexpr int maskEnd = maskOff + kBdWaves * maskSlot;
-    // epilogue: every wave parks its (O, m, l) rows here, [4 key quarters][64
-    // rows][D + 4] f32 (+16 B per row: the accumulator-layout writes are
-    // conflict-free) then [4][64] (m, l)
-    static constexpr int parkStride = D + 4;
-    static constexpr int parkMl = 4 * kBdRows * parkStride * 4;
-    static constexpr int parkBytes = parkMl + 4 * kBdRows * 8;
+    // epilogue: every wave parks its (O, m, l) rows at the front, [4 key
+    // quarters][64 rows][D + 4] f32 then [4][64] (m, l) (BdPark)
+    static constexpr int parkBytes = 4 * kBdRows * (D + 4) * 4 + 4 * kBdRows * 8;
     static constexpr int ldsBytes = maskEnd > parkBytes ? maskEnd : parkBytes;
     // Q staged as f32 rows [64][D] in the K image's place before the first tile
     static_assert(kBdRows * D * 4 <= img && D * 4 / 16 == 32, "Q rows of 32 16-B chunks in the image's place");
@@ -98,6 +103,40 @@ __device__ __forceinline__ void bd_issue(const StepSrc& rs, int n0, uint32_t lds
         if (C::kvRaw % 1024 == 0 || byte < C::kvRaw)
             dma<16, kDecodeNT>(is_v ? rs.v : rs.k, lds + (is_v ? C::kvRaw : 0) + i * 1024,
                                (uint32_t)n0 * C::rowB + byte);
+    }
+}
+
+// f16 K/V: tile rows -> the pair's f16 images by LDS-DMA, laid out exactly as
+// bd_dequant writes them (so the compute reads one layout).  64 1-KiB
+// instructions per tile, instruction j = wave + 8 i: j < 32 K (dim slice j / 4,
+// keys 32 (j % 4) ..: lane l = key pair half), else V (dim block (j - 32) / 8,
+// keys 16 ((j - 32) % 8) ..: lane l = key quarter chunk).  Each lane's SOURCE
+// offset carries the image swizzle (the LDS side of a DMA is lane-linear,
+// cdna_hip_programming.md rule 21); rows are addressed by nb1, so llama.cpp's
+// [N][Hkv] cache works too.  Keys past N read past the descriptor: zeros.
+template <int D>
+__device__ __forceinline__ void bd_issue_f16(const StepSrc& rs, uint32_t k_nb1, uint32_t v_nb1, int n0, uint32_t lds,
+                                             int wave, int lane) {
+#ifdef FATTN_MQ_NOMEM
+    return;  // diagnostic build only
+#endif
+    constexpr int img = kBdKeys * D * 2;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int j = wave + kBdWaves * i;  // (i < 4: K; wave-uniform)
+        if (i < 4) {
+            const int w = j >> 2, kb = j & 3;
+            const int key = 32 * kb + (lane >> 1);
+            const int q = (lane & 1) ^ ((key >> 3) & 1);
+            dma<16, kDecodeNT>(rs.k, lds + w * (kBdKeys * 32) + kb * 1024,
+                               (uint32_t)(n0 + key) * k_nb1 + 32 * w + 16 * q);
+        } else {
+            const int jj = j - 32, b = jj >> 3, kb = jj & 7;
+            const int key = 16 * kb + (lane >> 2);
+            const int c = (lane & 3) ^ ((key >> 2) & 3);
+            dma<16, kDecodeNT>(rs.v, lds + img + b * (kBdKeys * 64) + kb * 1024,
+                               (uint32_t)(n0 + key) * v_nb1 + 64 * b + 16 * c);
+        }
     }
 }
 
@@ -213,24 +252,31 @@ __device__ __forceinline__ void bd_tile_merge(const SplitArgs& a, uint8_t* smem,
 }
 
 // ---- epilogue of the batched-decode kernels (all memory traffic of the tile
-// loop drained): merge the four key quarters of each row.  Every wave parks
-// its rows' (O, m, l) in LDS (accumulator layout -> [kq][row][D + 4]); then
-// each of the 512 threads merges 16 dims of one row (fixed order, kq = 0..3)
-// and stores them as 64 contiguous bytes, so every store instruction writes
-// whole rows (row-per-lane stores from the accumulator layout issue 32 lines
-// per instruction: MI355X_MICROARCH.md, epilogue store tail)
-template <int KT, int D>
+// loop drained): merge the NKG key groups of each row (bd: four key quarters;
+// bdp: two key halves).  Every wave that holds a state parks its rows' (O, m,
+// l) in LDS (accumulator layout -> [kg][row][D + 4]); then each of the 512
+// threads merges 16 dims of one row (fixed order, kg = 0..NKG-1) and stores
+// them as 64 contiguous bytes, so every store instruction writes whole rows
+// (row-per-lane stores from the accumulator layout issue 32 lines per
+// instruction: MI355X_MICROARCH.md, epilogue store tail)
+template <int D, int NKG>
+struct BdPark {
+    static constexpr int stride = D + 4;  // floats (+16 B per row: the accumulator-layout writes are conflict-free)
+    static constexpr int ml = NKG * kBdRows * stride * 4;
+    static constexpr int bytes = ml + NKG * kBdRows * 8;
+};
+template <int D, int NKG>
 __device__ __forceinline__ void bd_finish(const SplitArgs& a, uint8_t* smem, const f32x16 (&o)[D / 32], float m_run,
-                                          f32x2 l2, int kq, int p, int h, int tid, int lane, int wave, int qt, int ik2,
-                                          int iq3, int y, int chunk) {
-    using C = BdCfg<KT, D>;
+                                          f32x2 l2, int kq, int p, int h, bool has_state, int tid, int lane, int wave,
+                                          int qt, int ik2, int iq3, int y, int chunk) {
+    using PK = BdPark<D, NKG>;
     constexpr int NDB = D / 32;
     constexpr float kNegInf = -__builtin_inff();
     (void)lane; (void)wave;  // (stamps)
     const float l_own = xor32_pair(l2.x + l2.y, false);
     __syncthreads();  // every wave is done with the tiles' LDS
-    {
-        float* pk = (float*)smem + (kq * kBdRows + p) * C::parkStride + 4 * h;
+    if (has_state) {
+        float* pk = (float*)smem + (kq * kBdRows + p) * PK::stride + 4 * h;
 #pragma unroll
         for (int db = 0; db < NDB; db++) {
 #pragma unroll
@@ -238,17 +284,17 @@ __device__ __forceinline__ void bd_finish(const SplitArgs& a, uint8_t* smem, con
                 *(f32x4*)(pk + 32 * db + 8 * uu) = f32x4{o[db][4 * uu], o[db][4 * uu + 1], o[db][4 * uu + 2],
                                                          o[db][4 * uu + 3]};
         }
-        if (h == 0) ((f32x2*)(smem + C::parkMl))[kq * kBdRows + p] = f32x2{m_run, l_own};
+        if (h == 0) ((f32x2*)(smem + PK::ml))[kq * kBdRows + p] = f32x2{m_run, l_own};
     }
     __syncthreads();
     FATTN_STAMP(12);
     constexpr int kDpt = kBdRows * D / (kBdWaves * kWave);  // dims per thread: 16
     const int pr = tid / (D / kDpt), c0 = (tid % (D / kDpt)) * kDpt;
-    const f32x2* pml = (const f32x2*)(smem + C::parkMl);
-    f32x2 mlk[4];
+    const f32x2* pml = (const f32x2*)(smem + PK::ml);
+    f32x2 mlk[NKG];
     float M = kNegInf;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < NKG; k++) {
         mlk[k] = pml[k * kBdRows + pr];
         M = fmaxf(M, mlk[k].x);
     }
@@ -257,10 +303,10 @@ __device__ __forceinline__ void bd_finish(const SplitArgs& a, uint8_t* smem, con
 #pragma unroll
     for (int e = 0; e < kDpt; e++) acc[e] = 0.0f;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < NKG; k++) {
         const float wk = (mlk[k].x == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mlk[k].x - M);
         L += wk * mlk[k].y;
-        const float* src = (const float*)smem + (k * kBdRows + pr) * C::parkStride + c0;
+        const float* src = (const float*)smem + (k * kBdRows + pr) * PK::stride + c0;
 #pragma unroll
         for (int e = 0; e < kDpt; e += 4) {
             const f32x4 x = *(const f32x4*)(src + e);
@@ -272,11 +318,12 @@ __device__ __forceinline__ void bd_finish(const SplitArgs& a, uint8_t* smem, con
     }
     const int rq = div_R(a, pr);
     const int q1 = qt * a.QPT + rq;
+    const bool pr_ok = rq < a.QPT && q1 < a.NQ;  // (R not a power of two: rows past QPT * R are none)
     if (a.merge_launch == 2) {
-        bd_tile_merge<D>(a, smem, acc, M, L, pr, c0, q1 < a.NQ, tid, lane, wave, qt, iq3, y, chunk);
+        bd_tile_merge<D>(a, smem, acc, M, L, pr, c0, pr_ok, tid, lane, wave, qt, iq3, y, chunk);
         return;
     }
-    if (q1 >= a.NQ) return;
+    if (!pr_ok) return;
     if (a.n_chunks == 1) {
         const int q2 = ik2 * a.rk2 + (pr - rq * a.R);
         float* out = a.dst + (((int64_t)iq3 * a.NQ + q1) * a.H + q2) * D + c0;
@@ -338,8 +385,9 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     }
     if (a.rk3 != 1) ik3 = iq3 / a.rk3;
     const int p = kBdRowsW * rg + c32;  // packed row of the workgroup tile (its q head only
-    const int iq1 = qt * a.QPT + div_R(a, p);  // matters to Q and dst, both addressed per row below)
-    const bool row_ok = iq1 < a.NQ;
+    const int rq0 = div_R(a, p);        // matters to Q and dst, both addressed per row below)
+    const int iq1 = qt * a.QPT + rq0;
+    const bool row_ok = rq0 < a.QPT && iq1 < a.NQ;  // (R not a power of two: rows past QPT * R are none)
 
     // ---- this workgroup's KV chunk: 128-key tiles (N % 32 == 0; a tile's
     // quarters past the chunk are idle)
@@ -352,8 +400,9 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
     rs.m = make_srd(a.mask, HM ? a.m_span : 0);
     const uint32_t lds0 = lds_addr(smem);
-    auto raw_lds = [&](int s) { return lds0 + C::rawOff + (s % C::nRaw) * C::rawBytes; };
-    auto raw_ptr = [&](int s) { return smem + C::rawOff + (s % C::nRaw) * C::rawBytes; };
+    constexpr int kRing = C::nRaw ? C::nRaw : 1;  // (f16: no raw slots)
+    auto raw_lds = [&](int s) { return lds0 + C::rawOff + (s % kRing) * C::rawBytes; };
+    auto raw_ptr = [&](int s) { return smem + C::rawOff + (s % kRing) * C::rawBytes; };
 
     // ---- Q: the workgroup's 64 rows (f32, D per row) copied HBM -> LDS into the
     // V image's place by 1-KiB LDS-DMA instructions (2 rows each, dealt over
@@ -371,10 +420,10 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
             const int q1 = qt * a.QPT + rq, q2 = ik2 * a.rk2 + (pr - rq * a.R);
             // LDS chunk (lane & 31) of row pr holds the row's chunk (lane & 31) ^ (pr & 31):
             // the operand reads below (32 rows at once) then spread over the banks
-            const uint32_t off = q1 < a.NQ ? (uint32_t)q1 * (uint32_t)a.q_nb1 + (uint32_t)q2 * (uint32_t)a.q_nb2 +
+            const uint32_t off = rq < a.QPT && q1 < a.NQ ? (uint32_t)q1 * (uint32_t)a.q_nb1 + (uint32_t)q2 * (uint32_t)a.q_nb2 +
                                                  (((lane & 31) ^ (pr & 31)) * 16)
                                            : a.q_span;
-            dma<16>(qs, lds0 + j * 1024, off);
+            dma<16>(qs, lds0 + C::qOff + j * 1024, off);
         }
     }
     constexpr int kQInstW = kBdRows * D * 4 / 1024 / kBdWaves;  // Q DMA instructions per wave
@@ -385,9 +434,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     const uint32_t mslot = lds0 + C::maskOff + wave * C::maskSlot;
     uint32_t mrow_l;
     {
-        const int r = kBdRowsW * rg + c32;
-        const int q1 = qt * a.QPT + div_R(a, r);
-        mrow_l = q1 < a.NQ ? (uint32_t)q1 * (uint32_t)a.m_nb1 : a.m_span;
+        mrow_l = row_ok ? (uint32_t)iq1 * (uint32_t)a.m_nb1 : a.m_span;
     }
     auto mask_issue = [&](int s) {
         if constexpr (HM) {
@@ -417,9 +464,19 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     // mask goes BEFORE the raw tile that is two ahead: at the top of tile s
     // only mask s and raw s + 1 were issued after raw s, and only raw s + 1
     // after mask s -- tile s computes while tile s + 1 is still in flight.
+    // f16: Q | mask 0 | tile 0 into pair 0, then per tile s, right after the
+    // barrier that ends tile s - 1's compute (and, for s = 0, the Q reads):
+    // tile s + 1 into pair (s + 1) % 2 | mask s + 1
+    const uint32_t k_nb1 = (uint32_t)a.k_nb1, v_nb1 = (uint32_t)a.v_nb1;
+    auto tile_issue = [&](int s) {
+        if constexpr (C::kF16)
+            bd_issue_f16<D>(rs, k_nb1, v_nb1, c_lo + s * kBdKeys, lds0 + (s & 1) * 2 * C::img, wave, lane);
+        else
+            bd_issue<KT, D>(rs, c_lo + s * kBdKeys, raw_lds(s), wave, lane);
+    };
     if (ntiles > 0) mask_issue(0);
-    if (ntiles > 0) bd_issue<KT, D>(rs, c_lo, raw_lds(0), wave, lane);
-    if (ntiles > 1) bd_issue<KT, D>(rs, c_lo + kBdKeys, raw_lds(1), wave, lane);
+    if (ntiles > 0) tile_issue(0);
+    if (!C::kF16 && ntiles > 1) tile_issue(1);
 
     float m_run = kNegInf;    // reference max (log2 domain) of this lane's row
     f32x2 l2 = {0.0f, 0.0f};  // this lane's partial row sums (16 of every 32 keys)
@@ -435,7 +492,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     FATTN_STAMP(1);
     // Q landed (mask 0, raw 0 and raw 1 may fly on); every wave's Q pieces in LDS
     {
-        const int n1 = ntiles > 1 ? 1 : 0, n0 = ntiles > 0 ? 1 : 0;
+        const int n1 = (!C::kF16 && ntiles > 1) ? 1 : 0, n0 = ntiles > 0 ? 1 : 0;
         bd_vm_wait<KT, D, HM>(wave, n0 + n1, n0);
     }
     __syncthreads();
@@ -444,7 +501,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     f16x8 qop[NK];
 #pragma unroll
     for (int kk = 0; kk < NK; kk++) {
-        const float* qr = (const float*)smem + p * D;
+        const float* qr = (const float*)(smem + C::qOff) + p * D;
         const f32x4 x0 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h) ^ (p & 31)));
         const f32x4 x1 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h + 1) ^ (p & 31)));
         f16x8 hq;
@@ -456,17 +513,24 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     FATTN_STAMP(2);
 
     for (int s = 0; s < ntiles; s++) {
-        // raw s landed (mask s (s >= 1) and raw s + 1 may fly on)
-        bd_vm_wait<KT, D, HM>(wave, s + 1 < ntiles ? 1 : 0, s > 0 ? 1 : 0);
+        // quantised: raw s landed (mask s (s >= 1) and raw s + 1 may fly on);
+        // f16: tile s landed (mask s (s >= 1) may fly on; tile s + 1 is
+        // issued below)
+        bd_vm_wait<KT, D, HM>(wave, (!C::kF16 && s + 1 < ntiles) ? 1 : 0, s > 0 ? 1 : 0);
         if (s < 4) FATTN_STAMP(3 + 2 * s);
-        // every wave's pieces of raw s landed; every wave is done with tile
-        // s - 1 (the images are free)
+        // every wave's pieces of tile s landed; every wave is done with tile
+        // s - 1 (quantised: the images are free; f16: pair (s + 1) % 2 is)
         __syncthreads();
         if (s == 0) FATTN_STAMP(14);
-        bd_dequant<KT, D>(raw_ptr(s), smem, smem + C::img, wave, lane);
-        // the images are complete and raw s's slot is free
-        __syncthreads();
+        if constexpr (C::kF16) {
+            if (s + 1 < ntiles) tile_issue(s + 1);
+        } else {
+            bd_dequant<KT, D>(raw_ptr(s), smem, smem + C::img, wave, lane);
+            // the images are complete and raw s's slot is free
+            __syncthreads();
+        }
         if (s == 0) FATTN_STAMP(15);
+        const int pofs = C::kF16 ? (s & 1) * 2 * C::img : 0;  // this tile's image pair
         // this lane's mask values of tile s (keys 8 u + 4 h + 0..3 of the
         // quarter) out of the wave's slot (mask s landed: only raw s + 1 was
         // issued after it; mask 0 went before raw 0), then mask s + 1 into the
@@ -476,6 +540,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
         u32x2 mh[4];
         uint32_t open = 1;  // any key not at -inf (f16 0xFC00)
         if constexpr (HM) {
+            // (f16, s = 0: the wait above was vmcnt(0); mask 0 went before tile 0)
             if (s > 0) bd_vm_wait<KT, D, HM>(wave, s + 1 < ntiles ? 1 : 0, 0);
             open = 0;
             const uint8_t* ms = smem + C::maskOff + wave * C::maskSlot + c32 * 16 + h * 8;
@@ -489,7 +554,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
                 mask_issue(s + 1);
             }
         }
-        if (s + 2 < ntiles) bd_issue<KT, D>(rs, c_lo + (s + 2) * kBdKeys, raw_lds(s + 2), wave, lane);
+        if (!C::kF16 && s + 2 < ntiles) tile_issue(s + 2);
 #ifdef FATTN_MQ_NOCOMPUTE
         continue;  // diagnostic build only: copies, V dequant and barriers
 #endif
@@ -502,7 +567,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
         // from the image before the MFMA chain (one LDS wait, not eight)
         f16x8 ka[NK];
 #pragma unroll
-        for (int kk = 0; kk < NK; kk++) ka[kk] = *(const f16x8*)(smem + kk * (kBdKeys * 32) + kq * 1024 + kbase);
+        for (int kk = 0; kk < NK; kk++) ka[kk] = *(const f16x8*)(smem + pofs + kk * (kBdKeys * 32) + kq * 1024 + kbase);
         __builtin_amdgcn_sched_barrier(0);
         f32x16 st;
 #pragma unroll
@@ -564,7 +629,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
             u32x4 va[NDB];
 #pragma unroll
             for (int db = 0; db < NDB; db++) {
-                const uint32_t off = db * (kBdKeys * 64) + q * 1024;
+                const uint32_t off = pofs + db * (kBdKeys * 64) + q * 1024;
                 const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + vbase[0] + off));
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + vbase[1] + off));
                 const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
@@ -585,7 +650,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     }
     FATTN_STAMP(11);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    bd_finish<KT, D>(a, smem, o, m_run, l2, kq, p, h, tid, lane, wave, qt, ik2, iq3, y, chunk);
+    bd_finish<D, 4>(a, smem, o, m_run, l2, kq, p, h, true, tid, lane, wave, qt, ik2, iq3, y, chunk);
 }
 
 // Second launch of a split batched-decode plan: one wave per (tile, packed

@@ -1,0 +1,395 @@
+// fattn_bdp.h -- batched decode over ggml-quantised KV with the dequantisation
+// taken off the compute waves' path (gfx950).  Same problem and math as
+// fattn_bd.h (64 packed (query row x q-head) rows of one kv head per
+// workgroup, BASELINE config 5 and its head shards; replaces
+// flash_attn_ext_f16<D,Q,C>, src/flash-llama.h:5-438, whose 16-row Q tiles
+// re-read K/V per 16 rows):
+//
+//  * one workgroup = 8 waves with fixed roles, one pair per SIMD: waves 0-3
+//    COMPUTE (wave c: row group c & 1 = 32 rows, key half c >> 1 = 32 keys of
+//    every 64-key tile), waves 4-7 BUILD (wave 4 + b: ggml block b of every
+//    key, K and V);
+//  * per 64-key tile s, between two workgroup barriers, the compute waves run
+//    S^T = K.Q^T, the online softmax and O^T += V^T.P^T on tile s (one image
+//    pair) while the build waves dequantise raw tile s + 1 into the other pair
+//    and issue raw tile s + 4 into the raw slot they just emptied -- the
+//    dequantisation VALU of one SIMD partner runs beside the matrix work of
+//    the other, and there is ONE barrier per tile (fattn_bd.h: the whole
+//    workgroup dequantises 128-key tile s between two barriers and then
+//    computes it, every SIMD idle on one pipe in each phase);
+//  * HBM -> LDS by buffer_load ... lds: raw tiles (three in flight, issued by
+//    the build waves), each compute wave's 32 x 32 mask block (two tiles in
+//    flight, by the compute wave itself), Q's 64 f32 rows once before the loop
+//    (by all waves, into the second image pair's place);
+//  * dequantisation h(q * d) with one f16 rounding (src/utils.h:10-11), images
+//    and operand reads exactly as fattn_bd.h / fattn_pf.h (64-key images);
+//  * epilogue: bd_finish over the two key halves (whole-row stores; partials
+//    merged by fattn_bd_merge_kernel when the KV is split).
+//
+// LDS (D = 128, Q8_0): [0, 64 KiB) two image pairs (K [8 dim slices][64 keys]
+// [32 B], V [4 dim blocks][64 keys][64 B]), then 3 raw tiles [K rows | V rows]
+// of 17 KiB, then 4 compute waves x 2 mask slots of 2 KiB: 130 KiB.
+#pragma once
+
+#include "fattn_bd.h"
+
+namespace fattn {
+
+constexpr int kBdpKeys = 64;      // keys per tile (two 32-key halves)
+constexpr int kBdpCompute = 4;    // waves 0..3 compute, 4..7 build
+
+template <int KT, int D>
+struct BdpCfg {
+    static_assert(D == 128, "one ggml block per build wave");
+    static_assert(KT == FATTN_TYPE_Q8_0 || KT == FATTN_TYPE_Q4_0, "quantised K/V (f16 takes fattn_bd.h's image ring)");
+    static constexpr int rowB = row_bytes<KT, D>();
+    static constexpr int kvRaw = kBdpKeys * rowB;                // raw K (or V) bytes per tile
+    static constexpr int rawBytes = (2 * kvRaw + 15) / 16 * 16;  // [K rows | V rows]
+    static constexpr int nRaw = 3;
+    static constexpr int img = kBdpKeys * D * 2;                 // one f16 image
+    static constexpr int pair = 2 * img;
+    static constexpr int rawOff = 2 * pair;
+    static constexpr int maskOff = rawOff + nRaw * rawBytes;
+    static constexpr int maskSlot = 2048;                        // [4 key octets][32 rows][16 B]
+    static constexpr int maskEnd = maskOff + kBdpCompute * 2 * maskSlot;
+    static constexpr int ldsBytes = maskEnd > BdPark<D, 2>::bytes ? maskEnd : BdPark<D, 2>::bytes;
+    static constexpr int qOff = pair;                            // Q's f32 rows before the loop (pair 1)
+    static constexpr int NI = (kvRaw + 1023) / 1024;             // 1-KiB DMA instructions per K (or V) tile
+    // raw instructions j = 0 .. 2 NI - 1 (K then V) go to build wave 4 + j % 4;
+    // the smallest per-wave group counts every build wave's waits (a wave with
+    // one more instruction also waits for one of the next group: fattn_pf.h)
+    static constexpr int ni_min = (2 * NI) / 4;
+    static constexpr int NM = 2;                                 // mask DMA instructions per compute wave and tile
+    static_assert(kBdRows * D * 4 <= pair, "Q rows in the second pair's place");
+    static_assert(ldsBytes <= 163840, "");
+};
+
+template <int KT, int D>
+__device__ __forceinline__ void bdp_issue(const StepSrc& rs, int n0, uint32_t lds, int bw, int lane) {
+#ifdef FATTN_MQ_NOMEM
+    return;  // diagnostic build only
+#endif
+    using C = BdpCfg<KT, D>;
+    for (int j = bw; j < 2 * C::NI; j += 4) {  // wave-uniform
+        const bool is_v = j >= C::NI;
+        const int i = is_v ? j - C::NI : j;
+        const int byte = i * 1024 + lane * 16;
+        if (C::kvRaw % 1024 == 0 || byte < C::kvRaw)  // pieces past the tile's bytes idle (the instruction counts)
+            dma<16, kDecodeNT>(is_v ? rs.v : rs.k, lds + (is_v ? C::kvRaw : 0) + i * 1024, (uint32_t)n0 * C::rowB + byte);
+    }
+}
+
+// build wave b: block b of key `lane` (both halves), K into dim slices 2b, 2b + 1
+// and V into dim block b, in the layouts fattn_bd.h / fattn_pf.h read
+template <int KT, int D>
+__device__ __forceinline__ void bdp_dequant(const uint8_t* raw, uint8_t* k16, uint8_t* v16, int b, int lane) {
+#ifdef FATTN_MQ_NODEQ
+    return;  // diagnostic build only
+#endif
+    using C = BdpCfg<KT, D>;
+    const int r = lane;
+    const int sk = (r >> 3) & 1, sv = (r >> 2) & 3;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        u32x4 ck[2], cv[2];
+        dequant_half<KT, D>(raw, r, b, h, ck);
+        dequant_half<KT, D>(raw + C::kvRaw, r, b, h, cv);
+        uint8_t* kd = k16 + (2 * b + h) * (kBdpKeys * 32) + r * 32;
+        *(u32x4*)(kd + sk * 16) = ck[0];
+        *(u32x4*)(kd + (sk ^ 1) * 16) = ck[1];
+        uint8_t* vd = v16 + b * (kBdpKeys * 64) + r * 64;
+        *(u32x4*)(vd + ((2 * h) ^ sv) * 16) = cv[0];
+        *(u32x4*)(vd + ((2 * h + 1) ^ sv) * 16) = cv[1];
+    }
+}
+
+// build waves: at most n (0..2) raw groups issued after the awaited one in flight
+template <int KT, int D>
+__device__ __forceinline__ void bdp_build_wait(int n) {
+    constexpr int NI = BdpCfg<KT, D>::ni_min;
+    if (n >= 2) wait_vmcnt_c<2 * NI>();
+    else if (n == 1) wait_vmcnt_c<NI>();
+    else wait_vmcnt_c<0>();
+}
+
+template <int KT, int D, bool HM>
+__global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const SplitArgs a) {
+    using C = BdpCfg<KT, D>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NK = D / 16;   // 16-dim k-steps of S^T = K.Q^T
+    constexpr int NDB = D / 32;  // 32-dim blocks of O^T
+    constexpr int NM = HM ? C::NM : 0;
+    constexpr float kNegInf = -__builtin_inff();
+    constexpr float kDeferLog2 = 8.0f;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool compute = wave < kBdpCompute;  // wave-uniform role
+    const int rg = wave & 1, kh = (wave >> 1) & 1;  // compute waves: row group, key half
+    const int bw = wave - kBdpCompute;              // build waves: ggml block
+    const int h = lane >> 5;
+    const int c32 = lane & 31;
+    FATTN_STAMP(0);
+
+    // ---- tile decode (fattn_bd.h)
+    const int chunk = blockIdx.x;
+    const int y = blockIdx.y;
+    const int iq3 = blockIdx.z;
+    if (a.merge_launch == 2 && tid == 0) arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
+    int qt = 0, ik2 = y, ik3 = iq3;
+    if (a.n_qt != 1) {
+        qt = y % a.n_qt;
+        ik2 = y / a.n_qt;
+    }
+    if (a.rk3 != 1) ik3 = iq3 / a.rk3;
+    const int p = kBdRowsW * rg + c32;  // compute waves: this lane's packed row
+    const int rq0 = div_R(a, p);
+    const int iq1 = qt * a.QPT + rq0;
+    const bool row_ok = rq0 < a.QPT && iq1 < a.NQ;  // (R not a power of two: rows past QPT * R are none)
+
+    const int c_lo = chunk * a.chunk_len;
+    const int c_hi = min(a.N, c_lo + a.chunk_len);
+    const int ntiles = c_hi > c_lo ? (c_hi - c_lo + kBdpKeys - 1) / kBdpKeys : 0;
+
+    StepSrc rs;
+    rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
+    rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
+    rs.m = make_srd(a.mask, HM ? a.m_span : 0);
+    const uint32_t lds0 = lds_addr(smem);
+    auto raw_lds = [&](int s) { return lds0 + C::rawOff + (s % C::nRaw) * C::rawBytes; };
+    auto raw_ptr = [&](int s) { return smem + C::rawOff + (s % C::nRaw) * C::rawBytes; };
+
+    // ---- Q: 64 f32 rows -> LDS (pair 1's place) by 32 1-KiB DMA instructions,
+    // 4 per wave (fattn_bd.h's layout: row pr's 16-B chunk c at c ^ (pr & 31))
+    {
+        const i32x4 qs = make_srd(a.q + (int64_t)iq3 * a.q_nb3, a.q_span);
+        constexpr int kQInst = kBdRows * D * 4 / 1024;
+        static_assert(kQInst % kBdWaves == 0, "");
+#pragma unroll
+        for (int i = 0; i < kQInst / kBdWaves; i++) {
+            const int j = wave + kBdWaves * i;
+            const int pr = 2 * j + (lane >> 5);
+            const int rq = div_R(a, pr);
+            const int q1 = qt * a.QPT + rq, q2 = ik2 * a.rk2 + (pr - rq * a.R);
+            const uint32_t off = rq < a.QPT && q1 < a.NQ ? (uint32_t)q1 * (uint32_t)a.q_nb1 + (uint32_t)q2 * (uint32_t)a.q_nb2 +
+                                                 (((lane & 31) ^ (pr & 31)) * 16)
+                                           : a.q_span;
+            dma<16>(qs, lds0 + C::qOff + j * 1024, off);
+        }
+    }
+
+    // ---- compute waves' mask blocks: rows 32 rg + c32, keys 32 kh .. + 32 of a
+    // tile, slot (wave, s & 1); DMA instruction i, lane l: octet 2 i + (l >> 5)
+    const uint32_t mslot0 = lds0 + C::maskOff + (wave & 3) * 2 * C::maskSlot;
+    uint32_t mrow_l;
+    mrow_l = row_ok ? (uint32_t)iq1 * (uint32_t)a.m_nb1 : a.m_span;
+    auto mask_issue = [&](int s) {
+        if constexpr (HM) {
+            const uint32_t n2 = (uint32_t)(c_lo + s * kBdpKeys + 32 * kh) * 2;
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                dma<16>(rs.m, mslot0 + (s & 1) * C::maskSlot + i * 1024,
+                        mrow_l == a.m_span ? a.m_span : mrow_l + n2 + 16 * (2 * i + h));
+        }
+    };
+
+    // ---- prologue.  Compute waves: Q | mask 0 | mask 1.  Build waves: Q | raw 0
+    // | raw 1 | raw 2, then (after the barrier that completes raw 0) raw 0 ->
+    // pair 0 and raw 3 into its slot.
+    if (compute) {
+        if (ntiles > 0) mask_issue(0);
+        if (ntiles > 1) mask_issue(1);
+    } else {
+        for (int t = 0; t < min(3, ntiles); t++) bdp_issue<KT, D>(rs, c_lo + t * kBdpKeys, raw_lds(t), bw, lane);
+    }
+    FATTN_STAMP(1);
+    if (compute) {
+        // Q landed (this wave's pieces; masks 0 and 1 may fly on)
+        const int nm = min(2, ntiles);
+        if (nm >= 2) wait_vmcnt_c<2 * NM>();
+        else if (nm == 1) wait_vmcnt_c<NM>();
+        else wait_vmcnt_c<0>();
+    } else {
+        bdp_build_wait<KT, D>(min(2, ntiles - 1));  // raw 0 (and Q) landed
+    }
+    __syncthreads();  // Q and raw 0 complete in LDS
+    f16x8 qop[NK];
+    if (compute) {
+#pragma unroll
+        for (int kk = 0; kk < NK; kk++) {
+            const float* qr = (const float*)(smem + C::qOff) + p * D;
+            const f32x4 x0 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h) ^ (p & 31)));
+            const f32x4 x1 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h + 1) ^ (p & 31)));
+            f16x8 hq;
+            hq.s0 = (f16)x0.x; hq.s1 = (f16)x0.y; hq.s2 = (f16)x0.z; hq.s3 = (f16)x0.w;
+            hq.s4 = (f16)x1.x; hq.s5 = (f16)x1.y; hq.s6 = (f16)x1.z; hq.s7 = (f16)x1.w;
+            qop[kk] = hq;
+        }
+        // mask 0 landed (only mask 1 was issued after it)
+        if (ntiles > 1) wait_vmcnt_c<NM>();
+        else wait_vmcnt_c<0>();
+    } else {
+        if (ntiles > 0) {
+            bdp_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, bw, lane);
+            if (ntiles > 3) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot 0 read out
+                bdp_issue<KT, D>(rs, c_lo + 3 * kBdpKeys, raw_lds(3), bw, lane);
+            }
+            // raw 1 landed (raw 2, raw 3 may fly on)
+            if (ntiles > 1) bdp_build_wait<KT, D>(min(2, ntiles - 2));
+        }
+    }
+    FATTN_STAMP(2);
+
+    float m_run = kNegInf;    // compute waves: reference max (log2 domain) of this lane's row
+    f32x2 l2 = {0.0f, 0.0f};  // this lane's partial row sums
+    f32x16 o[NDB];
+#pragma unroll
+    for (int db = 0; db < NDB; db++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) o[db][j] = 0.0f;
+    }
+    const float log2e = 1.4426950408889634f;
+    const float scale = a.scale;
+    // per-lane K read base (key 32 kh + c32, half h; 16-B halves swapped on keys
+    // with bit 3 set) and V^T gather bases (fattn_bd.h, 64-key images)
+    const uint32_t kbase = kh * 1024 + c32 * 32 + ((h ^ ((c32 >> 3) & 1)) * 16);
+    const int gi = lane & 15, dh = (lane >> 4) & 1;
+    uint32_t vbase[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int row = 8 * e + 4 * h + (gi >> 2);
+        const int ch = (2 * dh + ((gi & 3) >> 1)) ^ ((h + 2 * e) & 3);
+        vbase[e] = C::img + kh * 2048 + row * 64 + ch * 16 + (gi & 1) * 8;
+    }
+
+    for (int s = 0; s < ntiles; s++) {
+        // pair s % 2 holds tile s (built before this barrier by the build
+        // waves); every compute wave is done with tile s - 1, so pair
+        // (s + 1) % 2 is free; raw s + 1 is complete (its build waves waited)
+        __syncthreads();
+        if (s < 4) FATTN_STAMP(3 + s);
+        if (!compute) {
+            // ---- build: raw s + 1 -> pair (s + 1) % 2; raw s + 4 into its slot;
+            // then wait for this wave's pieces of raw s + 2
+            if (s + 1 < ntiles) {
+                bdp_dequant<KT, D>(raw_ptr(s + 1), smem + ((s + 1) & 1) * C::pair,
+                                   smem + ((s + 1) & 1) * C::pair + C::img, bw, lane);
+                if (s + 4 < ntiles) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot has been read
+                    bdp_issue<KT, D>(rs, c_lo + (s + 4) * kBdpKeys, raw_lds(s + 4), bw, lane);
+                }
+                if (s + 2 < ntiles) bdp_build_wait<KT, D>(min(2, ntiles - 3 - s));
+            }
+            continue;
+        }
+        // ---- compute tile s.  This lane's mask values (keys 8 u + 4 h + 0..3 of
+        // the half) out of slot s & 1 (landed: waited for before the barrier),
+        // then mask s + 2 into that slot
+        const uint32_t pofs = (s & 1) * C::pair;
+        u32x2 mh[4];
+        uint32_t open = 1;  // any key not at -inf (f16 0xFC00)
+        if constexpr (HM) {
+            open = 0;
+            const uint8_t* ms = smem + C::maskOff + (wave & 3) * 2 * C::maskSlot + (s & 1) * C::maskSlot + c32 * 16 + h * 8;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                mh[u] = *(const u32x2*)(ms + u * 512);
+                open |= (mh[u].x ^ 0xFC00FC00u) | (mh[u].y ^ 0xFC00FC00u);
+            }
+            if (s + 2 < ntiles) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot has been read
+                mask_issue(s + 2);
+            }
+        }
+        // this wave's 32 keys past the chunk, or -inf for every valid row: nothing to add (exact)
+        const bool live = c_lo + s * kBdpKeys + 32 * kh < c_hi &&
+                          (!HM || __builtin_amdgcn_ballot_w64(open != 0 && row_ok) != 0);
+        if (live) {
+            f16x8 ka[NK];
+#pragma unroll
+            for (int kk = 0; kk < NK; kk++) ka[kk] = *(const f16x8*)(smem + pofs + kk * (kBdpKeys * 32) + kbase);
+            __builtin_amdgcn_sched_barrier(0);
+            f32x16 st;
+#pragma unroll
+            for (int j = 0; j < 16; j++) st[j] = 0.0f;
+#pragma unroll
+            for (int kk = 0; kk < NK; kk++) st = mfma32(ka[kk], qop[kk], st);
+
+            // u = scale * s + mask (natural units); element j = key 8 (j/4) + 4 h + j%4
+            float u[16];
+#pragma unroll
+            for (int uu = 0; uu < 4; uu++) {
+                if constexpr (HM) {
+                    const f16x2 m01 = as_h2(mh[uu].x), m23 = as_h2(mh[uu].y);
+                    u[4 * uu + 0] = fmaf(st[4 * uu + 0], scale, (float)m01.x);
+                    u[4 * uu + 1] = fmaf(st[4 * uu + 1], scale, (float)m01.y);
+                    u[4 * uu + 2] = fmaf(st[4 * uu + 2], scale, (float)m23.x);
+                    u[4 * uu + 3] = fmaf(st[4 * uu + 3], scale, (float)m23.y);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) u[4 * uu + r] = st[4 * uu + r] * scale;
+                }
+            }
+            float tmax = kNegInf;
+#pragma unroll
+            for (int j = 0; j < 16; j++) tmax = fmaxf(tmax, u[j]);
+            tmax = xor32_pair(tmax, true) * log2e;
+            // deferred max (cdna_hip_programming.md T13), the whole previous
+            // tile's P.V already accumulated
+            if (__builtin_amdgcn_ballot_w64(tmax > m_run + kDeferLog2)) {
+                const float m_new = fmaxf(m_run, tmax);
+                const float alpha = (m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run - m_new);
+                l2 *= alpha;
+#pragma unroll
+                for (int db = 0; db < NDB; db++) o[db] *= alpha;
+                m_run = m_new;
+            }
+            const float nm = (m_run == kNegInf) ? 0.0f : -m_run;
+            f16x8 pb[2];
+            {
+                float pv[16];
+#pragma unroll
+                for (int j = 0; j < 16; j++) pv[j] = __builtin_amdgcn_exp2f(fmaf(u[j], log2e, nm));
+#pragma unroll
+                for (int j = 0; j < 16; j += 2) l2 += f32x2{pv[j], pv[j + 1]};
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    f16x8 x;
+                    x.s0 = (f16)pv[8 * q]; x.s1 = (f16)pv[8 * q + 1]; x.s2 = (f16)pv[8 * q + 2]; x.s3 = (f16)pv[8 * q + 3];
+                    x.s4 = (f16)pv[8 * q + 4]; x.s5 = (f16)pv[8 * q + 5]; x.s6 = (f16)pv[8 * q + 6]; x.s7 = (f16)pv[8 * q + 7];
+                    pb[q] = x;
+                }
+            }
+            // O^T += V^T.P^T: k-step q covers keys 32 kh + 16 q + 8 (i/4) + 4 h + i%4
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+                u32x4 va[NDB];
+#pragma unroll
+                for (int db = 0; db < NDB; db++) {
+                    const uint32_t off = pofs + db * (kBdpKeys * 64) + q * 1024;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + vbase[0] + off));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + vbase[1] + off));
+                    const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                    va[db] = u32x4{a2.x, a2.y, b2.x, b2.y};
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[q], o[db]);
+            }
+        }
+        // mask s + 1 landed before the next barrier (only mask s + 2 after it)
+        if constexpr (HM) {
+            if (s + 1 < ntiles) {
+                if (s + 2 < ntiles) wait_vmcnt_c<NM>();
+                else wait_vmcnt_c<0>();
+            }
+        }
+    }
+    FATTN_STAMP(11);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    bd_finish<D, 2>(a, smem, o, m_run, l2, kh, p, h, compute, tid, lane, wave, qt, ik2, iq3, y, chunk);
+}
+
+}  // namespace fattn

@@ -14,6 +14,7 @@
 #include "fattn_mq.h"
 #include "fattn_pf.h"
 #include "fattn_bd.h"
+#include "fattn_bdp.h"
 #include "fattn_split.h"
 
 namespace fattn {
@@ -33,6 +34,7 @@ struct Plan {
     bool mq;  // multi-query kernel (fattn_mq.h)
     bool pf;  // prefill kernel (fattn_pf.h)
     bool bd;  // batched-decode kernel (fattn_bd.h)
+    bool bdp; // ... in its compute / build-role form (fattn_bdp.h; Q8_0 / Q4_0)
     bool pf_flags;          // masked prefill: live-block flags pre-pass (tile-range skipping)
     int nw;   // mq kernel: waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
 };
@@ -179,6 +181,9 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
 template <int KT, bool HM>
 int launch_bd_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     auto kern = fattn_bd_kernel<KT, 128, HM>;
+    if constexpr (KT != FATTN_TYPE_F16) {  // (the role form: quantised K/V only)
+        if (pl.bdp) kern = fattn_bdp_kernel<KT, 128, HM>;
+    }
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         hipLaunchKernelGGL(kern, pl.grid, dim3(kBdWaves * kWave), pl.lds, st, pl.a);
         if (pl.a.merge_launch == 1) {
@@ -238,6 +243,7 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
         if (pl.bd) {
             if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_bd<FATTN_TYPE_Q8_0>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_bd<FATTN_TYPE_Q4_0>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_bd<FATTN_TYPE_F16>(pl, st, ev);
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
     }

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(NW * kWave, NW == 8 ? 1 : 2) void fattn_mq_kernel(c
         mq[gi] = div_R(a, p);
         iq1[gi] = qt * a.QPT + mq[gi];
         iq2[gi] = ik2 * a.rk2 + (p - mq[gi] * a.R);
-        row_ok[gi] = iq1[gi] < a.NQ;
+        row_ok[gi] = mq[gi] < a.QPT && iq1[gi] < a.NQ;  // (R not a power of two: rows past QPT * R are none)
     }
 
     // ---- this workgroup's KV chunk: whole 32-position tiles (N % 32 == 0)
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(NW * kWave, NW == 8 ? 1 : 2) void fattn_mq_kernel(c
         if constexpr (HM) {
 #pragma unroll
             for (int gi = 0; gi < NG; gi++) {
-                const uint8_t* mb = rb + 2 * C::kvRaw + mq[gi] * (kStep * 2) + 8 * g;
+                const uint8_t* mb = rb + 2 * C::kvRaw + (mq[gi] < a.QPT ? mq[gi] : 0) * (kStep * 2) + 8 * g;
                 mk[gi][0] = *(const u32x2*)mb;
                 mk[gi][1] = *(const u32x2*)(mb + 32);
             }

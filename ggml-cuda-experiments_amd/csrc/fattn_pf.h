@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         const int mq = div_R(a, p);
         iq1 = qt * a.QPT + mq;
         iq2 = ik2 * a.rk2 + (p - mq * a.R);
-        return iq1 < a.NQ;
+        return mq < a.QPT && iq1 < a.NQ;  // (R not a power of two: rows past QPT * R are none)
     };
     int iq1, iq2;
     const bool row_ok = row_of(kPfRowsW * wave + c32, iq1, iq2);

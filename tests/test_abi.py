@@ -68,14 +68,18 @@ def test_workspace_size_config3():
     (dict(), ["8waves>", "grid(8,32,1)", "steps/slots 1"]),                                 # config 3
     (dict(N=2048, kt=fattn.TYPE_F16), ["f16,f16", "8waves>", "grid(8,32,1)"]),              # config 2
     (dict(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0), ["4waves> + fattn_merge_kernel", "grid(32,8,1)"]),  # config 4
-    (dict(NQ=64), ["fattn_bd_kernel", "+ fattn_bd_merge_kernel", "grid(8,32,1)"]),         # config 5, one GPU
+    (dict(NQ=64), ["fattn_bdp_kernel<q8_0", "+ fattn_bd_merge_kernel", "grid(8,32,1)"]),   # config 5, one GPU
     (dict(NQ=64, H=4, Hkv=4), ["fattn_split_kernel", "+ fattn_merge_kernel"]),             # config 5, 8-rank shard
-    (dict(NQ=64, H=16, Hkv=16), ["fattn_bd_kernel", "+ fattn_bd_merge_kernel", "grid(16,16,1)"]),  # config 5, 2-rank shard
-    (dict(NQ=256), ["fattn_bd_kernel", "grid(2,128,1)"]),                                   # batched: 4 row tiles
+    (dict(NQ=64, H=16, Hkv=16), ["fattn_bdp_kernel", "+ fattn_bd_merge_kernel", "grid(16,16,1)"]),  # config 5, 2-rank shard
+    (dict(NQ=256), ["fattn_bdp_kernel", "grid(2,128,1)"]),                                  # batched: 4 row tiles
+    (dict(NQ=64, kt=fattn.TYPE_F16), ["fattn_bd_kernel<f16,D128", "+ fattn_bd_merge_kernel"]),  # config 5 shape, f16
+    (dict(NQ=64, H=24, Hkv=4), ["fattn_bdp_kernel<q8_0", "grid(8,28,1)"]),                  # GQA 6: 7 tiles of 10 queries
+    (dict(NQ=64, H=4, Hkv=4, kt=fattn.TYPE_F16), ["fattn_split_kernel<f16,f16"]),           # f16, 8-rank shard
     (dict(NQ=8, H=32, Hkv=8), ["fattn_split_kernel", "+ fattn_merge_kernel"]),              # < 64 rows per kv head
     (dict(D=64, NQ=4096, H=32, Hkv=32), ["fattn_pf_kernel<q8_0,D64"]),                       # D = 64 prefill
     (dict(D=256, NQ=4096, H=16, Hkv=16), ["fattn_mq_kernel<q8_0,D256,4waves"]),              # D = 256 prefill
-], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "split_nq8_gqa", "pf_d64", "mq_d256"])
+], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "bd_f16",
+        "bd_gqa6", "bd_f16_shard", "split_nq8_gqa", "pf_d64", "mq_d256"])
 def test_planner_picks(kw, want):
     """The plans the round-2 measurements chose, at 256 CUs:
     one-row tiles take 8 waves with the fused row merge; multi-row split tiles
@@ -84,6 +88,18 @@ def test_planner_picks(kw, want):
     d = fattn.describe(_params(**kw))
     for w in want:
         assert w in d, d
+
+
+def test_bd_option_forms():
+    """FATTN_OPT_BD: 2 = the all-waves form, 3 = the compute / build-role form
+    (quantised K/V only; f16 keeps the all-waves form's image ring)."""
+    with fattn.options({fattn.OPT_BD: 2}):
+        assert fattn.describe(_params(NQ=64)).startswith("fattn_bd_kernel<q8_0")
+    with fattn.options({fattn.OPT_BD: 3}):
+        assert fattn.describe(_params(NQ=64, kt=fattn.TYPE_Q4_0)).startswith("fattn_bdp_kernel<q4_0")
+        assert fattn.describe(_params(NQ=64, kt=fattn.TYPE_F16)).startswith("fattn_bd_kernel<f16")
+    with pytest.raises(Exception):
+        fattn.set_option(fattn.OPT_BD, 4)
 
 
 def test_merge_in_kernel_option():

@@ -109,6 +109,19 @@ def test_config5_full_batch64(dev):
     assert attn_elem_err(got, ref) <= 1.0
 
 
+def test_config5_shape_f16_full(dev):
+    """Config 5's shape over the reference's own cache type (f16 K/V, 64 query
+    rows x 32 heads, N = 4096): the batched-decode kernel's f16 path, every
+    row against the oracle."""
+    p = make_problem(D=128, NQ=64, H=32, N=4096, kv_type="f16", seed=52)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert "fattn_bd_kernel<f16" in d, d
+    got, ref = run_gpu(p), p.oracle(n_threads=16)
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 @pytest.fixture
 def mq_on():
     """The multi-query kernel from 32 packed rows per kv head (the planner
@@ -131,6 +144,8 @@ MQ_CASES = [
     dict(D=64, kv_type="q8_0", NQ=70, H=2, Hkv=2, N=32, mask="random", S=2),     # one tile, 2 sequences
     dict(D=128, kv_type="q8_0", NQ=300, H=2, Hkv=2, N=256, mask="none"),        # no mask: DMA budget w/o mask
     dict(D=128, kv_type="q4_0", NQ=64, H=8, Hkv=8, N=1024, mask="none"),
+    dict(D=128, kv_type="q8_0", NQ=40, H=24, Hkv=4, N=320, mask="random"),      # R=6: 10 queries x 6 heads a tile
+    dict(D=64, kv_type="q4_0", NQ=20, H=14, Hkv=2, N=256, mask="causal"),       # R=7
 ]
 
 
@@ -299,6 +314,22 @@ BD_CASES = [
     dict(kv_type="q8_0", NQ=64, H=2, Hkv=2, N=1024, mask="causal"),
     dict(kv_type="q8_0", NQ=33, H=2, Hkv=2, N=1024, mask="random", S=2),     # ne03 batch
     dict(kv_type="q4_0", NQ=64, H=4, Hkv=2, N=640, mask="tail", S=2, Skv=1),  # seq broadcast, padded cache
+    # GQA ratios that are not powers of two (R = 6, 3, 48): a tile packs floor(64 / R)
+    # whole head groups, its last rows stay empty
+    dict(kv_type="q8_0", NQ=64, H=24, Hkv=4, N=1024, mask="random"),
+    dict(kv_type="q4_0", NQ=40, H=12, Hkv=4, N=768, mask="causal"),
+    dict(kv_type="q8_0", NQ=5, H=48, Hkv=1, N=512, mask="random"),
+    dict(kv_type="f16", NQ=64, H=24, Hkv=4, N=1024, mask="random"),
+    # f16 K/V (the reference's own cache type): images filled by LDS-DMA from the rows
+    dict(kv_type="f16", NQ=64, H=8, Hkv=8, N=4096, mask="random"),           # config 5 shape, 8 heads
+    dict(kv_type="f16", NQ=16, H=16, Hkv=4, N=1024, mask="random"),          # GQA
+    dict(kv_type="f16", NQ=40, H=2, Hkv=2, N=800, mask="random"),            # ragged rows, N % 128 = 32
+    dict(kv_type="f16", NQ=64, H=2, Hkv=2, N=96, mask="random"),             # one partial tile
+    dict(kv_type="f16", NQ=64, H=4, Hkv=4, N=1024, mask="none"),
+    dict(kv_type="f16", NQ=64, H=2, Hkv=2, N=2048, mask="neginf_blocks"),
+    dict(kv_type="f16", NQ=64, H=4, Hkv=2, N=1056, mask="causal", layout="pos"),  # llama.cpp's [N][Hkv] cache
+    dict(kv_type="f16", NQ=33, H=2, Hkv=2, N=1024, mask="random", S=2),      # ne03 batch
+    dict(kv_type="f16", NQ=64, H=4, Hkv=2, N=640, mask="tail", S=2, Skv=1),  # seq broadcast, padded cache
 ]
 
 
@@ -311,6 +342,83 @@ def test_bd_sweep(dev, bd_force, case):
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
+# ------------------------------------------------------------------ batched decode, role form (fattn_bdp.h)
+# Q8_0 / Q4_0: compute waves 0-3 and build (dequantising) waves 4-7, 64-key
+# tiles, one barrier per tile; FATTN_OPT_BD = 3 forces it (0 picks it too).
+
+@pytest.fixture
+def bdp_force():
+    fattn.set_option(fattn.OPT_BD, 3)
+    yield
+    fattn.set_option(fattn.OPT_BD, 0)
+
+
+BDP_CASES = [c for c in BD_CASES if c["kv_type"] != "f16"] + [
+    dict(kv_type="q8_0", NQ=64, H=2, Hkv=2, N=192, mask="random"),           # 3 tiles: raw ring never refilled
+    dict(kv_type="q4_0", NQ=64, H=2, Hkv=2, N=320, mask="causal"),           # 5 tiles: one refill
+    dict(kv_type="q8_0", NQ=64, H=4, Hkv=4, N=1056, mask="random", layout="pos"),
+]
+
+
+@pytest.mark.parametrize("case", BDP_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_bdp_sweep(dev, bdp_force, case):
+    p = make_problem(D=128, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000 + 7, **case)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    if case.get("layout") == "pos":  # (quantised rows not contiguous per head: the split kernel)
+        assert "fattn_bdp_kernel" not in d, d
+    else:
+        assert "fattn_bdp_kernel" in d, d
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
+@pytest.mark.parametrize("chunk", [128, 384, 1024, 100000])
+@pytest.mark.parametrize("mask", ["random", "neginf_blocks", "causal"])
+def test_bdp_chunking_and_masks(dev, bdp_force, chunk, mask):
+    """One to many 64-key tiles per workgroup (the raw ring's refills, the
+    mask ring's), masks that skip whole 32 x 32 blocks."""
+    p = make_problem(D=128, NQ=64, H=4, N=2048, kv_type="q8_0", mask=mask, seed=37)
+    got, ref = run_gpu(p, kv_chunk=chunk), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
+def test_bdp_rescale(dev, bdp_force, kt):
+    p = make_problem(D=128, NQ=64, H=2, N=2048, kv_type=kt, seed=38, extreme=True)
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+    p = make_problem(D=128, NQ=64, H=2, N=4096, kv_type=kt, seed=39, ramp=12.0, mask="none")
+    assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
+
+
+def test_bdp_fully_masked_rows_are_nan_and_deterministic(dev, bdp_force):
+    p = make_problem(D=128, NQ=64, H=2, N=1024, kv_type="q8_0", mask="random", seed=41)
+    m = orc.f16_bits_to_f32(p.mask_bits)
+    m[7, :] = -np.inf
+    m[63, :] = -np.inf
+    p.mask_bits = orc.f32_to_f16_bits(m)
+    got, ref = run_gpu(p), p.oracle()
+    assert np.isnan(got[:, 7]).all() and np.isnan(got[:, 63]).all()
+    assert attn_rel_err(got, ref) <= RTOL
+    again = run_gpu(p)
+    assert np.array_equal(got.view(np.uint32), again.view(np.uint32))
+
+
+def test_bdp_matches_bd_bitwise_inputs(dev):
+    """The role form against the all-waves form on one problem (same
+    dequantisation, same products; only the merge order of the key groups
+    differs), and both against the oracle."""
+    p = make_problem(D=128, NQ=64, H=8, Hkv=4, N=4096, kv_type="q8_0", seed=44)
+    with fattn.options({fattn.OPT_BD: 3}):
+        a = run_gpu(p)
+    with fattn.options({fattn.OPT_BD: 2}):
+        b = run_gpu(p)
+    assert attn_rel_err(a, b) <= RTOL
+    assert attn_rel_err(a, p.oracle()) <= RTOL
+
+
 @pytest.mark.parametrize("case,chunk", [
     (dict(NQ=1024, H=8, N=1024, mask="causal"), 0),   # 16 query tiles x 2 chunks of 4 tiles
     (dict(NQ=1024, H=8, N=1024, mask="random"), 0),
@@ -319,30 +427,33 @@ def test_bd_sweep(dev, bd_force, case):
     (dict(NQ=64, H=1, N=512, mask="neginf_blocks"), 512),
     (dict(NQ=64, H=4, N=4096, mask="neginf_blocks"), 1024),
 ], ids=["causal-16qt", "random-16qt", "causal-1wg", "random-1wg", "neginf-1wg", "neginf-8tiles"])
-def test_bd_masked_multitile(dev, bd_force, case, chunk):
+@pytest.mark.parametrize("kt", ["q8_0", "f16"])
+def test_bd_masked_multitile(dev, bd_force, case, chunk, kt):
     """Masked problems whose workgroups walk several 128-key tiles: the mask
     of tile s + 1 is fetched while tile s computes (a one-workgroup launch
     leaves the least time for it to land).  A register-held form of that
-    prefetch failed exactly these cases (rows 31 / 63 NaN)."""
-    p = make_problem(D=128, kv_type="q8_0", seed=43, **case)
+    prefetch failed exactly these cases (rows 31 / 63 NaN).  f16: the image
+    pair of tile s + 1 is filled while tile s computes from the other."""
+    p = make_problem(D=128, kv_type=kt, seed=43, **case)
     got, ref = run_gpu(p, kv_chunk=chunk), p.oracle()
     assert attn_rel_err(got, ref) <= RTOL
     assert attn_elem_err(got, ref) <= 1.0
 
 
+@pytest.mark.parametrize("kt", ["q8_0", "f16"])
 @pytest.mark.parametrize("chunk", [128, 384, 1024, 100000])
-def test_bd_chunking_invariance(dev, bd_force, chunk):
-    p = make_problem(D=128, NQ=64, H=4, N=2048, kv_type="q8_0", seed=27)
+def test_bd_chunking_invariance(dev, bd_force, chunk, kt):
+    p = make_problem(D=128, NQ=64, H=4, N=2048, kv_type=kt, seed=27)
     assert attn_rel_err(run_gpu(p, kv_chunk=chunk), p.oracle()) <= RTOL
 
 
-@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0", "f16"])
 def test_bd_extreme_rescale(dev, bd_force, kt):
     p = make_problem(D=128, NQ=64, H=2, N=2048, kv_type=kt, seed=28, extreme=True)
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
-@pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
+@pytest.mark.parametrize("kt", ["q8_0", "q4_0", "f16"])
 def test_bd_rescale_ramp(dev, bd_force, kt):
     p = make_problem(D=128, NQ=64, H=2, N=4096, kv_type=kt, seed=29, ramp=12.0, mask="none")
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
@@ -360,8 +471,9 @@ def test_bd_fully_masked_rows_are_nan(dev, bd_force):
     assert attn_rel_err(got, ref) <= RTOL
 
 
-def test_bd_deterministic(dev, bd_force):
-    p = make_problem(D=128, NQ=64, H=4, N=4096, kv_type="q8_0", seed=32)
+@pytest.mark.parametrize("kt", ["q8_0", "f16"])
+def test_bd_deterministic(dev, bd_force, kt):
+    p = make_problem(D=128, NQ=64, H=4, N=4096, kv_type=kt, seed=32)
     a, b = run_gpu(p), run_gpu(p)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
@@ -428,6 +540,9 @@ PF_CASES = [
     dict(kv_type="q8_0", NQ=100, H=2, Hkv=2, N=192, mask="neginf_blocks", S=2),  # odd tile count, 2 seqs
     dict(kv_type="q4_0", NQ=256, H=2, Hkv=2, N=64, mask="zero"),             # one tile
     dict(kv_type="q8_0", NQ=4, H=64, Hkv=1, N=128, mask="random"),           # R=64, QPT=4
+    dict(kv_type="q8_0", NQ=100, H=24, Hkv=4, N=256, mask="causal"),         # R=6: QPT=42, 252 rows a tile
+    dict(kv_type="q4_0", NQ=90, H=20, Hkv=4, N=192, mask="random"),          # R=5
+    dict(kv_type="f16", NQ=64, H=24, Hkv=2, N=128, mask="random"),           # R=12, QPT=21
     # f16 K/V: images filled by LDS-DMA straight from the rows
     dict(kv_type="f16", NQ=256, H=4, Hkv=4, N=256, mask="causal"),
     dict(kv_type="f16", NQ=100, H=8, Hkv=2, N=192, mask="random", layout="pos"),  # rows strided by Hkv
@@ -532,7 +647,8 @@ def test_pf_causal_block_skip(dev, kt, skip):
 
 def test_pf_f16_prefill_full(dev):
     """f16 K/V at the prefill shape (n_q = N = 4096, 32 heads, random mask): the
-    prefill kernel against the split-KV kernel, one head against the oracle."""
+    prefill kernel against the split-KV kernel, and every head x three
+    query-row blocks (start, middle, end of the sequence) against the oracle."""
     p = make_problem(D=128, NQ=4096, H=32, N=4096, kv_type="f16", seed=33)
     a = run_gpu(p)
     fattn.set_option(fattn.OPT_PF, 1)
@@ -542,6 +658,14 @@ def test_pf_f16_prefill_full(dev):
         fattn.set_option(fattn.OPT_PF, 0)
     assert np.isfinite(a).all()
     assert attn_rel_err(a, b) <= RTOL
+    rows = np.r_[0:128, 2048:2176, 3968:4096]
+    sub = make_problem(D=128, NQ=len(rows), H=32, N=4096, kv_type="f16", seed=33)
+    sub.q = np.ascontiguousarray(p.q[:, rows])
+    sub.k_bytes, sub.v_bytes = p.k_bytes, p.v_bytes
+    sub.mask_bits = np.ascontiguousarray(p.mask_bits[rows])
+    ref = sub.oracle(n_threads=16)
+    assert attn_rel_err(a[:, rows], ref) <= RTOL
+    assert attn_elem_err(a[:, rows], ref) <= 1.0
 
 
 def test_pf_prefill_full_matches_mq(dev):
