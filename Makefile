@@ -13,7 +13,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-functi
 CSRC := $(wildcard $(PKG)/csrc/*.hip)
 CHDR := $(wildcard $(PKG)/csrc/*.h) include/fattn.h
 
-.PHONY: all lib harness oracle clean asm stamps tests-hip probe isa
+.PHONY: all lib harness oracle clean asm stamps tests-hip probe isa variant
 
 all: lib harness oracle tests-hip probe isa
 
@@ -40,6 +40,18 @@ stamps: $(LIBDIR)/libfattn_stamps.so
 $(LIBDIR)/libfattn_stamps.so: $(STAMP_OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared $(STAMP_OBJS) -o $@
+
+# diagnostic / A-B variant of the library (never the product):
+#   make variant VAR=nr3 VFLAGS=-DFATTN_BDP_MAX_RAW=3  ->  lib/libfattn_nr3.so
+VAR ?= var
+VFLAGS ?=
+VAR_OBJS := $(patsubst $(PKG)/csrc/%.hip,$(OBJDIR)/$(VAR)_%.o,$(CSRC))
+$(OBJDIR)/$(VAR)_%.o: $(PKG)/csrc/%.hip $(CHDR)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $< -o $@
+variant: $(VAR_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared $(VAR_OBJS) -o $(LIBDIR)/libfattn_$(VAR).so
 
 harness: $(HARNESS)
 

@@ -334,8 +334,9 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     a.nbuf = 0;
     a.wave_bytes = 0;
-    pl.lds = pl.bdp ? (pl.kt == FATTN_TYPE_Q8_0 ? BdpCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
-                                                : BdpCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes)
+    const bool q8 = pl.kt == FATTN_TYPE_Q8_0;
+    pl.lds = pl.bdp && pl.D == 64 ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 64>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 64>::ldsBytes)
+             : pl.bdp             ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes)
              : pl.kt == FATTN_TYPE_Q8_0 ? BdCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
              : pl.kt == FATTN_TYPE_Q4_0 ? BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes
                                         : BdCfg<FATTN_TYPE_F16, 128>::ldsBytes;
@@ -468,11 +469,11 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // config 5, 64 rows, 15.5 vs 37.6 us at 4 heads; FATTN_OPT_MQ_MIN_ROWS)
     // (any rk2 <= 64: with R = rk2 not a power of two a tile packs
     // floor(rows / R) whole head groups and its last rows stay empty)
-    const bool mq_ok = !g_opt_mq_disable && !mixed && is_quant(k.type) && g16 && (D == 64 || D == 128 || D == 256) &&
-                       NQ * a.rk2 >= 32 && a.rk2 <= 64;
+    const bool heads_ok = NQ * a.rk2 >= 32 && a.rk2 <= 64;
+    const bool quant_ok = !g_opt_mq_disable && !mixed && is_quant(k.type) && g16 && heads_ok;
+    const bool mq_ok = quant_ok && (D == 64 || D == 128 || D == 256);
     // the same packing for f16 K/V rows (not transposed V): the prefill and
     // batched-decode kernels fill their f16 images by LDS-DMA straight from the rows
-    const bool heads_ok = NQ * a.rk2 >= 32 && a.rk2 <= 64;
     const bool f16_ok = !g_opt_mq_disable && !mixed && k.type == FATTN_TYPE_F16 && !v_trans && g16 && heads_ok;
     // Both 64-row-tile kernels (multi-query, batched decode) need every KV
     // chunk to hold at least two 128-key tiles: a workgroup with one tile is all
@@ -500,7 +501,8 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // the (kv head x query tile x seq) workgroups alone fill the chip
     // (f16 K/V rows, not transposed V: the same kernel, images filled by DMA)
     pl.pf = false;
-    if ((mq_ok || f16_ok) && g_opt_pf != 1 && (D == 64 || D == 128) && p->kv_chunk <= 0 && N % kPfKeys == 0 &&
+    if ((quant_ok || f16_ok) && g_opt_pf != 1 && (D == 64 || D == 96 || D == 128) && p->kv_chunk <= 0 &&
+        N % kPfKeys == 0 &&
         p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= pl.cus)) {
         pl.pf = true;
         pl.mq = false;
@@ -515,9 +517,11 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // chunk partials merged in a second launch; Q8_0 / Q4_0 and f16 K/V
     // (from 64 rows, when the chunks hold two tiles or more: `wide` above)
     // Q8_0 / Q4_0 take the compute / build-role form (fattn_bdp.h) unless
-    // FATTN_OPT_BD = 2 asks for the all-waves form
+    // FATTN_OPT_BD = 2 asks for the all-waves form; head dim 64 (Q8_0 / Q4_0)
+    // has the role form only, taken when FATTN_OPT_BD = 3 asks for it
     pl.bd = pl.bdp = false;
-    if (!pl.pf && g_opt_bd != 1 && (mq_ok || f16_ok) && D == 128 && N % kStep == 0 &&
+    const bool bd_dim = D == 128 || (D == 64 && mq_ok && g_opt_bd == 3);
+    if (!pl.pf && g_opt_bd != 1 && (mq_ok || f16_ok) && bd_dim && N % kStep == 0 &&
         (g_opt_bd >= 2 || (NQ * a.rk2 >= kBdRows && wide))) {
         pl.bd = true;
         pl.bdp = mq_ok && g_opt_bd != 2;
@@ -543,7 +547,9 @@ int make_plan(const fattn_params* p, Plan& pl) {
                    : pl.kt == FATTN_TYPE_Q8_0 ? PfCfg<FATTN_TYPE_Q8_0, DD>::ldsBytes
                                               : PfCfg<FATTN_TYPE_Q4_0, DD>::ldsBytes;
         };
-        pl.lds = D == 64 ? pf_lds(std::integral_constant<int, 64>()) : pf_lds(std::integral_constant<int, 128>());
+        pl.lds = D == 64   ? pf_lds(std::integral_constant<int, 64>())
+                 : D == 96 ? pf_lds(std::integral_constant<int, 96>())
+                           : pf_lds(std::integral_constant<int, 128>());
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
         // share the front of the workspace with the split-KV arrival words; a

@@ -12,13 +12,13 @@
 //  * per 64-key tile s, between two workgroup barriers, the compute waves run
 //    S^T = K.Q^T, the online softmax and O^T += V^T.P^T on tile s (one image
 //    pair) while the build waves dequantise raw tile s + 1 into the other pair
-//    and issue raw tile s + 4 into the raw slot they just emptied -- the
+//    and issue raw tile s + 1 + nRaw into the raw slot they just emptied -- the
 //    dequantisation VALU of one SIMD partner runs beside the matrix work of
 //    the other, and there is ONE barrier per tile (fattn_bd.h: the whole
 //    workgroup dequantises 128-key tile s between two barriers and then
 //    computes it, every SIMD idle on one pipe in each phase);
-//  * HBM -> LDS by buffer_load ... lds: raw tiles (three in flight, issued by
-//    the build waves), each compute wave's 32 x 32 mask block (two tiles in
+//  * HBM -> LDS by buffer_load ... lds: raw tiles (nRaw in flight -- as many
+//    as the LDS holds, Q8_0 4, Q4_0 5 -- issued by the build waves), each compute wave's 32 x 32 mask block (two tiles in
 //    flight, by the compute wave itself), Q's 64 f32 rows once before the loop
 //    (by all waves, into the second image pair's place);
 //  * dequantisation h(q * d) with one f16 rounding (src/utils.h:10-11), images
@@ -27,8 +27,8 @@
 //    merged by fattn_bd_merge_kernel when the KV is split).
 //
 // LDS (D = 128, Q8_0): [0, 64 KiB) two image pairs (K [8 dim slices][64 keys]
-// [32 B], V [4 dim blocks][64 keys][64 B]), then 3 raw tiles [K rows | V rows]
-// of 17 KiB, then 4 compute waves x 2 mask slots of 2 KiB: 130 KiB.
+// [32 B], V [4 dim blocks][64 keys][64 B]), then nRaw = 4 raw tiles [K rows |
+// V rows] of 17 KiB, then 4 compute waves x 2 mask slots of 2 KiB: 148 KiB.
 #pragma once
 
 #include "fattn_bd.h"
@@ -37,21 +37,29 @@ namespace fattn {
 
 constexpr int kBdpKeys = 64;      // keys per tile (two 32-key halves)
 constexpr int kBdpCompute = 4;    // waves 0..3 compute, 4..7 build
+#ifndef FATTN_BDP_MAX_RAW
+#define FATTN_BDP_MAX_RAW 5
+#endif
+constexpr int kBdpMaxRaw = FATTN_BDP_MAX_RAW;  // (diagnostic builds lower it for A/B runs)
 
 template <int KT, int D>
 struct BdpCfg {
-    static_assert(D == 128, "one ggml block per build wave");
+    static_assert(D == 128 || D == 64, "one ggml block (D = 128) or half-block (D = 64) per build wave");
     static_assert(KT == FATTN_TYPE_Q8_0 || KT == FATTN_TYPE_Q4_0, "quantised K/V (f16 takes fattn_bd.h's image ring)");
     static constexpr int rowB = row_bytes<KT, D>();
     static constexpr int kvRaw = kBdpKeys * rowB;                // raw K (or V) bytes per tile
     static constexpr int rawBytes = (2 * kvRaw + 15) / 16 * 16;  // [K rows | V rows]
-    static constexpr int nRaw = 3;
     static constexpr int img = kBdpKeys * D * 2;                 // one f16 image
     static constexpr int pair = 2 * img;
     static constexpr int rawOff = 2 * pair;
-    static constexpr int maskOff = rawOff + nRaw * rawBytes;
     static constexpr int maskSlot = 2048;                        // [4 key octets][32 rows][16 B]
-    static constexpr int maskEnd = maskOff + kBdpCompute * 2 * maskSlot;
+    static constexpr int maskBytes = kBdpCompute * 2 * maskSlot;
+    // raw tiles in flight: as many as the LDS holds beside the images and the
+    // mask slots, at most kBdpMaxRaw (Q8_0: 4 x 17 KiB, Q4_0: 5 x 9 KiB)
+    static constexpr int nRawFit = (163840 - rawOff - maskBytes) / rawBytes;
+    static constexpr int nRaw = nRawFit < kBdpMaxRaw ? nRawFit : kBdpMaxRaw;
+    static constexpr int maskOff = rawOff + nRaw * rawBytes;
+    static constexpr int maskEnd = maskOff + maskBytes;
     static constexpr int ldsBytes = maskEnd > BdPark<D, 2>::bytes ? maskEnd : BdPark<D, 2>::bytes;
     static constexpr int qOff = pair;                            // Q's f32 rows before the loop (pair 1)
     static constexpr int NI = (kvRaw + 1023) / 1024;             // 1-KiB DMA instructions per K (or V) tile
@@ -79,18 +87,21 @@ __device__ __forceinline__ void bdp_issue(const StepSrc& rs, int n0, uint32_t ld
     }
 }
 
-// build wave b: block b of key `lane` (both halves), K into dim slices 2b, 2b + 1
+// build wave bw: half-blocks D/64 bw .. + D/64 of key `lane` (D = 128: block bw,
+// both halves; D = 64: half bw & 1 of block bw >> 1), K into dim slice 2b + h
 // and V into dim block b, in the layouts fattn_bd.h / fattn_pf.h read
 template <int KT, int D>
-__device__ __forceinline__ void bdp_dequant(const uint8_t* raw, uint8_t* k16, uint8_t* v16, int b, int lane) {
+__device__ __forceinline__ void bdp_dequant(const uint8_t* raw, uint8_t* k16, uint8_t* v16, int bw, int lane) {
 #ifdef FATTN_MQ_NODEQ
     return;  // diagnostic build only
 #endif
     using C = BdpCfg<KT, D>;
     const int r = lane;
     const int sk = (r >> 3) & 1, sv = (r >> 2) & 3;
+    constexpr int HPW = D / 64;  // half-blocks per build wave
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int i = 0; i < HPW; i++) {
+        const int b = (HPW * bw + i) >> 1, h = (HPW * bw + i) & 1;
         u32x4 ck[2], cv[2];
         dequant_half<KT, D>(raw, r, b, h, ck);
         dequant_half<KT, D>(raw + C::kvRaw, r, b, h, cv);
@@ -103,12 +114,16 @@ __device__ __forceinline__ void bdp_dequant(const uint8_t* raw, uint8_t* k16, ui
     }
 }
 
-// build waves: at most n (0..2) raw groups issued after the awaited one in flight
+// build waves: at most n (0 .. nRaw - 1) raw groups issued after the awaited one in flight
 template <int KT, int D>
 __device__ __forceinline__ void bdp_build_wait(int n) {
     constexpr int NI = BdpCfg<KT, D>::ni_min;
-    if (n >= 2) wait_vmcnt_c<2 * NI>();
-    else if (n == 1) wait_vmcnt_c<NI>();
+    constexpr int NR = BdpCfg<KT, D>::nRaw;
+    static_assert(NR >= 2 && NR <= 5, "");
+    if (NR >= 5 && n >= 4) wait_vmcnt_c<4 * NI>();
+    else if (NR >= 4 && n >= 3) wait_vmcnt_c<3 * NI>();
+    else if (NR >= 3 && n >= 2) wait_vmcnt_c<2 * NI>();
+    else if (n >= 1) wait_vmcnt_c<NI>();
     else wait_vmcnt_c<0>();
 }
 
@@ -159,8 +174,10 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
     auto raw_lds = [&](int s) { return lds0 + C::rawOff + (s % C::nRaw) * C::rawBytes; };
     auto raw_ptr = [&](int s) { return smem + C::rawOff + (s % C::nRaw) * C::rawBytes; };
 
-    // ---- Q: 64 f32 rows -> LDS (pair 1's place) by 32 1-KiB DMA instructions,
-    // 4 per wave (fattn_bd.h's layout: row pr's 16-B chunk c at c ^ (pr & 31))
+    // ---- Q: 64 f32 rows -> LDS (pair 1's place) by D / 4 1-KiB DMA
+    // instructions, D / 32 per wave (fattn_bd.h's layout: row pr's 16-B chunk c
+    // of CPR = D / 4 at c ^ (pr % CPR))
+    constexpr int CPR = D / 4;
     {
         const i32x4 qs = make_srd(a.q + (int64_t)iq3 * a.q_nb3, a.q_span);
         constexpr int kQInst = kBdRows * D * 4 / 1024;
@@ -168,11 +185,11 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
 #pragma unroll
         for (int i = 0; i < kQInst / kBdWaves; i++) {
             const int j = wave + kBdWaves * i;
-            const int pr = 2 * j + (lane >> 5);
+            const int pr = (64 / CPR) * j + lane / CPR;
             const int rq = div_R(a, pr);
             const int q1 = qt * a.QPT + rq, q2 = ik2 * a.rk2 + (pr - rq * a.R);
             const uint32_t off = rq < a.QPT && q1 < a.NQ ? (uint32_t)q1 * (uint32_t)a.q_nb1 + (uint32_t)q2 * (uint32_t)a.q_nb2 +
-                                                 (((lane & 31) ^ (pr & 31)) * 16)
+                                                 (((lane % CPR) ^ (pr % CPR)) * 16)
                                            : a.q_span;
             dma<16>(qs, lds0 + C::qOff + j * 1024, off);
         }
@@ -200,7 +217,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
         if (ntiles > 0) mask_issue(0);
         if (ntiles > 1) mask_issue(1);
     } else {
-        for (int t = 0; t < min(3, ntiles); t++) bdp_issue<KT, D>(rs, c_lo + t * kBdpKeys, raw_lds(t), bw, lane);
+        for (int t = 0; t < min(C::nRaw, ntiles); t++) bdp_issue<KT, D>(rs, c_lo + t * kBdpKeys, raw_lds(t), bw, lane);
     }
     FATTN_STAMP(1);
     if (compute) {
@@ -210,7 +227,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
         else if (nm == 1) wait_vmcnt_c<NM>();
         else wait_vmcnt_c<0>();
     } else {
-        bdp_build_wait<KT, D>(min(2, ntiles - 1));  // raw 0 (and Q) landed
+        bdp_build_wait<KT, D>(min(C::nRaw - 1, ntiles - 1));  // raw 0 (and Q) landed
     }
     __syncthreads();  // Q and raw 0 complete in LDS
     f16x8 qop[NK];
@@ -218,8 +235,8 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
 #pragma unroll
         for (int kk = 0; kk < NK; kk++) {
             const float* qr = (const float*)(smem + C::qOff) + p * D;
-            const f32x4 x0 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h) ^ (p & 31)));
-            const f32x4 x1 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h + 1) ^ (p & 31)));
+            const f32x4 x0 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h) ^ (p % CPR)));
+            const f32x4 x1 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h + 1) ^ (p % CPR)));
             f16x8 hq;
             hq.s0 = (f16)x0.x; hq.s1 = (f16)x0.y; hq.s2 = (f16)x0.z; hq.s3 = (f16)x0.w;
             hq.s4 = (f16)x1.x; hq.s5 = (f16)x1.y; hq.s6 = (f16)x1.z; hq.s7 = (f16)x1.w;
@@ -231,12 +248,12 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
     } else {
         if (ntiles > 0) {
             bdp_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, bw, lane);
-            if (ntiles > 3) {
+            if (ntiles > C::nRaw) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot 0 read out
-                bdp_issue<KT, D>(rs, c_lo + 3 * kBdpKeys, raw_lds(3), bw, lane);
+                bdp_issue<KT, D>(rs, c_lo + C::nRaw * kBdpKeys, raw_lds(C::nRaw), bw, lane);
             }
-            // raw 1 landed (raw 2, raw 3 may fly on)
-            if (ntiles > 1) bdp_build_wait<KT, D>(min(2, ntiles - 2));
+            // raw 1 landed (raw 2 .. nRaw may fly on)
+            if (ntiles > 1) bdp_build_wait<KT, D>(min(C::nRaw - 1, ntiles - 2));
         }
     }
     FATTN_STAMP(2);
@@ -263,6 +280,12 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
         vbase[e] = C::img + kh * 2048 + row * 64 + ch * 16 + (gi & 1) * 8;
     }
 
+    // (diagnostic build only, FATTN_STAMPS, tools/stamps_bd.py --form bdp: 0
+    // start, 1 prologue issued, 2 prologue done, 3 + s past tile s's barrier,
+    // 7 + s tile s's work done -- compute: tile s computed and mask s + 1
+    // landed; build: raw s + 1 dequantised and raw s + 2 landed -- (s < 4),
+    // 11 loop done, 12 states parked, 13 partials stored; build waves, tile 2:
+    // 14 dequantised, 15 raw 6 issued)
     for (int s = 0; s < ntiles; s++) {
         // pair s % 2 holds tile s (built before this barrier by the build
         // waves); every compute wave is done with tile s - 1, so pair
@@ -270,17 +293,20 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
         __syncthreads();
         if (s < 4) FATTN_STAMP(3 + s);
         if (!compute) {
-            // ---- build: raw s + 1 -> pair (s + 1) % 2; raw s + 4 into its slot;
+            // ---- build: raw s + 1 -> pair (s + 1) % 2; raw s + 1 + nRaw into its slot;
             // then wait for this wave's pieces of raw s + 2
             if (s + 1 < ntiles) {
                 bdp_dequant<KT, D>(raw_ptr(s + 1), smem + ((s + 1) & 1) * C::pair,
                                    smem + ((s + 1) & 1) * C::pair + C::img, bw, lane);
-                if (s + 4 < ntiles) {
+                if (s + 1 + C::nRaw < ntiles) {
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot has been read
-                    bdp_issue<KT, D>(rs, c_lo + (s + 4) * kBdpKeys, raw_lds(s + 4), bw, lane);
+                    if (s == 2) FATTN_STAMP(14);
+                    bdp_issue<KT, D>(rs, c_lo + (s + 1 + C::nRaw) * kBdpKeys, raw_lds(s + 1 + C::nRaw), bw, lane);
+                    if (s == 2) FATTN_STAMP(15);
                 }
-                if (s + 2 < ntiles) bdp_build_wait<KT, D>(min(2, ntiles - 3 - s));
+                if (s + 2 < ntiles) bdp_build_wait<KT, D>(min(C::nRaw - 1, ntiles - 3 - s));
             }
+            if (s < 4) FATTN_STAMP(7 + s);
             continue;
         }
         // ---- compute tile s.  This lane's mask values (keys 8 u + 4 h + 0..3 of
@@ -386,6 +412,14 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
                 else wait_vmcnt_c<0>();
             }
         }
+#ifdef FATTN_STAMPS
+        if (s < 4) {
+            float z = 0.0f;
+            for (int db = 0; db < NDB; db++) z += o[db][0];
+            asm volatile("" ::"v"(z));  // the MFMA results are in before the stamp
+            FATTN_STAMP(7 + s);
+        }
+#endif
     }
     FATTN_STAMP(11);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");

@@ -178,28 +178,32 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     });
 }
 
-template <int KT, bool HM>
+// D = 128: the all-waves form, or the role form for quantised K/V (pl.bdp);
+// D = 64: the role form only (the planner sets pl.bdp)
+template <int KT, int D, bool HM>
 int launch_bd_hm(const Plan& pl, hipStream_t st, const Events& ev) {
-    auto kern = fattn_bd_kernel<KT, 128, HM>;
-    if constexpr (KT != FATTN_TYPE_F16) {  // (the role form: quantised K/V only)
-        if (pl.bdp) kern = fattn_bdp_kernel<KT, 128, HM>;
+    void (*kern)(SplitArgs) = nullptr;
+    if constexpr (D == 128) kern = fattn_bd_kernel<KT, D, HM>;
+    if constexpr (KT != FATTN_TYPE_F16) {
+        if (pl.bdp) kern = fattn_bdp_kernel<KT, D, HM>;
     }
+    if (kern == nullptr || (D != 128 && !pl.bdp)) return FATTN_ERR_UNSUPPORTED_TYPE;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         hipLaunchKernelGGL(kern, pl.grid, dim3(kBdWaves * kWave), pl.lds, st, pl.a);
         if (pl.a.merge_launch == 1) {
             const dim3 g(kBdRows / 4, pl.grid.y, pl.grid.z);
-            const int need = (pl.a.n_chunks + merge_ppr<128>() - 1) / merge_ppr<128>();
-            if (need <= 2) hipLaunchKernelGGL((fattn_bd_merge_kernel<128, 2>), g, dim3(256), 0, st, pl.a);
-            else if (need <= 4) hipLaunchKernelGGL((fattn_bd_merge_kernel<128, 4>), g, dim3(256), 0, st, pl.a);
-            else if (need <= 8) hipLaunchKernelGGL((fattn_bd_merge_kernel<128, 8>), g, dim3(256), 0, st, pl.a);
-            else hipLaunchKernelGGL((fattn_bd_merge_kernel<128, 16>), g, dim3(256), 0, st, pl.a);
+            const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
+            if (need <= 2) hipLaunchKernelGGL((fattn_bd_merge_kernel<D, 2>), g, dim3(256), 0, st, pl.a);
+            else if (need <= 4) hipLaunchKernelGGL((fattn_bd_merge_kernel<D, 4>), g, dim3(256), 0, st, pl.a);
+            else if (need <= 8) hipLaunchKernelGGL((fattn_bd_merge_kernel<D, 8>), g, dim3(256), 0, st, pl.a);
+            else hipLaunchKernelGGL((fattn_bd_merge_kernel<D, 16>), g, dim3(256), 0, st, pl.a);
         }
     });
 }
 
-template <int KT>
+template <int KT, int D>
 int launch_bd(const Plan& pl, hipStream_t st, const Events& ev) {
-    return pl.a.has_mask ? launch_bd_hm<KT, true>(pl, st, ev) : launch_bd_hm<KT, false>(pl, st, ev);
+    return pl.a.has_mask ? launch_bd_hm<KT, D, true>(pl, st, ev) : launch_bd_hm<KT, D, false>(pl, st, ev);
 }
 
 template <int KT, int D>
@@ -231,7 +235,7 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
     if constexpr (D == 64 || D == 128 || D == 256) {
         if (pl.kt != pl.vt && pl.vt != VT_F16T) return launch_mixed<D>(pl, st, ev);
     }
-    if constexpr (D == 64 || D == 128) {
+    if constexpr (D == 64 || D == 96 || D == 128) {
         if (pl.pf) {
             if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_pf<FATTN_TYPE_F16, D>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0, D>(pl, st, ev);
@@ -239,11 +243,13 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
     }
-    if constexpr (D == 128) {
+    if constexpr (D == 64 || D == 128) {
         if (pl.bd) {
-            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_bd<FATTN_TYPE_Q8_0>(pl, st, ev);
-            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_bd<FATTN_TYPE_Q4_0>(pl, st, ev);
-            if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_bd<FATTN_TYPE_F16>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_bd<FATTN_TYPE_Q8_0, D>(pl, st, ev);
+            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_bd<FATTN_TYPE_Q4_0, D>(pl, st, ev);
+            if constexpr (D == 128) {
+                if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_bd<FATTN_TYPE_F16, D>(pl, st, ev);
+            }
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
     }

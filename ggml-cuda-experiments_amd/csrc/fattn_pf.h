@@ -51,7 +51,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <int KT, int D>
 struct PfCfg {
-    static_assert(D == 64 || D == 128, "at most one half ggml block per wave and row");
+    static_assert(D == 64 || D == 96 || D == 128, "at most one half ggml block per wave and row");
     static constexpr int NT = kPfWaves * kWave;
     // f16 K/V: LDS-DMA straight into the images (no raw tiles, no dequantisation);
     // three image pairs: tile s in use, s+1 and s+2 in flight
@@ -97,17 +97,17 @@ __device__ __forceinline__ void pf_issue(const StepSrc& rs, int n0, uint32_t lds
 // (any 16-B aligned stride).
 template <int D>
 struct PfDirect {
-    static constexpr int NJ = kPfKeys * D * 2 / 1024;  // 1-KiB pieces per image
+    static constexpr int NJ = kPfKeys * D * 2 / 1024;  // 1-KiB pieces per image (D = 96: 12)
     static constexpr int NIW = 2 * NJ / kPfWaves;      // DMA instructions per wave and tile
-    static_assert(kPfWaves == 8 && NIW * kPfWaves == 2 * NJ && NJ % kPfWaves == 0, "");
+    static_assert(kPfWaves == 8 && NIW * kPfWaves == 2 * NJ && NIW <= 4, "every wave the same count");
 };
 template <int D>
 __device__ __forceinline__ void pf_direct_offsets(const SplitArgs& a, int wave, int lane, uint32_t (&off)[4]) {
     constexpr int NJ = PfDirect<D>::NJ;
 #pragma unroll
     for (int i = 0; i < PfDirect<D>::NIW; i++) {
-        const int j = wave + 8 * i;
-        if (i < PfDirect<D>::NIW / 2) {  // K: slice kk = j / 2, rows 32 (j & 1) + lane / 2, stored half lane & 1
+        const int j = wave + 8 * i;      // (wave-uniform; K pieces first)
+        if (j < NJ) {  // K: slice kk = j / 2, rows 32 (j & 1) + lane / 2, stored half lane & 1
             const int kk = j >> 1, r = 32 * (j & 1) + (lane >> 1), hh = lane & 1;
             off[i] = (uint32_t)r * (uint32_t)a.k_nb1 + kk * 32 + ((hh ^ ((r >> 3) & 1)) * 16);
         } else {  // V: dim block db = jj / 4, rows 16 (jj & 3) + lane / 4, stored chunk lane & 3
@@ -128,7 +128,7 @@ __device__ __forceinline__ void pf_direct_issue(const SplitArgs& a, const StepSr
 #pragma unroll
     for (int i = 0; i < PfDirect<D>::NIW; i++) {
         const int j = wave + 8 * i;
-        if (i < PfDirect<D>::NIW / 2)
+        if (j < NJ)
             dma<16>(rs.k, pair_lds + j * 1024, nk + off[i]);
         else
             dma<16>(rs.v, pair_lds + PfCfg<FATTN_TYPE_F16, D>::img + (j - NJ) * 1024, nv + off[i]);

@@ -419,6 +419,38 @@ def test_bdp_matches_bd_bitwise_inputs(dev):
     assert attn_rel_err(a, p.oracle()) <= RTOL
 
 
+# head dim 64: the role form with one half-block per build wave (FATTN_OPT_BD = 3)
+BDP64_CASES = [
+    dict(kv_type="q8_0", NQ=64, H=8, Hkv=8, N=4096, mask="random"),
+    dict(kv_type="q4_0", NQ=64, H=4, Hkv=4, N=2048, mask="random"),
+    dict(kv_type="q8_0", NQ=16, H=16, Hkv=4, N=1024, mask="causal"),
+    dict(kv_type="q4_0", NQ=40, H=12, Hkv=4, N=768, mask="random"),          # R = 3
+    dict(kv_type="q8_0", NQ=40, H=2, Hkv=2, N=800, mask="random"),           # ragged rows, partial tile
+    dict(kv_type="q8_0", NQ=64, H=2, Hkv=2, N=192, mask="neginf_blocks"),
+    dict(kv_type="q4_0", NQ=64, H=4, Hkv=2, N=640, mask="tail", S=2, Skv=1),
+    dict(kv_type="q8_0", NQ=64, H=4, Hkv=4, N=1024, mask="none"),
+]
+
+
+@pytest.mark.parametrize("case", BDP64_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_bdp_d64(dev, bdp_force, case):
+    p = make_problem(D=64, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000 + 9, **case)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert "fattn_bdp_kernel" in d and "D64" in d, d
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
+@pytest.mark.parametrize("chunk", [128, 1024])
+def test_bdp_d64_chunking(dev, bdp_force, chunk):
+    p = make_problem(D=64, NQ=64, H=4, N=2048, kv_type="q8_0", mask="causal", seed=46)
+    got, ref = run_gpu(p, kv_chunk=chunk), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 @pytest.mark.parametrize("case,chunk", [
     (dict(NQ=1024, H=8, N=1024, mask="causal"), 0),   # 16 query tiles x 2 chunks of 4 tiles
     (dict(NQ=1024, H=8, N=1024, mask="random"), 0),
@@ -574,6 +606,29 @@ def test_pf_d64(dev, pf_force, case):
     t = upload(p, dev)
     d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
     assert "fattn_pf_kernel" in d and "D64" in d, d
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
+PF96_CASES = [
+    dict(kv_type="q8_0", NQ=256, H=4, Hkv=4, N=512, mask="causal"),           # 102-B rows
+    dict(kv_type="q4_0", NQ=300, H=2, Hkv=2, N=256, mask="random"),           # 54-B rows, ragged tiles
+    dict(kv_type="q8_0", NQ=64, H=24, Hkv=4, N=192, mask="zero"),             # R = 6 (QPT 42)
+    dict(kv_type="f16", NQ=256, H=4, Hkv=4, N=256, mask="neginf_blocks"),     # 192-B rows, direct fill
+    dict(kv_type="f16", NQ=100, H=8, Hkv=2, N=128, mask="none", layout="pos", S=2),
+]
+
+
+@pytest.mark.parametrize("case", PF96_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_pf_d96(dev, pf_force, case):
+    """The prefill kernel at D = 96: six K dim slices /
+    three V dim blocks per image, waves 0-5 dequantise (one half block each);
+    f16: 24 1-KiB image pieces per tile, three per wave."""
+    p = make_problem(D=96, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000, **case)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert "fattn_pf_kernel" in d and "D96" in d, d
     got, ref = run_gpu(p), p.oracle()
     assert attn_rel_err(got, ref) <= RTOL
     assert attn_elem_err(got, ref) <= 1.0

@@ -21,3 +21,8 @@ run c5q4_bd 200 python bench.py $B --kv-type q4_0 --bd 2; line "cfg5-shape q4_0 
 run c5q4_bdp 200 python bench.py $B --kv-type q4_0 --bd 3; line "cfg5-shape q4_0 bdp" c5q4_bdp
 grep -E "passed|failed" gpurun_out/t_bdp.log | tail -2 > $F/tests_tail.txt
 cat $F/tests_tail.txt $F/ab.txt
+# per-kernel durations (attention kernel vs the merge launch), both forms
+run kt_bd 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4b_kt_bd -o kt -- python3 bench.py $B --bd 2
+run kt_bdp 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4b_kt_bdp -o kt -- python3 bench.py $B --bd 3
+for f in $(find gpurun_out/r4b_kt_bd gpurun_out/r4b_kt_bdp -name "*kernel_stats.csv"); do echo "== $f"; python3 tools/kstats.py $f; done > $F/kstats.txt 2>&1
+cat $F/kstats.txt

@@ -5,7 +5,12 @@ Stamps (s_memrealtime, 100 MHz = 10 ns) per wave, g_stamps[block][16][16],
 fattn_bd.h: 0 start, 1 prologue issued, 2 Q ready, 3 + 2s tile s landed, 4 + 2s
 tile s computed (s < 4), 14 / 15 tile 0 past barrier 1 / 2, 11 loop done,
 12 states parked, 13 stores drained.
-Usage: python tools/stamps_bd.py [--heads 4] [--kv-len 4096] [--n-q 64] [--kv-chunk 0]
+--form bdp (fattn_bdp.h, FATTN_OPT_BD = 3): 0 start, 1 prologue issued, 2
+prologue done, 3 + s past tile s's barrier, 7 + s tile s's work done (compute
+waves 0-3: tile s computed; build waves 4-7: raw s + 1 dequantised and raw
+s + 2 landed), s < 4; 11 loop done, 12 states parked, 13 partials stored --
+printed per role.
+Usage: python tools/stamps_bd.py [--form bd|bdp] [--heads 4] [--kv-len 4096] [--n-q 64] [--kv-chunk 0]
 """
 import argparse
 import ctypes as C
@@ -36,7 +41,9 @@ def main():
     ap.add_argument("--heads", type=int, default=4)
     ap.add_argument("--kv-len", type=int, default=4096)
     ap.add_argument("--n-q", type=int, default=64)
+    ap.add_argument("--form", default="bd", choices=["bd", "bdp"])
     args = ap.parse_args()
+    fattn.set_option(fattn.OPT_BD, 2 if args.form == "bd" else 3)
     dev = torch.device("cuda:0")
     D, H, N, NQ = 128, args.heads, args.kv_len, args.n_q
     typ = fattn.TYPE_NAMES[args.kv_type]
@@ -73,11 +80,25 @@ def main():
     print(f"blocks {nblk}  waves {live.sum()}  stamp span {(s.max() - t0) * 0.01:.2f} us")
     pct = lambda a: " ".join(f"{np.percentile(a, p):6.2f}" for p in (0, 10, 50, 90, 100)) if len(a) else "   -"
     print("                              min    p10    p50    p90    max  (us since the first wave's start)")
-    for k in (0, 1, 2, 3, 14, 15, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13):
-        v = s[:, :, k]
-        m = live & (v > 0)
-        if m.any():
-            print(f"{NAMES[k]:28s}", pct((v[m] - t0) * 0.01))
+    if args.form == "bd":
+        for k in (0, 1, 2, 3, 14, 15, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13):
+            v = s[:, :, k]
+            m = live & (v > 0)
+            if m.any():
+                print(f"{NAMES[k]:28s}", pct((v[m] - t0) * 0.01))
+        return
+    names = {0: "start", 1: "prologue issued", 2: "prologue done", 11: "loop done", 12: "states parked",
+             13: "partials stored", 14: "tile 2: raw 3 dequantised", 15: "tile 2: raw 6 issued"}
+    for s_ in range(4):
+        names[3 + s_] = f"past tile {s_} barrier"
+        names[7 + s_] = f"tile {s_} work done"
+    for role, ws in (("compute waves 0-3", slice(0, 4)), ("build waves 4-7", slice(4, 8))):
+        print(f"-- {role}")
+        for k in (0, 1, 2, 3, 7, 4, 8, 5, 14, 15, 9, 6, 10, 11, 12, 13):
+            v = s[:, ws, k]
+            m = live[:, ws] & (v > 0)
+            if m.any():
+                print(f"{names[k]:28s}", pct((v[m] - t0) * 0.01))
     print("per-wave durations (us)      min    p10    p50    p90    max")
     for a_, b_, name in ((0, 1, "start -> prologue issued"), (1, 2, "-> Q ready"), (2, 3, "Q ready -> tile 0 landed"),
                          (3, 14, "-> barrier 1"), (14, 15, "-> V image (barrier 2)"), (15, 4, "-> tile 0 computed"),
