@@ -12,7 +12,7 @@
 //  * per 64-key tile s, between two workgroup barriers, the compute waves run
 //    S^T = K.Q^T, the online softmax and O^T += V^T.P^T on tile s (one image
 //    pair) while the build waves dequantise raw tile s + 1 into the other pair
-//    and issue raw tile s + 1 + nRaw into the raw slot they just emptied -- the
+//    and issue raw tile s + nRaw into the raw slot they all emptied before the barrier -- the
 //    dequantisation VALU of one SIMD partner runs beside the matrix work of
 //    the other, and there is ONE barrier per tile (fattn_bd.h: the whole
 //    workgroup dequantises 128-key tile s between two barriers and then
@@ -248,12 +248,10 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
     } else {
         if (ntiles > 0) {
             bdp_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, bw, lane);
-            if (ntiles > C::nRaw) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot 0 read out
-                bdp_issue<KT, D>(rs, c_lo + C::nRaw * kBdpKeys, raw_lds(C::nRaw), bw, lane);
-            }
-            // raw 1 landed (raw 2 .. nRaw may fly on)
-            if (ntiles > 1) bdp_build_wait<KT, D>(min(C::nRaw - 1, ntiles - 2));
+            // raw 1 landed (raw 2 .. nRaw - 1 may fly on).  Raw nRaw goes into
+            // slot 0 after the loop's first barrier: every build wave reads all
+            // of a slot's rows, so a slot is free only once they all have.
+            if (ntiles > 1) bdp_build_wait<KT, D>(min(C::nRaw - 2, ntiles - 2));
         }
     }
     FATTN_STAMP(2);
@@ -285,7 +283,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
     // 7 + s tile s's work done -- compute: tile s computed and mask s + 1
     // landed; build: raw s + 1 dequantised and raw s + 2 landed -- (s < 4),
     // 11 loop done, 12 states parked, 13 partials stored; build waves, tile 2:
-    // 14 dequantised, 15 raw 6 issued)
+    // 14 before and 15 after issuing raw 2 + nRaw)
     for (int s = 0; s < ntiles; s++) {
         // pair s % 2 holds tile s (built before this barrier by the build
         // waves); every compute wave is done with tile s - 1, so pair
@@ -293,18 +291,16 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
         __syncthreads();
         if (s < 4) FATTN_STAMP(3 + s);
         if (!compute) {
-            // ---- build: raw s + 1 -> pair (s + 1) % 2; raw s + 1 + nRaw into its slot;
-            // then wait for this wave's pieces of raw s + 2
+            // ---- build: raw s + nRaw into raw s's slot (every build wave read it
+            // before this barrier); raw s + 1 -> pair (s + 1) % 2; then wait for
+            // this wave's pieces of raw s + 2 (raw s + 3 .. s + nRaw may fly on)
+            if (s == 2) FATTN_STAMP(14);
+            if (s + C::nRaw < ntiles) bdp_issue<KT, D>(rs, c_lo + (s + C::nRaw) * kBdpKeys, raw_lds(s + C::nRaw), bw, lane);
+            if (s == 2) FATTN_STAMP(15);
             if (s + 1 < ntiles) {
                 bdp_dequant<KT, D>(raw_ptr(s + 1), smem + ((s + 1) & 1) * C::pair,
                                    smem + ((s + 1) & 1) * C::pair + C::img, bw, lane);
-                if (s + 1 + C::nRaw < ntiles) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot has been read
-                    if (s == 2) FATTN_STAMP(14);
-                    bdp_issue<KT, D>(rs, c_lo + (s + 1 + C::nRaw) * kBdpKeys, raw_lds(s + 1 + C::nRaw), bw, lane);
-                    if (s == 2) FATTN_STAMP(15);
-                }
-                if (s + 2 < ntiles) bdp_build_wait<KT, D>(min(C::nRaw - 1, ntiles - 3 - s));
+                if (s + 2 < ntiles) bdp_build_wait<KT, D>(min(C::nRaw - 2, ntiles - 3 - s));
             }
             if (s < 4) FATTN_STAMP(7 + s);
             continue;

@@ -88,7 +88,7 @@ def main():
                 print(f"{NAMES[k]:28s}", pct((v[m] - t0) * 0.01))
         return
     names = {0: "start", 1: "prologue issued", 2: "prologue done", 11: "loop done", 12: "states parked",
-             13: "partials stored", 14: "tile 2: raw 3 dequantised", 15: "tile 2: raw 6 issued"}
+             13: "partials stored", 14: "tile 2: raw issue begins", 15: "tile 2: raw 2+nRaw issued"}
     for s_ in range(4):
         names[3 + s_] = f"past tile {s_} barrier"
         names[7 + s_] = f"tile {s_} work done"
