@@ -310,7 +310,7 @@ def parse_args(argv=None):
     ap.add_argument("--pf-stagger", type=int, default=2)
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--no-mq", action="store_true", help="never pick the multi-query kernel (split-KV kernel only)")
-    ap.add_argument("--bd", type=int, default=0, help="batched-decode kernel: 0 auto, 1 never, 2 whenever eligible")
+    ap.add_argument("--bd", type=int, default=0, help="batched-decode kernel: 0 auto, 1 never, 2 all-waves form, 3 role form (fattn.h FATTN_OPT_BD)")
     ap.add_argument("--merge-in-kernel", type=int, default=0,
                     help="multi-row chunk merge: 0 second launch, 1 in-kernel when the grid is co-resident")
     ap.add_argument("--split-prio", type=int, default=0,

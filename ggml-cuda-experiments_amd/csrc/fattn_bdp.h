@@ -18,7 +18,8 @@
 //    workgroup dequantises 128-key tile s between two barriers and then
 //    computes it, every SIMD idle on one pipe in each phase);
 //  * HBM -> LDS by buffer_load ... lds: raw tiles (nRaw in flight -- as many
-//    as the LDS holds, Q8_0 4, Q4_0 5 -- issued by the build waves), each compute wave's 32 x 32 mask block (two tiles in
+//    as the LDS holds, Q8_0 4, Q4_0 5 -- issued by all eight waves once a
+//    tile has 8 or more 1-KiB pieces, else by the build waves), each compute wave's 32 x 32 mask block (two tiles in
 //    flight, by the compute wave itself), Q's 64 f32 rows once before the loop
 //    (by all waves, into the second image pair's place);
 //  * dequantisation h(q * d) with one f16 rounding (src/utils.h:10-11), images
@@ -63,27 +64,57 @@ struct BdpCfg {
     static constexpr int ldsBytes = maskEnd > BdPark<D, 2>::bytes ? maskEnd : BdPark<D, 2>::bytes;
     static constexpr int qOff = pair;                            // Q's f32 rows before the loop (pair 1)
     static constexpr int NI = (kvRaw + 1023) / 1024;             // 1-KiB DMA instructions per K (or V) tile
-    // raw instructions j = 0 .. 2 NI - 1 (K then V) go to build wave 4 + j % 4;
-    // the smallest per-wave group counts every build wave's waits (a wave with
-    // one more instruction also waits for one of the next group: fattn_pf.h)
-    static constexpr int ni_min = (2 * NI) / 4;
+    // Raw instructions j = 0 .. T - 1 (K then V) of a tile.  From 8 of them on,
+    // ALL eight waves issue them (the CU's LDS-DMA throughput grows with the
+    // number of issuing waves: with the build waves alone each issue stalled
+    // ~1.2 us per tile on config 5, profiles/r04_d): j -> wave j % 8, the
+    // remainder to the build waves first (or one more to every compute wave
+    // when more than four are left), so the compute waves' counts are equal
+    // -- their waits sit right behind the youngest group and must count it
+    // exactly.  Fewer than 8: the build waves, j -> 4 + j % 4.  The smallest
+    // per-role count counts the waits (a build wave with one more instruction
+    // also waits for one of a younger group: fattn_pf.h).
+    static constexpr int T = 2 * NI;
+#ifdef FATTN_BDP_BUILD_ISSUE
+    static constexpr bool kAll = false;  // diagnostic build only (A/B)
+#else
+    static constexpr bool kAll = T >= 8;
+#endif
+    static constexpr int kBase = T / 8, kRem = T % 8;
+    static constexpr int owner(int j) {
+        return !kAll ? 4 + j % 4
+               : j < 8 * kBase ? j % 8
+               : kRem <= 4     ? 4 + (j - 8 * kBase)
+               : j - 8 * kBase < 4 ? j - 8 * kBase
+                                   : 4 + (j - 8 * kBase - 4);
+    }
+    static constexpr int R_c = kAll ? kBase + (kRem > 4 ? 1 : 0) : 0;  // per compute wave (exact)
+    static constexpr int R_b = kAll ? kBase : T / 4;                   // per build wave (smallest)
     static constexpr int NM = 2;                                 // mask DMA instructions per compute wave and tile
     static_assert(kBdRows * D * 4 <= pair, "Q rows in the second pair's place");
+    static_assert(nRaw >= 3, "a compute wave's raw s + 2 is older than its mask s + 1");
     static_assert(ldsBytes <= 163840, "");
 };
 
+// (the K/V DMA without the non-temporal policy: config 5 24.4-24.7 vs
+// 25.1-25.3 us with it, profiles/r04_d)
+constexpr bool kBdpNT = false;
+
+// this wave's raw instructions of the tile at key n0 (BdpCfg::owner)
 template <int KT, int D>
-__device__ __forceinline__ void bdp_issue(const StepSrc& rs, int n0, uint32_t lds, int bw, int lane) {
+__device__ __forceinline__ void bdp_issue(const StepSrc& rs, int n0, uint32_t lds, int wave, int lane) {
 #ifdef FATTN_MQ_NOMEM
     return;  // diagnostic build only
 #endif
     using C = BdpCfg<KT, D>;
-    for (int j = bw; j < 2 * C::NI; j += 4) {  // wave-uniform
+#pragma unroll
+    for (int j = 0; j < C::T; j++) {
+        if (C::owner(j) != wave) continue;  // wave-uniform
         const bool is_v = j >= C::NI;
         const int i = is_v ? j - C::NI : j;
         const int byte = i * 1024 + lane * 16;
         if (C::kvRaw % 1024 == 0 || byte < C::kvRaw)  // pieces past the tile's bytes idle (the instruction counts)
-            dma<16, kDecodeNT>(is_v ? rs.v : rs.k, lds + (is_v ? C::kvRaw : 0) + i * 1024, (uint32_t)n0 * C::rowB + byte);
+            dma<16, kBdpNT>(is_v ? rs.v : rs.k, lds + (is_v ? C::kvRaw : 0) + i * 1024, (uint32_t)n0 * C::rowB + byte);
     }
 }
 
@@ -117,7 +148,7 @@ __device__ __forceinline__ void bdp_dequant(const uint8_t* raw, uint8_t* k16, ui
 // build waves: at most n (0 .. nRaw - 1) raw groups issued after the awaited one in flight
 template <int KT, int D>
 __device__ __forceinline__ void bdp_build_wait(int n) {
-    constexpr int NI = BdpCfg<KT, D>::ni_min;
+    constexpr int NI = BdpCfg<KT, D>::R_b;
     constexpr int NR = BdpCfg<KT, D>::nRaw;
     static_assert(NR >= 2 && NR <= 5, "");
     if (NR >= 5 && n >= 4) wait_vmcnt_c<4 * NI>();
@@ -125,6 +156,26 @@ __device__ __forceinline__ void bdp_build_wait(int n) {
     else if (NR >= 3 && n >= 2) wait_vmcnt_c<2 * NI>();
     else if (n >= 1) wait_vmcnt_c<NI>();
     else wait_vmcnt_c<0>();
+}
+
+// compute waves: at most `raws` raw groups (R_c instructions each) and `masks`
+// (0 / 1) mask groups issued after the awaited instruction in flight
+template <int KT, int D, int NM>
+__device__ __forceinline__ void bdp_compute_wait(int raws, int masks) {
+    constexpr int R = BdpCfg<KT, D>::R_c;
+    switch (__builtin_amdgcn_readfirstlane(2 * raws + masks)) {
+        case 0: wait_vmcnt_c<0>(); break;
+        case 1: wait_vmcnt_c<NM>(); break;
+        case 2: wait_vmcnt_c<R>(); break;
+        case 3: wait_vmcnt_c<R + NM>(); break;
+        case 4: wait_vmcnt_c<2 * R>(); break;
+        case 5: wait_vmcnt_c<2 * R + NM>(); break;
+        case 6: wait_vmcnt_c<3 * R>(); break;
+        case 7: wait_vmcnt_c<3 * R + NM>(); break;
+        case 8: wait_vmcnt_c<4 * R>(); break;
+        case 9: wait_vmcnt_c<4 * R + NM>(); break;
+        default: wait_vmcnt_c<0>(); break;  // (not reached: raws <= nRaw - 1 <= 4)
+    }
 }
 
 template <int KT, int D, bool HM>
@@ -210,25 +261,19 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
         }
     };
 
-    // ---- prologue.  Compute waves: Q | mask 0 | mask 1.  Build waves: Q | raw 0
-    // | raw 1 | raw 2, then (after the barrier that completes raw 0) raw 0 ->
-    // pair 0 and raw 3 into its slot.
+    // ---- prologue.  Compute waves: Q | mask 0 | mask 1 | their pieces of raw
+    // 0 .. nRaw - 1.  Build waves: Q | their pieces of raw 0 .. nRaw - 1; after
+    // the barrier that completes raw 0 they dequantise it into pair 0.
+    const int npro = min(C::nRaw, ntiles);  // raw tiles of the prologue
     if (compute) {
         if (ntiles > 0) mask_issue(0);
         if (ntiles > 1) mask_issue(1);
-    } else {
-        for (int t = 0; t < min(C::nRaw, ntiles); t++) bdp_issue<KT, D>(rs, c_lo + t * kBdpKeys, raw_lds(t), bw, lane);
     }
+    for (int t = 0; t < npro; t++) bdp_issue<KT, D>(rs, c_lo + t * kBdpKeys, raw_lds(t), wave, lane);
     FATTN_STAMP(1);
-    if (compute) {
-        // Q landed (this wave's pieces; masks 0 and 1 may fly on)
-        const int nm = min(2, ntiles);
-        if (nm >= 2) wait_vmcnt_c<2 * NM>();
-        else if (nm == 1) wait_vmcnt_c<NM>();
-        else wait_vmcnt_c<0>();
-    } else {
-        bdp_build_wait<KT, D>(min(C::nRaw - 1, ntiles - 1));  // raw 0 (and Q) landed
-    }
+    // Q, (masks 0 and 1,) this wave's pieces of raw 0 landed
+    if (compute) bdp_compute_wait<KT, D, NM>(max(npro - 1, 0), 0);
+    else bdp_build_wait<KT, D>(npro - 1);
     __syncthreads();  // Q and raw 0 complete in LDS
     f16x8 qop[NK];
     if (compute) {
@@ -242,16 +287,16 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
             hq.s4 = (f16)x1.x; hq.s5 = (f16)x1.y; hq.s6 = (f16)x1.z; hq.s7 = (f16)x1.w;
             qop[kk] = hq;
         }
-        // mask 0 landed (only mask 1 was issued after it)
-        if (ntiles > 1) wait_vmcnt_c<NM>();
-        else wait_vmcnt_c<0>();
+        // this wave's pieces of raw 1 landed (the build waves dequantise it
+        // after the loop's first barrier)
+        if (ntiles > 1) bdp_compute_wait<KT, D, NM>(npro - 2, 0);
     } else {
         if (ntiles > 0) {
             bdp_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, bw, lane);
             // raw 1 landed (raw 2 .. nRaw - 1 may fly on).  Raw nRaw goes into
             // slot 0 after the loop's first barrier: every build wave reads all
             // of a slot's rows, so a slot is free only once they all have.
-            if (ntiles > 1) bdp_build_wait<KT, D>(min(C::nRaw - 2, ntiles - 2));
+            if (ntiles > 1) bdp_build_wait<KT, D>(npro - 2);
         }
     }
     FATTN_STAMP(2);
@@ -290,13 +335,14 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
         // (s + 1) % 2 is free; raw s + 1 is complete (its build waves waited)
         __syncthreads();
         if (s < 4) FATTN_STAMP(3 + s);
+        // every wave: its pieces of raw s + nRaw into raw s's slot (every build
+        // wave read it before this barrier)
+        if (s == 2) FATTN_STAMP(14);
+        if (s + C::nRaw < ntiles) bdp_issue<KT, D>(rs, c_lo + (s + C::nRaw) * kBdpKeys, raw_lds(s + C::nRaw), wave, lane);
+        if (s == 2) FATTN_STAMP(15);
         if (!compute) {
-            // ---- build: raw s + nRaw into raw s's slot (every build wave read it
-            // before this barrier); raw s + 1 -> pair (s + 1) % 2; then wait for
-            // this wave's pieces of raw s + 2 (raw s + 3 .. s + nRaw may fly on)
-            if (s == 2) FATTN_STAMP(14);
-            if (s + C::nRaw < ntiles) bdp_issue<KT, D>(rs, c_lo + (s + C::nRaw) * kBdpKeys, raw_lds(s + C::nRaw), bw, lane);
-            if (s == 2) FATTN_STAMP(15);
+            // ---- build: raw s + 1 -> pair (s + 1) % 2; then wait for this
+            // wave's pieces of raw s + 2 (raw s + 3 .. s + nRaw may fly on)
             if (s + 1 < ntiles) {
                 bdp_dequant<KT, D>(raw_ptr(s + 1), smem + ((s + 1) & 1) * C::pair,
                                    smem + ((s + 1) & 1) * C::pair + C::img, bw, lane);
@@ -401,12 +447,20 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
                 for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[q], o[db]);
             }
         }
-        // mask s + 1 landed before the next barrier (only mask s + 2 after it)
+        // before the next barrier: mask s + 1 and this wave's pieces of raw s + 2
+        // landed.  Issue order per tile: raw s + nRaw, then mask s + 2, so raw
+        // s + 2 (issued with tile s + 2 - nRaw <= s - 1, or in the prologue) is
+        // older than mask s + 1 (tile s - 1) for s >= 1; tile 0's mask 1 went
+        // before the prologue's raw tiles.  Without a mask only the raw counts.
         if constexpr (HM) {
-            if (s + 1 < ntiles) {
-                if (s + 2 < ntiles) wait_vmcnt_c<NM>();
-                else wait_vmcnt_c<0>();
+            if (s == 0) {
+                if (ntiles > 1)
+                    bdp_compute_wait<KT, D, NM>(max(npro - 3, 0) + (C::nRaw < ntiles ? 1 : 0), 2 < ntiles ? 1 : 0);
+            } else if (s + 1 < ntiles) {
+                bdp_compute_wait<KT, D, NM>(s + C::nRaw < ntiles ? 1 : 0, s + 2 < ntiles ? 1 : 0);
             }
+        } else {
+            if (s + 2 < ntiles) bdp_compute_wait<KT, D, NM>(min(C::nRaw - 2, ntiles - 3 - s), 0);
         }
 #ifdef FATTN_STAMPS
         if (s < 4) {

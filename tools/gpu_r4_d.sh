@@ -3,7 +3,8 @@
 # LDS (Q8_0 4 tiles, Q4_0 5) -- its tests, then config 5 alternating the
 # product library, the 3-tile ring (libfattn_nr3.so) and a no-dequantisation
 # diagnostic build (libfattn_nodeq.so: build waves only move bytes), and the
-# phase stamps of the product form.
+# phase stamps of the product form; libfattn_nont.so: K/V DMA without the
+# non-temporal policy.
 source tools/gpu_round.sh
 export TMPDIR=/tmp
 F=gpurun_out/r4d
@@ -17,6 +18,7 @@ for r in 1 2; do
   FATTN_LIB=libfattn_nr3.so run c5_nr3_$r 200 python bench.py $B; line "cfg5 32h bdp nRaw 3 run $r" c5_nr3_$r
   FATTN_LIB=libfattn_nodeq.so run c5_nodeq_$r 200 python bench.py $B; line "cfg5 32h bdp no dequant (diag) run $r" c5_nodeq_$r
   run c5_bd_$r 200 python bench.py $B --bd 2; line "cfg5 32h bd (all waves) run $r" c5_bd_$r
+  FATTN_LIB=libfattn_nont.so run c5_nont_$r 200 python bench.py $B; line "cfg5 32h bdp nRaw 4, K/V DMA without nt run $r" c5_nont_$r
 done
 run c5s2_nr4 200 python bench.py $B --heads 16 --kv-heads 16; line "cfg5 16h bdp nRaw 4" c5s2_nr4
 FATTN_LIB=libfattn_nr3.so run c5s2_nr3 200 python bench.py $B --heads 16 --kv-heads 16; line "cfg5 16h bdp nRaw 3" c5s2_nr3

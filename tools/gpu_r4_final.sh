@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-4 evidence on a final tree: GPU suite, smoke, the default bench line,
+# the two-rank rehearsal of the default N > 1 line (config-5 head shard, one
+# gather per step), the rocprofv3 kernel-trace summary of the bench, and the
+# FETCH_SIZE / WRITE_SIZE passes (traffic files tagged with plan + source hash)
+# for config 3 and for the prefill shape (SURVEY's zero mask, as the bench's
+# prefill object).  Summaries land in gpurun_out/r4final/.
+#   PROF_ONLY=1: the profiling steps only.
+source tools/gpu_round.sh
+export TMPDIR=/tmp
+F=gpurun_out/r4final
+mkdir -p $F
+if [ -z "$PROF_ONLY" ]; then
+  run pytest_gpu 1100 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  run bench 600 python bench.py
+  grep '^{' gpurun_out/bench.log > $F/bench.json || true
+  FATTN_BENCH_REHEARSE=1 run rehearse_head 300 python bench.py --gpus 2 --steps 20 --warmup 5
+  grep '^{' gpurun_out/rehearse_head.log > $F/rehearse_world2_head.json || true
+fi
+run kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4f_kt -o kt -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline
+D="--no-cpu-baseline --no-scale-ref --no-copy-peak --no-prefill --steps 50 --warmup 5"
+run fetch_cfg3 180 timeout -s KILL 170 rocprofv3 --output-format csv --pmc FETCH_SIZE -d gpurun_out/r4f_fetch -o f -- python3 bench.py $D
+run write_cfg3 180 timeout -s KILL 170 rocprofv3 --output-format csv --pmc WRITE_SIZE -d gpurun_out/r4f_write -o w -- python3 bench.py $D
+python tools/pmc_summary.py --kernel fattn_split_kernel --traffic $F/traffic_r04_cfg3.json --bench-line gpurun_out/fetch_cfg3.log \
+  $(find gpurun_out/r4f_fetch gpurun_out/r4f_write -name "*counter_collection.csv") > $F/traffic_cfg3.txt 2>&1
+run fetch_pf 240 timeout -s KILL 230 rocprofv3 --output-format csv --pmc FETCH_SIZE -d gpurun_out/r4f_pfetch -o f -- python3 bench.py --prefill-only
+run write_pf 240 timeout -s KILL 230 rocprofv3 --output-format csv --pmc WRITE_SIZE -d gpurun_out/r4f_pwrite -o w -- python3 bench.py --prefill-only
+python tools/pmc_summary.py --kernel fattn_pf_kernel --traffic $F/traffic_r04_prefill.json --bench-line gpurun_out/fetch_pf.log \
+  $(find gpurun_out/r4f_pfetch gpurun_out/r4f_pwrite -name "*counter_collection.csv") > $F/traffic_prefill.txt 2>&1
+for f in $(find gpurun_out/r4f_kt -name "*kernel_stats.csv"); do cp "$f" $F/kernel_stats.csv; done
+python tools/kstats.py $F/kernel_stats.csv > $F/kernel_stats_summary.txt
+tail -3 gpurun_out/pytest_gpu.log > $F/pytest_gpu_tail.txt 2>/dev/null
+tail -2 gpurun_out/smoke.log > $F/smoke.txt 2>/dev/null
+ls -la $F; cat $F/pytest_gpu_tail.txt $F/kernel_stats_summary.txt $F/traffic_cfg3.txt $F/traffic_prefill.txt $F/bench.json
