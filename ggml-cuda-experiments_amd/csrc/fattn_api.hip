@@ -518,9 +518,10 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // (from 64 rows, when the chunks hold two tiles or more: `wide` above)
     // Q8_0 / Q4_0 take the compute / build-role form (fattn_bdp.h) unless
     // FATTN_OPT_BD = 2 asks for the all-waves form; head dim 64 (Q8_0 / Q4_0)
-    // has the role form only, taken when FATTN_OPT_BD = 3 asks for it
+    // has the role form only (config-5 shape at D = 64: 19.2 us against 21.3
+    // for the multi-query kernel, profiles/r04_e)
     pl.bd = pl.bdp = false;
-    const bool bd_dim = D == 128 || (D == 64 && mq_ok && g_opt_bd == 3);
+    const bool bd_dim = D == 128 || (D == 64 && mq_ok && g_opt_bd != 2);
     if (!pl.pf && g_opt_bd != 1 && (mq_ok || f16_ok) && bd_dim && N % kStep == 0 &&
         (g_opt_bd >= 2 || (NQ * a.rk2 >= kBdRows && wide))) {
         pl.bd = true;

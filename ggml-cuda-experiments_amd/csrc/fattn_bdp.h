@@ -18,8 +18,8 @@
 //    workgroup dequantises 128-key tile s between two barriers and then
 //    computes it, every SIMD idle on one pipe in each phase);
 //  * HBM -> LDS by buffer_load ... lds: raw tiles (nRaw in flight -- as many
-//    as the LDS holds, Q8_0 4, Q4_0 5 -- issued by all eight waves once a
-//    tile has 8 or more 1-KiB pieces, else by the build waves), each compute wave's 32 x 32 mask block (two tiles in
+//    as the LDS holds, Q8_0 4, Q4_0 5 -- issued by the build waves), each
+//    compute wave's 32 x 32 mask block (two tiles in
 //    flight, by the compute wave itself), Q's 64 f32 rows once before the loop
 //    (by all waves, into the second image pair's place);
 //  * dequantisation h(q * d) with one f16 rounding (src/utils.h:10-11), images
@@ -64,21 +64,22 @@ struct BdpCfg {
     static constexpr int ldsBytes = maskEnd > BdPark<D, 2>::bytes ? maskEnd : BdPark<D, 2>::bytes;
     static constexpr int qOff = pair;                            // Q's f32 rows before the loop (pair 1)
     static constexpr int NI = (kvRaw + 1023) / 1024;             // 1-KiB DMA instructions per K (or V) tile
-    // Raw instructions j = 0 .. T - 1 (K then V) of a tile.  From 8 of them on,
-    // ALL eight waves issue them (the CU's LDS-DMA throughput grows with the
-    // number of issuing waves: with the build waves alone each issue stalled
-    // ~1.2 us per tile on config 5, profiles/r04_d): j -> wave j % 8, the
-    // remainder to the build waves first (or one more to every compute wave
-    // when more than four are left), so the compute waves' counts are equal
-    // -- their waits sit right behind the youngest group and must count it
-    // exactly.  Fewer than 8: the build waves, j -> 4 + j % 4.  The smallest
+    // Raw instructions j = 0 .. T - 1 (K then V) of a tile, issued by the build
+    // waves, j -> 4 + j % 4.  (FATTN_BDP_ALL_ISSUE, A/B builds: from 8 of them
+    // on ALL eight waves issue them, j -> wave j % 8, the remainder to the
+    // build waves first -- or one more to every compute wave when more than
+    // four are left -- so the compute waves' counts are equal: their waits sit
+    // right behind the youngest group and must count it exactly.  The issue
+    // of the build waves alone stalls ~1.2 us per tile on config 5 (a full
+    // memory pipeline), but spreading it over all waves made the compute
+    // waves stall as long: 25.1 vs 24.4 us, profiles/r04_e.)  The smallest
     // per-role count counts the waits (a build wave with one more instruction
     // also waits for one of a younger group: fattn_pf.h).
     static constexpr int T = 2 * NI;
-#ifdef FATTN_BDP_BUILD_ISSUE
-    static constexpr bool kAll = false;  // diagnostic build only (A/B)
+#ifdef FATTN_BDP_ALL_ISSUE
+    static constexpr bool kAll = T >= 8;  // diagnostic build only (A/B)
 #else
-    static constexpr bool kAll = T >= 8;
+    static constexpr bool kAll = false;
 #endif
     static constexpr int kBase = T / 8, kRem = T % 8;
     static constexpr int owner(int j) {

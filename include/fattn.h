@@ -169,11 +169,11 @@ enum {
                                        merge one wave per (tile, row), in a second launch or in-kernel
                                        (FATTN_OPT_MERGE_IN_KERNEL) (default), 1 = the last-arriving workgroup merges
                                        the whole tile (combine_tile) */
-    FATTN_OPT_BD = 22               /* batched-decode kernels (64-row workgroups, D = 128, Q8_0 / Q4_0 / f16 K/V,
-                                       16-B rows): 0 = auto (from 64 packed rows per kv head, below the prefill
-                                       shapes; Q8_0 / Q4_0 in the compute / build-role form), 1 = never,
-                                       2 = the all-waves form whenever eligible, 3 = the role form whenever
-                                       eligible (quantised K/V) */,
+    FATTN_OPT_BD = 22               /* batched-decode kernels (64-row workgroups, D = 128 Q8_0 / Q4_0 / f16 K/V
+                                       and D = 64 Q8_0 / Q4_0, 16-B rows): 0 = auto (from 64 packed rows per kv
+                                       head, below the prefill shapes; Q8_0 / Q4_0 in the compute / build-role
+                                       form), 1 = never, 2 = the all-waves form whenever eligible (D = 128),
+                                       3 = the role form whenever eligible (quantised K/V) */,
     /* 23: a removed experiment (one-row partials as data-tagged granules), rejected */
     FATTN_OPT_MERGE_IN_KERNEL = 24  /* chunk partials of multi-row tiles (split kernel with 4+ chunks, batched-
                                        decode kernel): 0 = merged in a second launch (default); 1 = inside the

@@ -103,7 +103,9 @@ def test_bd_option_forms():
         # head dim 64: the role form (quantised only)
         assert fattn.describe(_params(D=64, NQ=64)).startswith("fattn_bdp_kernel<q8_0,D64")
         assert "fattn_bd" not in fattn.describe(_params(D=64, NQ=64, kt=fattn.TYPE_F16))
-    assert "fattn_bd" not in fattn.describe(_params(D=64, NQ=64))  # (auto: the multi-query kernel)
+    assert fattn.describe(_params(D=64, NQ=64)).startswith("fattn_bdp_kernel<q8_0,D64")  # (auto too)
+    with fattn.options({fattn.OPT_BD: 2}):  # (the all-waves form is D = 128 only: the multi-query kernel)
+        assert fattn.describe(_params(D=64, NQ=64)).startswith("fattn_mq_kernel")
     with pytest.raises(Exception):
         fattn.set_option(fattn.OPT_BD, 4)
 
