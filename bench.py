@@ -311,6 +311,8 @@ def parse_args(argv=None):
     ap.add_argument("--pf", type=int, default=0, help="prefill kernel: 0 auto, 1 never, 2 whenever eligible")
     ap.add_argument("--no-mq", action="store_true", help="never pick the multi-query kernel (split-KV kernel only)")
     ap.add_argument("--bd", type=int, default=0, help="batched-decode kernel: 0 auto, 1 never, 2 all-waves form, 3 role form (fattn.h FATTN_OPT_BD)")
+    ap.add_argument("--bd-xcd", type=int, default=0,
+                    help="batched decode workgroup order: 0 auto, 1 plain, 2 XCD-grouped (fattn.h FATTN_OPT_BD_XCD)")
     ap.add_argument("--merge-in-kernel", type=int, default=0,
                     help="multi-row chunk merge: 0 second launch, 1 in-kernel when the grid is co-resident")
     ap.add_argument("--split-prio", type=int, default=0,
@@ -342,7 +344,7 @@ def parse_args(argv=None):
 def apply_options(args):
     import fattn
     opts = [(args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT), (args.pf, fattn.OPT_PF),
-            (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO), (args.bd, fattn.OPT_BD),
+            (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO), (args.bd, fattn.OPT_BD), (args.bd_xcd, fattn.OPT_BD_XCD),
             (args.waves, fattn.OPT_SPLIT_WAVES)]
     fattn.set_option(fattn.OPT_SPLIT_SKIP, 1 if args.no_step_skip else 0)
     fattn.set_option(fattn.OPT_SPLIT_MERGE, 1 if args.fused_merge else 0)

@@ -60,6 +60,7 @@ std::atomic<int> g_opt_split_waves{0};      // split kernel waves per workgroup 
 std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
+std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto, 1 off, 2 on
 std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
 std::atomic<uint32_t> g_epoch{0};
@@ -336,11 +337,14 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     a.wave_bytes = 0;
     const bool q8 = pl.kt == FATTN_TYPE_Q8_0;
     pl.lds = pl.bdp && pl.D == 64 ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 64>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 64>::ldsBytes)
+             : pl.bdp && pl.D == 96 ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 96>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 96>::ldsBytes)
              : pl.bdp             ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes)
              : pl.kt == FATTN_TYPE_Q8_0 ? BdCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
              : pl.kt == FATTN_TYPE_Q4_0 ? BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes
                                         : BdCfg<FATTN_TYPE_F16, 128>::ldsBytes;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
+    // XCD-grouped workgroup order (bd_tile_coords): whole tiles per XCD
+    a.xcd_group = g_opt_bd_xcd == 2 && (a.n_chunks * Y * S) % 8 == 0 ? 1 : 0;
     // the chunk partials merge inside the launch (bd_tile_merge: the tile's
     // workgroups wait for each other, so only when the whole grid is
     // co-resident -- one workgroup per CU by LDS) or in a second launch
@@ -479,7 +483,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // chunk to hold at least two 128-key tiles: a workgroup with one tile is all
     // prologue and epilogue (config-5 shard, 4 heads x 64 rows: split kernel
     // 9.4 + 4.3 us merge, multi-query 11.0 + 4.3, batched decode 10.9 + 4.4)
-    const int64_t qpt64 = (mq_ok || f16_ok) ? 64 / a.rk2 : 1;  // query rows per 64-row tile (rk2 <= 64)
+    const int64_t qpt64 = (quant_ok || f16_ok) ? 64 / a.rk2 : 1;  // query rows per 64-row tile (rk2 <= 64)
     const int64_t y64 = Hkv * ((NQ + qpt64 - 1) / qpt64);
     const bool wide = N * y64 * S >= (int64_t)2 * kBdKeys * pl.cus;
     pl.mq = mq_ok && NQ * a.rk2 >= g_opt_mq_min_rows &&
@@ -517,15 +521,15 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // chunk partials merged in a second launch; Q8_0 / Q4_0 and f16 K/V
     // (from 64 rows, when the chunks hold two tiles or more: `wide` above)
     // Q8_0 / Q4_0 take the compute / build-role form (fattn_bdp.h) unless
-    // FATTN_OPT_BD = 2 asks for the all-waves form; head dim 64 (Q8_0 / Q4_0)
-    // has the role form only (config-5 shape at D = 64: 19.2 us against 21.3
-    // for the multi-query kernel, profiles/r04_e)
+    // FATTN_OPT_BD = 2 asks for the all-waves form; head dims 64 and 96 (Q8_0 /
+    // Q4_0) have the role form only (config-5 shape at D = 64: 19.2 us against
+    // 21.3 for the multi-query kernel, profiles/r04_e)
     pl.bd = pl.bdp = false;
-    const bool bd_dim = D == 128 || (D == 64 && mq_ok && g_opt_bd != 2);
-    if (!pl.pf && g_opt_bd != 1 && (mq_ok || f16_ok) && bd_dim && N % kStep == 0 &&
+    const bool bd_dim = (D == 128 && (mq_ok || f16_ok)) || ((D == 64 || D == 96) && quant_ok && g_opt_bd != 2);
+    if (!pl.pf && g_opt_bd != 1 && bd_dim && N % kStep == 0 &&
         (g_opt_bd >= 2 || (NQ * a.rk2 >= kBdRows && wide))) {
         pl.bd = true;
-        pl.bdp = mq_ok && g_opt_bd != 2;
+        pl.bdp = quant_ok && g_opt_bd != 2;
         pl.mq = false;
         a.R = a.rk2;
         a.R_inv = 1.0f / (float)a.R;
@@ -650,6 +654,10 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 1) return FATTN_ERR_INVALID_ARG;
             g_opt_merge_in_kernel = value;
             return FATTN_OK;
+        case FATTN_OPT_BD_XCD:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_bd_xcd = value;
+            return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:
             if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
             g_opt_split_nbuf = value;
@@ -710,7 +718,8 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
         std::snprintf(kern, sizeof kern, "%sfattn_pf_kernel<%s,D%d,%s>", pl.pf_flags ? "pf_mask_flags_kernel + " : "",
                       tn(pl.kt), pl.D, hm);
     else if (pl.bd)
-        std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D, hm,
+        std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,
+                      hm, pl.a.xcd_group ? " (xcd order)" : "",
                       pl.a.merge_launch == 1 ? " + fattn_bd_merge_kernel" : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     else if (pl.mq)
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,

@@ -45,7 +45,7 @@ constexpr int kBdpMaxRaw = FATTN_BDP_MAX_RAW;  // (diagnostic builds lower it fo
 
 template <int KT, int D>
 struct BdpCfg {
-    static_assert(D == 128 || D == 64, "one ggml block (D = 128) or half-block (D = 64) per build wave");
+    static_assert(D == 64 || D == 96 || D == 128, "half-blocks dealt over the build waves; 16-B Q chunks");
     static_assert(KT == FATTN_TYPE_Q8_0 || KT == FATTN_TYPE_Q4_0, "quantised K/V (f16 takes fattn_bd.h's image ring)");
     static constexpr int rowB = row_bytes<KT, D>();
     static constexpr int kvRaw = kBdpKeys * rowB;                // raw K (or V) bytes per tile
@@ -119,9 +119,10 @@ __device__ __forceinline__ void bdp_issue(const StepSrc& rs, int n0, uint32_t ld
     }
 }
 
-// build wave bw: half-blocks D/64 bw .. + D/64 of key `lane` (D = 128: block bw,
-// both halves; D = 64: half bw & 1 of block bw >> 1), K into dim slice 2b + h
-// and V into dim block b, in the layouts fattn_bd.h / fattn_pf.h read
+// build wave bw: half-blocks hb = bw, bw + 4, ... (< D / 16) of key `lane` --
+// half hb & 1 of ggml block hb >> 1 -- K into dim slice hb and V into dim
+// block hb >> 1, in the layouts fattn_bd.h / fattn_pf.h read (D = 96: waves 4
+// and 5 take two half-blocks, waves 6 and 7 one)
 template <int KT, int D>
 __device__ __forceinline__ void bdp_dequant(const uint8_t* raw, uint8_t* k16, uint8_t* v16, int bw, int lane) {
 #ifdef FATTN_MQ_NODEQ
@@ -130,10 +131,11 @@ __device__ __forceinline__ void bdp_dequant(const uint8_t* raw, uint8_t* k16, ui
     using C = BdpCfg<KT, D>;
     const int r = lane;
     const int sk = (r >> 3) & 1, sv = (r >> 2) & 3;
-    constexpr int HPW = D / 64;  // half-blocks per build wave
 #pragma unroll
-    for (int i = 0; i < HPW; i++) {
-        const int b = (HPW * bw + i) >> 1, h = (HPW * bw + i) & 1;
+    for (int i = 0; i < (D / 16 + 3) / 4; i++) {
+        const int hb = bw + 4 * i;
+        if (hb >= D / 16) break;  // wave-uniform
+        const int b = hb >> 1, h = hb & 1;
         u32x4 ck[2], cv[2];
         dequant_half<KT, D>(raw, r, b, h, ck);
         dequant_half<KT, D>(raw + C::kvRaw, r, b, h, cv);
@@ -199,9 +201,8 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
     FATTN_STAMP(0);
 
     // ---- tile decode (fattn_bd.h)
-    const int chunk = blockIdx.x;
-    const int y = blockIdx.y;
-    const int iq3 = blockIdx.z;
+    int chunk, y, iq3;
+    bd_tile_coords(a, chunk, y, iq3);
     if (a.merge_launch == 2 && tid == 0) arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
     int qt = 0, ik2 = y, ik3 = iq3;
     if (a.n_qt != 1) {
@@ -227,9 +228,12 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
     auto raw_ptr = [&](int s) { return smem + C::rawOff + (s % C::nRaw) * C::rawBytes; };
 
     // ---- Q: 64 f32 rows -> LDS (pair 1's place) by D / 4 1-KiB DMA
-    // instructions, D / 32 per wave (fattn_bd.h's layout: row pr's 16-B chunk c
-    // of CPR = D / 4 at c ^ (pr % CPR))
+    // instructions, D / 32 per wave; 16-B chunk g = 64 j + lane of the image is
+    // chunk c = g % CPR of row g / CPR (CPR = D / 4 chunks a row), holding the
+    // row's chunk c ^ (row & SW) (fattn_bd.h's layout; SW = swz_mask(CPR): 31,
+    // 15 and 7 at D = 128, 64, 96)
     constexpr int CPR = D / 4;
+    constexpr int SW = swz_mask(CPR);
     {
         const i32x4 qs = make_srd(a.q + (int64_t)iq3 * a.q_nb3, a.q_span);
         constexpr int kQInst = kBdRows * D * 4 / 1024;
@@ -237,11 +241,12 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
 #pragma unroll
         for (int i = 0; i < kQInst / kBdWaves; i++) {
             const int j = wave + kBdWaves * i;
-            const int pr = (64 / CPR) * j + lane / CPR;
+            const int g = kWave * j + lane;
+            const int pr = g / CPR, cc = g % CPR;
             const int rq = div_R(a, pr);
             const int q1 = qt * a.QPT + rq, q2 = ik2 * a.rk2 + (pr - rq * a.R);
             const uint32_t off = rq < a.QPT && q1 < a.NQ ? (uint32_t)q1 * (uint32_t)a.q_nb1 + (uint32_t)q2 * (uint32_t)a.q_nb2 +
-                                                 (((lane % CPR) ^ (pr % CPR)) * 16)
+                                                 ((cc ^ (pr & SW)) * 16)
                                            : a.q_span;
             dma<16>(qs, lds0 + C::qOff + j * 1024, off);
         }
@@ -281,8 +286,8 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
 #pragma unroll
         for (int kk = 0; kk < NK; kk++) {
             const float* qr = (const float*)(smem + C::qOff) + p * D;
-            const f32x4 x0 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h) ^ (p % CPR)));
-            const f32x4 x1 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h + 1) ^ (p % CPR)));
+            const f32x4 x0 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h) ^ (p & SW)));
+            const f32x4 x1 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h + 1) ^ (p & SW)));
             f16x8 hq;
             hq.s0 = (f16)x0.x; hq.s1 = (f16)x0.y; hq.s2 = (f16)x0.z; hq.s3 = (f16)x0.w;
             hq.s4 = (f16)x1.x; hq.s5 = (f16)x1.y; hq.s6 = (f16)x1.z; hq.s7 = (f16)x1.w;

@@ -179,7 +179,7 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
 }
 
 // D = 128: the all-waves form, or the role form for quantised K/V (pl.bdp);
-// D = 64: the role form only (the planner sets pl.bdp)
+// D = 64 / 96: the role form only (the planner sets pl.bdp)
 template <int KT, int D, bool HM>
 int launch_bd_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     void (*kern)(SplitArgs) = nullptr;
@@ -243,7 +243,7 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
     }
-    if constexpr (D == 64 || D == 128) {
+    if constexpr (D == 64 || D == 96 || D == 128) {
         if (pl.bd) {
             if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_bd<FATTN_TYPE_Q8_0, D>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_bd<FATTN_TYPE_Q4_0, D>(pl, st, ev);

@@ -93,7 +93,7 @@ struct SplitArgs {
     int merge_launch;   // chunk partials of multi-row tiles: 1 = merged by a second launch (fattn_merge_kernel,
                         // fattn_bd_merge_kernel), 2 = inside the launch (tile_arrive_wait: grid co-resident)
     int step_skip;      // split kernel: 1 = skip steps whose mask is all -inf for the tile (FATTN_OPT_SPLIT_SKIP)
-                        // flight beside the compute), 0 = refill a buffer once its step is computed
+    int xcd_group;      // batched decode: workgroups in XCD-grouped order (bd_tile_coords; grid size % 8 == 0)
 };
 
 // XOR mask of the 16-B chunk swizzle of an LDS row of `cpr` chunks: the largest

@@ -104,10 +104,25 @@ def test_bd_option_forms():
         assert fattn.describe(_params(D=64, NQ=64)).startswith("fattn_bdp_kernel<q8_0,D64")
         assert "fattn_bd" not in fattn.describe(_params(D=64, NQ=64, kt=fattn.TYPE_F16))
     assert fattn.describe(_params(D=64, NQ=64)).startswith("fattn_bdp_kernel<q8_0,D64")  # (auto too)
+    assert fattn.describe(_params(D=96, NQ=64, kt=fattn.TYPE_Q4_0)).startswith("fattn_bdp_kernel<q4_0,D96")
     with fattn.options({fattn.OPT_BD: 2}):  # (the all-waves form is D = 128 only: the multi-query kernel)
         assert fattn.describe(_params(D=64, NQ=64)).startswith("fattn_mq_kernel")
     with pytest.raises(Exception):
         fattn.set_option(fattn.OPT_BD, 4)
+
+
+def test_bd_xcd_option():
+    """FATTN_OPT_BD_XCD: 2 = XCD-grouped workgroup order for the batched-decode
+    kernels when the grid is a multiple of 8 workgroups; other plans unchanged."""
+    with fattn.options({fattn.OPT_BD_XCD: 2}):
+        assert "(xcd order)" in fattn.describe(_params(NQ=64))                   # grid(8,32,1)
+        assert "(xcd order)" not in fattn.describe(_params())                    # config 3: split kernel
+        d5 = fattn.describe(_params(NQ=64, H=5, Hkv=5, N=32768))             # grid(52,5,1): not a multiple of 8
+        assert d5.startswith("fattn_bdp_kernel") and "(xcd order)" not in d5, d5
+    with fattn.options({fattn.OPT_BD_XCD: 1}):
+        assert "(xcd order)" not in fattn.describe(_params(NQ=64))
+    with pytest.raises(Exception):
+        fattn.set_option(fattn.OPT_BD_XCD, 3)
 
 
 def test_merge_in_kernel_option():

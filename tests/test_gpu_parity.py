@@ -419,6 +419,29 @@ def test_bdp_matches_bd_bitwise_inputs(dev):
     assert attn_rel_err(a, p.oracle()) <= RTOL
 
 
+@pytest.mark.parametrize("form", [2, 3])
+@pytest.mark.parametrize("case", [
+    dict(kv_type="q8_0", NQ=64, H=8, Hkv=8, N=4096, mask="random"),           # 8 chunks x 8 tiles: grid % 8 == 0
+    dict(kv_type="q4_0", NQ=40, H=12, Hkv=4, N=768, mask="causal"),           # R = 3, 2 row tiles
+    dict(kv_type="q8_0", NQ=64, H=4, Hkv=2, N=1024, mask="random", S=2),      # ne03 batch
+], ids=["cfg5x8", "gqa3", "batch2"])
+def test_bd_xcd_order(dev, case, form):
+    """The XCD-grouped workgroup order (FATTN_OPT_BD_XCD = 2) relabels the
+    grid only: same plan, results against the oracle and bit-identical to the
+    plain order (each workgroup's arithmetic is unchanged)."""
+    p = make_problem(D=128, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000 + 3, **case)
+    t = upload(p, dev)
+    with fattn.options({fattn.OPT_BD: form, fattn.OPT_BD_XCD: 2}):
+        d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+        got = run_gpu(p)
+    with fattn.options({fattn.OPT_BD: form, fattn.OPT_BD_XCD: 1}):
+        plain = run_gpu(p)
+    gx, gy, gz = (int(x) for x in d.split("grid(")[1].split(")")[0].split(","))
+    assert ("(xcd order)" in d) == ((gx * gy * gz) % 8 == 0), d
+    assert attn_rel_err(got, p.oracle()) <= RTOL
+    assert np.array_equal(got.view(np.uint32), plain.view(np.uint32))
+
+
 # head dim 64: the role form with one half-block per build wave (FATTN_OPT_BD = 3)
 BDP64_CASES = [
     dict(kv_type="q8_0", NQ=64, H=8, Hkv=8, N=4096, mask="random"),
@@ -432,20 +455,24 @@ BDP64_CASES = [
 ]
 
 
+@pytest.mark.parametrize("D", [64, 96])
 @pytest.mark.parametrize("case", BDP64_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
-def test_bdp_d64(dev, bdp_force, case):
-    p = make_problem(D=64, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000 + 9, **case)
+def test_bdp_d64(dev, bdp_force, case, D):
+    """Head dims 64 and 96 (D = 96: 102 / 54-B rows, three ggml blocks dealt
+    as six half-blocks over the four build waves; Q rows of 24 16-B chunks)."""
+    p = make_problem(D=D, seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000 + 9, **case)
     t = upload(p, dev)
     d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
-    assert "fattn_bdp_kernel" in d and "D64" in d, d
+    assert "fattn_bdp_kernel" in d and f"D{D}" in d, d
     got, ref = run_gpu(p), p.oracle()
     assert attn_rel_err(got, ref) <= RTOL
     assert attn_elem_err(got, ref) <= 1.0
 
 
+@pytest.mark.parametrize("D", [64, 96])
 @pytest.mark.parametrize("chunk", [128, 1024])
-def test_bdp_d64_chunking(dev, bdp_force, chunk):
-    p = make_problem(D=64, NQ=64, H=4, N=2048, kv_type="q8_0", mask="causal", seed=46)
+def test_bdp_d64_chunking(dev, bdp_force, chunk, D):
+    p = make_problem(D=D, NQ=64, H=4, N=2048, kv_type="q8_0", mask="causal", seed=46)
     got, ref = run_gpu(p, kv_chunk=chunk), p.oracle()
     assert attn_rel_err(got, ref) <= RTOL
     assert attn_elem_err(got, ref) <= 1.0
