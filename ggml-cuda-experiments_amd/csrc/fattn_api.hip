@@ -505,7 +505,9 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // the (kv head x query tile x seq) workgroups alone fill the chip
     // (f16 K/V rows, not transposed V: the same kernel, images filled by DMA)
     pl.pf = false;
-    if ((quant_ok || f16_ok) && g_opt_pf != 1 && (D == 64 || D == 96 || D == 128) && p->kv_chunk <= 0 &&
+    // (D = 80: f16 only, its images padded to 96 dims)
+    if ((quant_ok || f16_ok) && g_opt_pf != 1 && (D == 64 || D == 96 || D == 128 || (D == 80 && f16_ok)) &&
+        p->kv_chunk <= 0 &&
         N % kPfKeys == 0 &&
         p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= pl.cus)) {
         pl.pf = true;
@@ -553,6 +555,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
                                               : PfCfg<FATTN_TYPE_Q4_0, DD>::ldsBytes;
         };
         pl.lds = D == 64   ? pf_lds(std::integral_constant<int, 64>())
+                 : D == 80 ? PfCfg<FATTN_TYPE_F16, 80>::ldsBytes
                  : D == 96 ? pf_lds(std::integral_constant<int, 96>())
                            : pf_lds(std::integral_constant<int, 128>());
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);

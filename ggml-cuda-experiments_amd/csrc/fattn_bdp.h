@@ -7,13 +7,14 @@
 //
 //  * one workgroup = 8 waves with fixed roles, one pair per SIMD: waves 0-3
 //    COMPUTE (wave c: row group c & 1 = 32 rows, key half c >> 1 = 32 keys of
-//    every 64-key tile), waves 4-7 BUILD (wave 4 + b: ggml block b of every
-//    key, K and V);
+//    every 64-key tile), waves 4-7 BUILD (wave 4 + w: half-blocks w, w + 4,
+//    ... of every key, K and V -- at D = 128 two, at D = 64 one);
 //  * per 64-key tile s, between two workgroup barriers, the compute waves run
 //    S^T = K.Q^T, the online softmax and O^T += V^T.P^T on tile s (one image
-//    pair) while the build waves dequantise raw tile s + 1 into the other pair
-//    and issue raw tile s + nRaw into the raw slot they all emptied before the barrier -- the
-//    dequantisation VALU of one SIMD partner runs beside the matrix work of
+//    pair) while the build waves issue raw tile s + nRaw into the raw slot
+//    they all finished reading before the barrier and dequantise raw tile
+//    s + 1 into the other pair -- the dequantisation VALU of one SIMD partner
+//    runs beside the matrix work of
 //    the other, and there is ONE barrier per tile (fattn_bd.h: the whole
 //    workgroup dequantises 128-key tile s between two barriers and then
 //    computes it, every SIMD idle on one pipe in each phase);

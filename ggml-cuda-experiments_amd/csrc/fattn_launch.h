@@ -235,11 +235,13 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
     if constexpr (D == 64 || D == 128 || D == 256) {
         if (pl.kt != pl.vt && pl.vt != VT_F16T) return launch_mixed<D>(pl, st, ev);
     }
-    if constexpr (D == 64 || D == 96 || D == 128) {
+    if constexpr (D == 64 || D == 80 || D == 96 || D == 128) {
         if (pl.pf) {
             if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_pf<FATTN_TYPE_F16, D>(pl, st, ev);
-            if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0, D>(pl, st, ev);
-            if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0, D>(pl, st, ev);
+            if constexpr (D != 80) {  // (80 is not a whole number of ggml blocks)
+                if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_pf<FATTN_TYPE_Q8_0, D>(pl, st, ev);
+                if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_pf<FATTN_TYPE_Q4_0, D>(pl, st, ev);
+            }
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
     }

@@ -49,9 +49,15 @@ constexpr int kPfKeys = 64;                     // keys per tile
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// image dims: D = 80 (f16 K/V only) is laid out as 96 -- whole 32-dim blocks of
+// O^T -- with dims 80..95 zero in Q, K and V (DMA'd from past the descriptor)
+constexpr int pf_image_dims(int D) { return D == 80 ? 96 : D; }
+
 template <int KT, int D>
 struct PfCfg {
-    static_assert(D == 64 || D == 96 || D == 128, "at most one half ggml block per wave and row");
+    static_assert(D == 64 || D == 80 || D == 96 || D == 128, "at most one half ggml block per wave and row");
+    static_assert(D != 80 || KT == FATTN_TYPE_F16, "D = 80: f16 K/V (80 is not a whole number of ggml blocks)");
+    static constexpr int DI = pf_image_dims(D);
     static constexpr int NT = kPfWaves * kWave;
     // f16 K/V: LDS-DMA straight into the images (no raw tiles, no dequantisation);
     // three image pairs: tile s in use, s+1 and s+2 in flight
@@ -60,7 +66,7 @@ struct PfCfg {
     static constexpr int kvRaw = kPfKeys * rowB;                    // raw K (or V) bytes per tile
     static constexpr int rawBytes = (2 * kvRaw + 15) / 16 * 16;
     static constexpr int nRaw = kDirect ? 0 : 3;
-    static constexpr int img = kPfKeys * D * 2;                     // one f16 image
+    static constexpr int img = kPfKeys * DI * 2;                    // one f16 image
     static constexpr int pairBytes = 2 * img;                       // K image + V image
     static constexpr int nPairs = kDirect ? 3 : 2;
     static constexpr int ahead = kDirect ? 2 : 3;                   // tiles in flight beyond the current one
@@ -97,7 +103,7 @@ __device__ __forceinline__ void pf_issue(const StepSrc& rs, int n0, uint32_t lds
 // (any 16-B aligned stride).
 template <int D>
 struct PfDirect {
-    static constexpr int NJ = kPfKeys * D * 2 / 1024;  // 1-KiB pieces per image (D = 96: 12)
+    static constexpr int NJ = kPfKeys * pf_image_dims(D) * 2 / 1024;  // 1-KiB pieces per image (D = 80, 96: 12)
     static constexpr int NIW = 2 * NJ / kPfWaves;      // DMA instructions per wave and tile
     static_assert(kPfWaves == 8 && NIW * kPfWaves == 2 * NJ && NIW <= 4, "every wave the same count");
 };
@@ -107,12 +113,17 @@ __device__ __forceinline__ void pf_direct_offsets(const SplitArgs& a, int wave, 
 #pragma unroll
     for (int i = 0; i < PfDirect<D>::NIW; i++) {
         const int j = wave + 8 * i;      // (wave-uniform; K pieces first)
+        // (image dims past D -- D = 80 -- come from past the descriptor: zeros;
+        // kPadOff stays past it after the per-tile row offset is added)
+        constexpr uint32_t kPadOff = 0x80000000u;
         if (j < NJ) {  // K: slice kk = j / 2, rows 32 (j & 1) + lane / 2, stored half lane & 1
             const int kk = j >> 1, r = 32 * (j & 1) + (lane >> 1), hh = lane & 1;
-            off[i] = (uint32_t)r * (uint32_t)a.k_nb1 + kk * 32 + ((hh ^ ((r >> 3) & 1)) * 16);
+            const int sh = hh ^ ((r >> 3) & 1);
+            off[i] = 16 * kk + 8 * sh < D ? (uint32_t)r * (uint32_t)a.k_nb1 + kk * 32 + sh * 16 : kPadOff;
         } else {  // V: dim block db = jj / 4, rows 16 (jj & 3) + lane / 4, stored chunk lane & 3
             const int jj = j - NJ, db = jj >> 2, r = 16 * (jj & 3) + (lane >> 2), pc = lane & 3;
-            off[i] = (uint32_t)r * (uint32_t)a.v_nb1 + db * 64 + ((pc ^ ((r >> 2) & 3)) * 16);
+            const int lc = pc ^ ((r >> 2) & 3);
+            off[i] = 32 * db + 8 * lc < D ? (uint32_t)r * (uint32_t)a.v_nb1 + db * 64 + lc * 16 : kPadOff;
         }
     }
 }
@@ -188,8 +199,8 @@ template <int KT, int D, bool HM>
 __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const SplitArgs a) {
     using C = PfCfg<KT, D>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int NK = D / 16;   // 16-dim k-steps of S^T = K.Q^T
-    constexpr int NDB = D / 32;  // 32-dim blocks of O^T
+    constexpr int NK = C::DI / 16;   // 16-dim k-steps of S^T = K.Q^T
+    constexpr int NDB = C::DI / 32;  // 32-dim blocks of O^T
     constexpr int NM = HM ? 1 : 0;
     constexpr float kNegInf = -__builtin_inff();
     constexpr float kDeferLog2 = 8.0f;
@@ -290,9 +301,10 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             row_ok ? (uint32_t)iq1 * (uint32_t)a.q_nb1 + (uint32_t)iq2 * (uint32_t)a.q_nb2 + 32 * h : a.q_span;
 #pragma unroll
         for (int kk = 0; kk < NK; kk++) {
-            const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qoff + 64 * kk, 0, 0));
-            const f32x4 x1 =
-                __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qoff + 64 * kk + 16, 0, 0));
+            // (image dims past D, D = 80: from past the descriptor, zeros)
+            const uint32_t qk = 16 * kk + 8 * h < D ? qoff + 64 * kk : a.q_span;
+            const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qk, 0, 0));
+            const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qk + 16, 0, 0));
             f16x8 hq;
             hq.s0 = (f16)x0.x; hq.s1 = (f16)x0.y; hq.s2 = (f16)x0.z; hq.s3 = (f16)x0.w;
             hq.s4 = (f16)x1.x; hq.s5 = (f16)x1.y; hq.s6 = (f16)x1.z; hq.s7 = (f16)x1.w;
@@ -650,7 +662,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
                 f32x4 v;
 #pragma unroll
                 for (int r = 0; r < 4; r++) v[r] = l_tot == 0.0f ? __builtin_nanf("") : o[db][4 * u + r] * inv;
-                *(f32x4*)(out + 32 * db + 8 * u) = v;
+                if (32 * db + 8 * u + 4 * h < D) *(f32x4*)(out + 32 * db + 8 * u) = v;  // (D = 80: no padding dims)
             }
         }
     }

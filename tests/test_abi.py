@@ -79,9 +79,10 @@ def test_workspace_size_config3():
     (dict(D=64, NQ=4096, H=32, Hkv=32), ["fattn_pf_kernel<q8_0,D64"]),                       # D = 64 prefill
     (dict(D=96, NQ=4096, H=32, Hkv=32), ["fattn_pf_kernel<q8_0,D96"]),                       # D = 96 prefill
     (dict(D=96, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16), ["fattn_pf_kernel<f16,D96"]),
+    (dict(D=80, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16), ["fattn_pf_kernel<f16,D80"]),      # D = 80 prefill (f16)
     (dict(D=256, NQ=4096, H=16, Hkv=16), ["fattn_mq_kernel<q8_0,D256,4waves"]),              # D = 256 prefill
 ], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "bd_f16",
-        "bd_gqa6", "bd_f16_shard", "split_nq8_gqa", "pf_d64", "pf_d96", "pf_d96_f16", "mq_d256"])
+        "bd_gqa6", "bd_f16_shard", "split_nq8_gqa", "pf_d64", "pf_d96", "pf_d96_f16", "pf_d80_f16", "mq_d256"])
 def test_planner_picks(kw, want):
     """The plans the round-2 measurements chose, at 256 CUs:
     one-row tiles take 8 waves with the fused row merge; multi-row split tiles

@@ -661,6 +661,29 @@ def test_pf_d96(dev, pf_force, case):
     assert attn_elem_err(got, ref) <= 1.0
 
 
+PF80_CASES = [
+    dict(NQ=256, H=4, Hkv=4, N=256, mask="causal"),
+    dict(NQ=300, H=2, Hkv=2, N=192, mask="random"),                           # ragged query tiles
+    dict(NQ=64, H=24, Hkv=4, N=128, mask="zero"),                             # R = 6
+    dict(NQ=100, H=8, Hkv=2, N=128, mask="none", layout="pos", S=2),          # [N][Hkv] rows, 2 sequences
+    dict(NQ=256, H=2, Hkv=2, N=256, mask="neginf_blocks"),
+]
+
+
+@pytest.mark.parametrize("case", PF80_CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_pf_d80_f16(dev, pf_force, case):
+    """The prefill kernel at D = 80 (f16 K/V): images laid out as 96 dims, the
+    16 past D zero in Q, K and V (DMA'd from past the descriptor), the output's
+    padding dims not stored -- the neighbouring heads' dst rows stay intact."""
+    p = make_problem(D=80, kv_type="f16", seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000 + 5, **case)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert "fattn_pf_kernel" in d and "D80" in d, d
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 @pytest.mark.parametrize("kt", ["q8_0", "q4_0"])
 def test_pf_rescale(dev, pf_force, kt):
     """Large scores and scores rising along the sequence: deferred-max rescales."""
