@@ -60,7 +60,7 @@ std::atomic<int> g_opt_split_waves{0};      // split kernel waves per workgroup 
 std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and computes every step (FATTN_OPT_SPLIT_SKIP)
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
-std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto, 1 off, 2 on
+std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
 std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
 std::atomic<uint32_t> g_epoch{0};
@@ -343,8 +343,10 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
              : pl.kt == FATTN_TYPE_Q4_0 ? BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes
                                         : BdCfg<FATTN_TYPE_F16, 128>::ldsBytes;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
-    // XCD-grouped workgroup order (bd_tile_coords): whole tiles per XCD
-    a.xcd_group = g_opt_bd_xcd == 2 && (a.n_chunks * Y * S) % 8 == 0 ? 1 : 0;
+    // XCD-grouped workgroup order (bd_tile_coords): whole tiles per XCD, so a
+    // tile's Q rows come from HBM once (config 5: 49.7 vs 53.4 MB per launch,
+    // 24.8-24.9 vs 25.1-25.4 us kernel + merge; profiles/r04_f)
+    a.xcd_group = g_opt_bd_xcd != 1 && (a.n_chunks * Y * S) % 8 == 0 ? 1 : 0;
     // the chunk partials merge inside the launch (bd_tile_merge: the tile's
     // workgroups wait for each other, so only when the whole grid is
     // co-resident -- one workgroup per CU by LDS) or in a second launch

@@ -183,9 +183,9 @@ enum {
                                        device shared with other streams or processes (or CU-masked) a waiting
                                        workgroup's bounded poll can give up, and it then writes NaN rows while
                                        fattn_ext has returned FATTN_OK.  Diagnostics only; keep 0 in production */,
-    FATTN_OPT_BD_XCD = 25           /* batched-decode kernels: workgroup order. 0 = auto, 1 = plain (chunk
-                                       fastest), 2 = XCD-grouped: each of the 8 XCDs takes whole (kv head x row
-                                       tile)s, so a tile's Q rows come from HBM once, not once per chunk
+    FATTN_OPT_BD_XCD = 25           /* batched-decode kernels: workgroup order. 0 = auto (XCD-grouped), 1 = plain
+                                       (chunk fastest), 2 = XCD-grouped: each of the 8 XCDs takes whole (kv head x
+                                       row tile)s, so a tile's Q rows come from HBM once, not once per chunk
                                        (needs a grid of a multiple of 8 workgroups; otherwise plain) */
 };
 int fattn_set_option(int option, int value);

@@ -122,6 +122,7 @@ def test_bd_xcd_option():
         assert d5.startswith("fattn_bdp_kernel") and "(xcd order)" not in d5, d5
     with fattn.options({fattn.OPT_BD_XCD: 1}):
         assert "(xcd order)" not in fattn.describe(_params(NQ=64))
+    assert "(xcd order)" in fattn.describe(_params(NQ=64))  # (the default)
     with pytest.raises(Exception):
         fattn.set_option(fattn.OPT_BD_XCD, 3)
 

@@ -2,13 +2,14 @@
 # Round 4: XCD-grouped workgroup order for the batched-decode kernels
 # (--bd-xcd 2) against the plain order (--bd-xcd 1): time and HBM traffic
 # (FETCH_SIZE / WRITE_SIZE) on config 5, its 2-rank shard; the role form at head
-# dim 96 against the planner's previous pick (split kernel); their tests.
+# dim 96 against the planner's previous pick (split kernel); their tests and
+# the prefill tests at head dims 80 (f16) and 96.
 source tools/gpu_round.sh
 export TMPDIR=/tmp
 F=gpurun_out/r4f
 mkdir -p $F
 run t_bd 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider \
-  --timeout 250 --timeout-method thread -k "bdp or bd_ or xcd"
+  --timeout 250 --timeout-method thread -k "bdp or bd_ or xcd or pf_d80 or pf_d96"
 grep -E "passed|failed" gpurun_out/t_bd.log | tail -2 > $F/tests_tail.txt
 B="--no-cpu-baseline --no-prefill --no-scale-ref --no-copy-peak --steps 100 --warmup 10 --workload config5"
 line() { echo "$1 $(grep -o '"kernel_ms_avg": [0-9.]*' gpurun_out/$2.log | head -1) $(grep -o '"kernel_ms_median": [0-9.]*' gpurun_out/$2.log | head -1)" >> $F/ab.txt; }

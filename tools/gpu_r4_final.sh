@@ -1,18 +1,24 @@
 #!/bin/bash
-# Round-4 evidence on a final tree: GPU suite, smoke, the default bench line,
+# Round-4 evidence on a final tree (two calls): GPU suite and smoke; the default bench line,
 # the two-rank rehearsal of the default N > 1 line (config-5 head shard, one
 # gather per step), the rocprofv3 kernel-trace summary of the bench, and the
 # FETCH_SIZE / WRITE_SIZE passes (traffic files tagged with plan + source hash)
 # for config 3 and for the prefill shape (SURVEY's zero mask, as the bench's
 # prefill object).  Summaries land in gpurun_out/r4final/.
-#   PROF_ONLY=1: the profiling steps only.
+#   PART=tests: the GPU suite and smoke only; PART=prof: everything else.
 source tools/gpu_round.sh
 export TMPDIR=/tmp
 F=gpurun_out/r4final
 mkdir -p $F
+if [ "$PART" = tests ]; then
+  run pytest_gpu 1000 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
+  run smoke 150 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  tail -3 gpurun_out/pytest_gpu.log > $F/pytest_gpu_tail.txt 2>/dev/null
+  tail -2 gpurun_out/smoke.log > $F/smoke.txt 2>/dev/null
+  cat $F/pytest_gpu_tail.txt $F/smoke.txt
+  exit 0
+fi
 if [ -z "$PROF_ONLY" ]; then
-  run pytest_gpu 1100 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
-  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
   run bench 600 python bench.py
   grep '^{' gpurun_out/bench.log > $F/bench.json || true
   FATTN_BENCH_REHEARSE=1 run rehearse_head 300 python bench.py --gpus 2 --steps 20 --warmup 5
@@ -30,6 +36,4 @@ python tools/pmc_summary.py --kernel fattn_pf_kernel --traffic $F/traffic_r04_pr
   $(find gpurun_out/r4f_pfetch gpurun_out/r4f_pwrite -name "*counter_collection.csv") > $F/traffic_prefill.txt 2>&1
 for f in $(find gpurun_out/r4f_kt -name "*kernel_stats.csv"); do cp "$f" $F/kernel_stats.csv; done
 python tools/kstats.py $F/kernel_stats.csv > $F/kernel_stats_summary.txt
-tail -3 gpurun_out/pytest_gpu.log > $F/pytest_gpu_tail.txt 2>/dev/null
-tail -2 gpurun_out/smoke.log > $F/smoke.txt 2>/dev/null
-ls -la $F; cat $F/pytest_gpu_tail.txt $F/kernel_stats_summary.txt $F/traffic_cfg3.txt $F/traffic_prefill.txt $F/bench.json
+ls -la $F; cat $F/kernel_stats_summary.txt $F/traffic_cfg3.txt $F/traffic_prefill.txt $F/bench.json
