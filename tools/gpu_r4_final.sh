@@ -34,6 +34,12 @@ run fetch_pf 240 timeout -s KILL 230 rocprofv3 --output-format csv --pmc FETCH_S
 run write_pf 240 timeout -s KILL 230 rocprofv3 --output-format csv --pmc WRITE_SIZE -d gpurun_out/r4f_pwrite -o w -- python3 bench.py --prefill-only
 python tools/pmc_summary.py --kernel fattn_pf_kernel --traffic $F/traffic_r04_prefill.json --bench-line gpurun_out/fetch_pf.log \
   $(find gpurun_out/r4f_pfetch gpurun_out/r4f_pwrite -name "*counter_collection.csv") > $F/traffic_prefill.txt 2>&1
+# the prefill with its query tiles grouped by XCD (FATTN_OPT_PF_STAGGER bit 2): traffic and time
+run fetch_pf6 240 timeout -s KILL 230 rocprofv3 --output-format csv --pmc FETCH_SIZE -d gpurun_out/r4f_pfetch6 -o f -- python3 bench.py --prefill-only --pf-stagger 6
+run write_pf6 240 timeout -s KILL 230 rocprofv3 --output-format csv --pmc WRITE_SIZE -d gpurun_out/r4f_pwrite6 -o w -- python3 bench.py --prefill-only --pf-stagger 6
+python tools/pmc_summary.py --kernel fattn_pf_kernel --traffic $F/traffic_prefill_xcd.json --bench-line gpurun_out/fetch_pf6.log \
+  $(find gpurun_out/r4f_pfetch6 gpurun_out/r4f_pwrite6 -name "*counter_collection.csv") > $F/traffic_prefill_xcd.txt 2>&1
+for x in 2 6 2 6; do run pft_$x 120 python bench.py --prefill-only --pf-stagger $x; grep -o '"kernel_ms_avg": [0-9.]*' gpurun_out/pft_$x.log >> $F/prefill_xcd_ab.txt; echo " pf_stagger $x" >> $F/prefill_xcd_ab.txt; done
 for f in $(find gpurun_out/r4f_kt -name "*kernel_stats.csv"); do cp "$f" $F/kernel_stats.csv; done
 python tools/kstats.py $F/kernel_stats.csv > $F/kernel_stats_summary.txt
-ls -la $F; cat $F/kernel_stats_summary.txt $F/traffic_cfg3.txt $F/traffic_prefill.txt $F/bench.json
+ls -la $F; cat $F/kernel_stats_summary.txt $F/traffic_cfg3.txt $F/traffic_prefill.txt $F/traffic_prefill_xcd.txt $F/prefill_xcd_ab.txt $F/bench.json
