@@ -341,6 +341,8 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
              : pl.bdp             ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes)
              : pl.kt == FATTN_TYPE_Q8_0 ? BdCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
              : pl.kt == FATTN_TYPE_Q4_0 ? BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes
+             : pl.D == 64               ? BdCfg<FATTN_TYPE_F16, 64>::ldsBytes
+             : pl.D == 96               ? BdCfg<FATTN_TYPE_F16, 96>::ldsBytes
                                         : BdCfg<FATTN_TYPE_F16, 128>::ldsBytes;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     // XCD-grouped workgroup order (bd_tile_coords): whole tiles per XCD, so a
@@ -529,7 +531,8 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // Q4_0) have the role form only (config-5 shape at D = 64: 19.2 us against
     // 21.3 for the multi-query kernel, profiles/r04_e)
     pl.bd = pl.bdp = false;
-    const bool bd_dim = (D == 128 && (mq_ok || f16_ok)) || ((D == 64 || D == 96) && quant_ok && g_opt_bd != 2);
+    const bool bd_dim = (D == 128 && (mq_ok || f16_ok)) || ((D == 64 || D == 96) && quant_ok && g_opt_bd != 2) ||
+                        ((D == 64 || D == 96) && f16_ok);
     if (!pl.pf && g_opt_bd != 1 && bd_dim && N % kStep == 0 &&
         (g_opt_bd >= 2 || (NQ * a.rk2 >= kBdRows && wide))) {
         pl.bd = true;

@@ -55,11 +55,13 @@ constexpr int kBdKeys = 128;                   // keys per tile (four 32-key qua
 
 template <int KT, int D>
 struct BdCfg {
-    static_assert(D == 128, "four 32-dim blocks: one ggml block per V image block");
     // f16 K/V (the reference's own cache type): no raw tiles and no
     // dequantisation -- the LDS-DMA writes the images straight from the rows,
-    // into a ring of two image pairs (tile s computes while s + 1 lands)
+    // into a ring of two image pairs (tile s computes while s + 1 lands);
+    // head dims 64, 96, 128 (quantised K/V: 128, one ggml block per V image
+    // block and wave pair; fattn_bdp.h takes the others)
     static constexpr bool kF16 = KT == FATTN_TYPE_F16;
+    static_assert(D == 128 || (kF16 && (D == 64 || D == 96)), "");
     static constexpr int rowB = row_bytes<KT, D>();
     static constexpr int kvRaw = kBdKeys * rowB;                 // raw K (or V) bytes per tile
     static constexpr int rawBytes = (2 * kvRaw + 15) / 16 * 16;  // [K rows | V rows]
@@ -85,7 +87,7 @@ struct BdCfg {
     static constexpr int parkBytes = 4 * kBdRows * (D + 4) * 4 + 4 * kBdRows * 8;
     static constexpr int ldsBytes = maskEnd > parkBytes ? maskEnd : parkBytes;
     // Q staged as f32 rows [64][D] in the K image's place before the first tile
-    static_assert(kBdRows * D * 4 <= img && D * 4 / 16 == 32, "Q rows of 32 16-B chunks in the image's place");
+    static_assert(kBdRows * D * 4 <= img, "Q rows in the image's place");
     static_assert(ldsBytes <= 163840, "");
 };
 
@@ -107,10 +109,10 @@ __device__ __forceinline__ void bd_issue(const StepSrc& rs, int n0, uint32_t lds
 }
 
 // f16 K/V: tile rows -> the pair's f16 images by LDS-DMA, laid out exactly as
-// bd_dequant writes them (so the compute reads one layout).  64 1-KiB
-// instructions per tile, instruction j = wave + 8 i: j < 32 K (dim slice j / 4,
-// keys 32 (j % 4) ..: lane l = key pair half), else V (dim block (j - 32) / 8,
-// keys 16 ((j - 32) % 8) ..: lane l = key quarter chunk).  Each lane's SOURCE
+// bd_dequant writes them (so the compute reads one layout).  D / 2 1-KiB
+// instructions per tile (64 at D = 128), instruction j = wave + 8 i: j < D / 4
+// K (dim slice j / 4, keys 32 (j % 4) ..: lane l = key pair half), else V (dim
+// block (j - D / 4) / 8, keys 16 ((j - D / 4) % 8) ..: lane l = key quarter chunk).  Each lane's SOURCE
 // offset carries the image swizzle (the LDS side of a DMA is lane-linear,
 // cdna_hip_programming.md rule 21); rows are addressed by nb1, so llama.cpp's
 // [N][Hkv] cache works too.  Keys past N read past the descriptor: zeros.
@@ -121,17 +123,18 @@ __device__ __forceinline__ void bd_issue_f16(const StepSrc& rs, uint32_t k_nb1, 
     return;  // diagnostic build only
 #endif
     constexpr int img = kBdKeys * D * 2;
+    constexpr int NJK = D / 4;  // K instructions per tile (a multiple of 8)
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int j = wave + kBdWaves * i;  // (i < 4: K; wave-uniform)
-        if (i < 4) {
+    for (int i = 0; i < D / 16; i++) {
+        const int j = wave + kBdWaves * i;  // (i < D / 32: K; wave-uniform)
+        if (j < NJK) {
             const int w = j >> 2, kb = j & 3;
             const int key = 32 * kb + (lane >> 1);
             const int q = (lane & 1) ^ ((key >> 3) & 1);
             dma<16, kDecodeNT>(rs.k, lds + w * (kBdKeys * 32) + kb * 1024,
                                (uint32_t)(n0 + key) * k_nb1 + 32 * w + 16 * q);
         } else {
-            const int jj = j - 32, b = jj >> 3, kb = jj & 7;
+            const int jj = j - NJK, b = jj >> 3, kb = jj & 7;
             const int key = 16 * kb + (lane >> 2);
             const int c = (lane & 3) ^ ((key >> 2) & 3);
             dma<16, kDecodeNT>(rs.v, lds + img + b * (kBdKeys * 64) + kb * 1024,
@@ -430,19 +433,22 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
     // the waves); each wave then reads its rows' Q^T operands from there.
     // Rows past n_q come from past the descriptor: zeros.
     const i32x4 qs = make_srd(a.q + (int64_t)iq3 * a.q_nb3, a.q_span);
+    constexpr int CPR = D / 4;             // 16-B chunks of an f32 Q row
+    constexpr int SW = swz_mask(CPR);      // 31, 15, 7 at D = 128, 64, 96
     {
         constexpr int kQInst = kBdRows * D * 4 / 1024;  // 32 at D = 128
         static_assert(kQInst % kBdWaves == 0, "");
 #pragma unroll
         for (int i = 0; i < kQInst / kBdWaves; i++) {
-            const int j = wave + kBdWaves * i;              // instruction: rows 2j, 2j + 1
-            const int pr = 2 * j + (lane >> 5);              // packed row of this lane's 16 B
+            const int j = wave + kBdWaves * i;              // instruction: image chunks 64 j ..
+            const int g = kWave * j + lane;
+            const int pr = g / CPR, cc = g % CPR;            // packed row, chunk of this lane's 16 B
             const int rq = div_R(a, pr);
             const int q1 = qt * a.QPT + rq, q2 = ik2 * a.rk2 + (pr - rq * a.R);
-            // LDS chunk (lane & 31) of row pr holds the row's chunk (lane & 31) ^ (pr & 31):
-            // the operand reads below (32 rows at once) then spread over the banks
+            // LDS chunk cc of row pr holds the row's chunk cc ^ (pr & SW): the
+            // operand reads below (32 rows at once) then spread over the banks
             const uint32_t off = rq < a.QPT && q1 < a.NQ ? (uint32_t)q1 * (uint32_t)a.q_nb1 + (uint32_t)q2 * (uint32_t)a.q_nb2 +
-                                                 (((lane & 31) ^ (pr & 31)) * 16)
+                                                 ((cc ^ (pr & SW)) * 16)
                                            : a.q_span;
             dma<16>(qs, lds0 + C::qOff + j * 1024, off);
         }
@@ -523,8 +529,8 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
 #pragma unroll
     for (int kk = 0; kk < NK; kk++) {
         const float* qr = (const float*)(smem + C::qOff) + p * D;
-        const f32x4 x0 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h) ^ (p & 31)));
-        const f32x4 x1 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h + 1) ^ (p & 31)));
+        const f32x4 x0 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h) ^ (p & SW)));
+        const f32x4 x1 = *(const f32x4*)(qr + 4 * ((4 * kk + 2 * h + 1) ^ (p & SW)));
         f16x8 hq;
         hq.s0 = (f16)x0.x; hq.s1 = (f16)x0.y; hq.s2 = (f16)x0.z; hq.s3 = (f16)x0.w;
         hq.s4 = (f16)x1.x; hq.s5 = (f16)x1.y; hq.s6 = (f16)x1.z; hq.s7 = (f16)x1.w;

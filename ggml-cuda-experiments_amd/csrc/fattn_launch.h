@@ -179,15 +179,16 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
 }
 
 // D = 128: the all-waves form, or the role form for quantised K/V (pl.bdp);
-// D = 64 / 96: the role form only (the planner sets pl.bdp)
+// D = 64 / 96: the role form for quantised K/V (the planner sets pl.bdp), the
+// all-waves form's f16 image ring for f16
 template <int KT, int D, bool HM>
 int launch_bd_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     void (*kern)(SplitArgs) = nullptr;
-    if constexpr (D == 128) kern = fattn_bd_kernel<KT, D, HM>;
+    if constexpr (D == 128 || KT == FATTN_TYPE_F16) kern = fattn_bd_kernel<KT, D, HM>;
     if constexpr (KT != FATTN_TYPE_F16) {
         if (pl.bdp) kern = fattn_bdp_kernel<KT, D, HM>;
     }
-    if (kern == nullptr || (D != 128 && !pl.bdp)) return FATTN_ERR_UNSUPPORTED_TYPE;
+    if (kern == nullptr || (D != 128 && KT != FATTN_TYPE_F16 && !pl.bdp)) return FATTN_ERR_UNSUPPORTED_TYPE;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         hipLaunchKernelGGL(kern, pl.grid, dim3(kBdWaves * kWave), pl.lds, st, pl.a);
         if (pl.a.merge_launch == 1) {
@@ -249,9 +250,7 @@ int launch_types(const Plan& pl, hipStream_t st, const Events& ev) {
         if (pl.bd) {
             if (pl.kt == FATTN_TYPE_Q8_0 && pl.vt == FATTN_TYPE_Q8_0) return launch_bd<FATTN_TYPE_Q8_0, D>(pl, st, ev);
             if (pl.kt == FATTN_TYPE_Q4_0 && pl.vt == FATTN_TYPE_Q4_0) return launch_bd<FATTN_TYPE_Q4_0, D>(pl, st, ev);
-            if constexpr (D == 128) {
-                if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_bd<FATTN_TYPE_F16, D>(pl, st, ev);
-            }
+            if (pl.kt == FATTN_TYPE_F16 && pl.vt == FATTN_TYPE_F16) return launch_bd<FATTN_TYPE_F16, D>(pl, st, ev);
             return FATTN_ERR_UNSUPPORTED_TYPE;
         }
     }

@@ -73,6 +73,8 @@ def test_workspace_size_config3():
     (dict(NQ=64, H=16, Hkv=16), ["fattn_bdp_kernel", "+ fattn_bd_merge_kernel", "grid(16,16,1)"]),  # config 5, 2-rank shard
     (dict(NQ=256), ["fattn_bdp_kernel", "grid(2,128,1)"]),                                  # batched: 4 row tiles
     (dict(NQ=64, kt=fattn.TYPE_F16), ["fattn_bd_kernel<f16,D128", "+ fattn_bd_merge_kernel"]),  # config 5 shape, f16
+    (dict(D=64, NQ=64, kt=fattn.TYPE_F16), ["fattn_bd_kernel<f16,D64"]),                    # f16 at D = 64 / 96
+    (dict(D=96, NQ=64, kt=fattn.TYPE_F16), ["fattn_bd_kernel<f16,D96"]),
     (dict(NQ=64, H=24, Hkv=4), ["fattn_bdp_kernel<q8_0", "grid(8,28,1)"]),                  # GQA 6: 7 tiles of 10 queries
     (dict(NQ=64, H=4, Hkv=4, kt=fattn.TYPE_F16), ["fattn_split_kernel<f16,f16"]),           # f16, 8-rank shard
     (dict(NQ=8, H=32, Hkv=8), ["fattn_split_kernel", "+ fattn_merge_kernel"]),              # < 64 rows per kv head
@@ -81,7 +83,7 @@ def test_workspace_size_config3():
     (dict(D=96, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16), ["fattn_pf_kernel<f16,D96"]),
     (dict(D=80, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16), ["fattn_pf_kernel<f16,D80"]),      # D = 80 prefill (f16)
     (dict(D=256, NQ=4096, H=16, Hkv=16), ["fattn_mq_kernel<q8_0,D256,4waves"]),              # D = 256 prefill
-], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "bd_f16",
+], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "bd_f16", "bd_f16_d64", "bd_f16_d96",
         "bd_gqa6", "bd_f16_shard", "split_nq8_gqa", "pf_d64", "pf_d96", "pf_d96_f16", "pf_d80_f16", "mq_d256"])
 def test_planner_picks(kw, want):
     """The plans the round-2 measurements chose, at 256 CUs:
@@ -101,9 +103,9 @@ def test_bd_option_forms():
     with fattn.options({fattn.OPT_BD: 3}):
         assert fattn.describe(_params(NQ=64, kt=fattn.TYPE_Q4_0)).startswith("fattn_bdp_kernel<q4_0")
         assert fattn.describe(_params(NQ=64, kt=fattn.TYPE_F16)).startswith("fattn_bd_kernel<f16")
-        # head dim 64: the role form (quantised only)
+        # head dim 64: the role form (quantised; f16 keeps the image ring)
         assert fattn.describe(_params(D=64, NQ=64)).startswith("fattn_bdp_kernel<q8_0,D64")
-        assert "fattn_bd" not in fattn.describe(_params(D=64, NQ=64, kt=fattn.TYPE_F16))
+        assert fattn.describe(_params(D=64, NQ=64, kt=fattn.TYPE_F16)).startswith("fattn_bd_kernel<f16,D64")
     assert fattn.describe(_params(D=64, NQ=64)).startswith("fattn_bdp_kernel<q8_0,D64")  # (auto too)
     assert fattn.describe(_params(D=96, NQ=64, kt=fattn.TYPE_Q4_0)).startswith("fattn_bdp_kernel<q4_0,D96")
     with fattn.options({fattn.OPT_BD: 2}):  # (the all-waves form is D = 128 only: the multi-query kernel)

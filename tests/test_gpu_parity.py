@@ -342,6 +342,26 @@ def test_bd_sweep(dev, bd_force, case):
     assert attn_rel_err(run_gpu(p), p.oracle()) <= RTOL
 
 
+@pytest.mark.parametrize("D", [64, 96])
+@pytest.mark.parametrize("case", [
+    dict(NQ=64, H=8, Hkv=8, N=4096, mask="random"),                  # config-5 shape, 8 heads
+    dict(NQ=16, H=16, Hkv=4, N=1024, mask="causal"),                 # GQA
+    dict(NQ=40, H=12, Hkv=4, N=800, mask="random"),                  # R = 3, ragged rows, partial tile
+    dict(NQ=64, H=4, Hkv=2, N=1056, mask="neginf_blocks", layout="pos"),  # llama.cpp's [N][Hkv] cache
+    dict(NQ=33, H=2, Hkv=2, N=1024, mask="none", S=2),               # ne03 batch, no mask
+], ids=["cfg5x8", "gqa4", "gqa3", "pos", "batch2"])
+def test_bd_f16_dims(dev, bd_force, case, D):
+    """The f16 image ring of the batched-decode kernel at head dims 64 and 96
+    (D / 2 1-KiB image pieces per 128-key tile; Q rows of D / 4 16-B chunks)."""
+    p = make_problem(D=D, kv_type="f16", seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000 + D, **case)
+    t = upload(p, dev)
+    d = fattn.Attention(*views(p, t), t["dst"], p.scale).describe()
+    assert d.startswith("fattn_bd_kernel<f16") and f"D{D}" in d, d
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 # ------------------------------------------------------------------ batched decode, role form (fattn_bdp.h)
 # Q8_0 / Q4_0: compute waves 0-3 and build (dequantising) waves 4-7, 64-key
 # tiles, one barrier per tile; FATTN_OPT_BD = 3 forces it (0 picks it too).
