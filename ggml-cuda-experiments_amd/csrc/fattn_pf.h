@@ -73,7 +73,10 @@ struct PfCfg {
     static constexpr int rawOff = nPairs * pairBytes;
     static constexpr int maskOff = rawOff + nRaw * rawBytes;
     static constexpr int maskSlot = kPfRowsW * 128;                 // 32 rows x 64 keys x f16
-    static constexpr int ldsBytes = maskOff + kPfWaves * maskSlot;
+    // epilogue: every wave parks its 32 normalised rows, [8 waves][32 rows][DI + 4] f32
+    static constexpr int parkBytes = kPfWaves * kPfRowsW * (DI + 4) * 4;
+    static constexpr int loopBytes = maskOff + kPfWaves * maskSlot;
+    static constexpr int ldsBytes = loopBytes > parkBytes ? loopBytes : parkBytes;
     static constexpr int NI = (kvRaw + 1023) / 1024;                // 1-KiB DMA instructions per K (or V) tile
     // instructions j = 0 .. 2*NI-1 (K then V) go to wave j % 8
     static constexpr int ni_wave(int w) { return (2 * NI - w + kPfWaves - 1) / kPfWaves; }
@@ -649,12 +652,21 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
 #endif
 #undef PF_T
 
-    // ---- normalise and store: O^T element j of block db is dim
-    // 32db + 8(j/4) + 4h + (j%4) of this lane's row
+    // ---- normalise and store.  O^T element j of block db is dim 32db + 8(j/4)
+    // + 4h + (j%4) of this lane's row: stored straight from that layout, one
+    // instruction would write 32 B into each of 32 rows -- partial lines, which
+    // the memory writes as whole granules (WRITE_SIZE 2.1x the output on the
+    // prefill shape, profiles/r04_prof1).  So each wave parks its 32 normalised
+    // rows in LDS ([32 rows][DI + 4] f32, its own region; every wave is past
+    // the loop's last LDS read: one barrier) and stores them back as whole
+    // rows, 64 lanes x 16 B = 1 KiB of contiguous row bytes per instruction
+    // (cdna_hip_programming.md T21).
     const float l_tot = xor32_pair(l2.x + l2.y, false);
+#ifdef FATTN_PF_DIRECT_STORE
+    // diagnostic build only (A/B): the row-per-lane stores from the accumulator layout
     if (row_ok) {
         float* out = a.dst + (((int64_t)iq3 * a.NQ + iq1) * a.H + iq2) * D + 4 * h;
-        const float inv = 1.0f / l_tot;  // fully masked row -> NaN like the reference
+        const float inv = 1.0f / l_tot;
 #pragma unroll
         for (int db = 0; db < NDB; db++) {
 #pragma unroll
@@ -662,8 +674,41 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
                 f32x4 v;
 #pragma unroll
                 for (int r = 0; r < 4; r++) v[r] = l_tot == 0.0f ? __builtin_nanf("") : o[db][4 * u + r] * inv;
-                if (32 * db + 8 * u + 4 * h < D) *(f32x4*)(out + 32 * db + 8 * u) = v;  // (D = 80: no padding dims)
+                if (32 * db + 8 * u + 4 * h < D) *(f32x4*)(out + 32 * db + 8 * u) = v;
             }
+        }
+    }
+    return;
+#endif
+    constexpr int kStride = C::DI + 4;  // floats (+16 B a row: the parking writes are conflict-free)
+    static_assert(kPfWaves * kPfRowsW * kStride * 4 <= C::ldsBytes, "");
+    __syncthreads();  // every wave is done with the images, raw tiles and mask slots
+    float* park = (float*)smem + wave * (kPfRowsW * kStride);
+    {
+        const float inv = 1.0f / l_tot;  // fully masked row -> NaN like the reference
+        float* pk = park + c32 * kStride + 4 * h;
+#pragma unroll
+        for (int db = 0; db < NDB; db++) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; r++) v[r] = l_tot == 0.0f ? __builtin_nanf("") : o[db][4 * u + r] * inv;
+                *(f32x4*)(pk + 32 * db + 8 * u) = v;
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the wave reads back only its own rows)
+    constexpr int CPR = D / 4;                     // 16-B chunks of a dst row (D = 80: 20)
+    static_assert(kPfRowsW * CPR % kWave == 0, "");
+#pragma unroll
+    for (int i = 0; i < kPfRowsW * CPR / kWave; i++) {
+        const int g = kWave * i + lane;
+        const int r = g / CPR, c = g % CPR;        // row of the wave, chunk of the row
+        int q1, q2;
+        if (row_of(kPfRowsW * wave + r, q1, q2)) {
+            const f32x4 v = *(const f32x4*)(park + r * kStride + 4 * c);
+            *(f32x4*)(a.dst + (((int64_t)iq3 * a.NQ + q1) * a.H + q2) * D + 4 * c) = v;
         }
     }
 }
