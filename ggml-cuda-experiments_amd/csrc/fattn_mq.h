@@ -135,22 +135,34 @@ __device__ __forceinline__ void mq_wait_tiles(int wave, int pending) {
 // into the two 16-B f16 chunks 4b+2h, 4b+2h+1: h(q * d), one f16 rounding
 // (src/utils.h:10-11 dequantise-then-round).  The qs bytes are only 2-byte
 // aligned: dword reads + v_alignbyte with a runtime shift.
+// (in two steps, so a caller can issue the LDS reads early and convert later:
+// dequant_half_load -> HalfRaw -> dequant_half_cvt)
+struct HalfRaw {
+    uint32_t u[5];  // the dwords holding the 16 qs bytes
+    uint32_t dw;    // the dword holding the f16 scale
+    uint32_t blk;   // byte offset of the block in the tile
+};
 template <int KT, int D>
-__device__ __forceinline__ void dequant_half(const uint8_t* raw, int row, int b, int h, u32x4 (&out)[2]) {
+__device__ __forceinline__ HalfRaw dequant_half_load(const uint8_t* raw, int row, int b, int h) {
     constexpr int RB = row_bytes<KT, D>();
     constexpr int BB = TypeInfo<KT>::block_bytes;
-    const uint32_t blk = row * RB + BB * b;
+    HalfRaw r;
+    r.blk = row * RB + BB * b;
     // Q8_0: qs bytes 16h..16h+15; Q4_0: all 16 qs bytes (low / high nibbles)
-    const uint32_t q0 = blk + 2 + (KT == FATTN_TYPE_Q8_0 ? 16 * h : 0);
-    const uint32_t qb = q0 & ~3u, sh = q0 & 3u;
-    uint32_t u[5];
+    const uint32_t q0 = r.blk + 2 + (KT == FATTN_TYPE_Q8_0 ? 16 * h : 0);
+    const uint32_t qb = q0 & ~3u;
 #pragma unroll
-    for (int j = 0; j < 5; j++) u[j] = *(const uint32_t*)(raw + qb + 4 * j);
+    for (int j = 0; j < 5; j++) r.u[j] = *(const uint32_t*)(raw + qb + 4 * j);
+    r.dw = *(const uint32_t*)(raw + (r.blk & ~3u));
+    return r;
+}
+template <int KT>
+__device__ __forceinline__ void dequant_half_cvt(const HalfRaw& r, int h, u32x4 (&out)[2]) {
+    const uint32_t sh = (r.blk + 2 + (KT == FATTN_TYPE_Q8_0 ? 16 * h : 0)) & 3u;
     uint32_t q[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) q[j] = alignbyte(u[j + 1], u[j], sh);
-    const uint32_t dw = *(const uint32_t*)(raw + (blk & ~3u));
-    const f16x2 d = bcast_h((blk & 2) ? (dw >> 16) : dw);
+    for (int j = 0; j < 4; j++) q[j] = alignbyte(r.u[j + 1], r.u[j], sh);
+    const f16x2 d = bcast_h((r.blk & 2) ? (r.dw >> 16) : r.dw);
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         f16x2 h0, h1, h2, h3;
@@ -165,6 +177,10 @@ __device__ __forceinline__ void dequant_half(const uint8_t* raw, int row, int b,
         h0 *= d; h1 *= d; h2 *= d; h3 *= d;
         out[k] = u32x4{as_u32(h0), as_u32(h1), as_u32(h2), as_u32(h3)};
     }
+}
+template <int KT, int D>
+__device__ __forceinline__ void dequant_half(const uint8_t* raw, int row, int b, int h, u32x4 (&out)[2]) {
+    dequant_half_cvt<KT>(dequant_half_load<KT, D>(raw, row, b, h), h, out);
 }
 
 // Tile `rb` (raw) -> f16 images k16 / v16 (decode kernel's swizzles).  Units

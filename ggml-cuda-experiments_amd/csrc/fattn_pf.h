@@ -172,18 +172,34 @@ __device__ __forceinline__ void pf_vm_wait(int nraw, int nmask) {
 
 // raw tile -> f16 images: wave w dequantises half h = w & 1 of block b = w >> 1
 // of row `lane`, for K (into dim slice 2b + h) and V (dim block b, chunks 2h, 2h+1)
-// (D = 64: two blocks, waves 0-3; waves 4-7 -- the prioritised half -- skip it)
+// (D = 64: two blocks, waves 0-3; waves 4-7 -- the prioritised half -- skip it).
+// In two steps: pf_dequant_load issues the LDS reads of the raw words, and
+// pf_dequant_store converts them and writes the images -- the tile body
+// issues the reads of tile s + 1 before its own S^T operand reads, so their
+// latency runs under those reads and the S^T chains instead of in front of them.
+struct PfRaw {
+    HalfRaw k, v;
+};
 template <int KT, int D>
-__device__ __forceinline__ void pf_dequant(const uint8_t* rb, uint8_t* k16, uint8_t* v16, int wave, int lane) {
+__device__ __forceinline__ PfRaw pf_dequant_load(const uint8_t* rb, int wave, int lane) {
+    using C = PfCfg<KT, D>;
+    const int b = wave >> 1, h = wave & 1;
+    PfRaw r;
+    if (b >= D / QK) return r;  // wave-uniform (D = 64: waves 4-7 idle; r unused)
+    r.k = dequant_half_load<KT, D>(rb, lane, b, h);
+    r.v = dequant_half_load<KT, D>(rb + C::kvRaw, lane, b, h);
+    return r;
+}
+template <int KT, int D>
+__device__ __forceinline__ void pf_dequant_store(const PfRaw& r, uint8_t* k16, uint8_t* v16, int wave, int lane) {
 #ifdef FATTN_MQ_NODEQ
     return;  // diagnostic build only
 #endif
-    using C = PfCfg<KT, D>;
     const int b = wave >> 1, h = wave & 1;
     if (b >= D / QK) return;  // wave-uniform
     u32x4 ck[2], cv[2];
-    dequant_half<KT, D>(rb, lane, b, h, ck);
-    dequant_half<KT, D>(rb + C::kvRaw, lane, b, h, cv);
+    dequant_half_cvt<KT>(r.k, h, ck);
+    dequant_half_cvt<KT>(r.v, h, cv);
     uint8_t* kd = k16 + wave * (kPfKeys * 32) + lane * 32;
     const int sk = (lane >> 3) & 1;
     *(u32x4*)(kd + sk * 16) = ck[0];
@@ -192,6 +208,11 @@ __device__ __forceinline__ void pf_dequant(const uint8_t* rb, uint8_t* k16, uint
     const int sv = (lane >> 2) & 3;
     *(u32x4*)(vd + ((2 * h) ^ sv) * 16) = cv[0];
     *(u32x4*)(vd + ((2 * h + 1) ^ sv) * 16) = cv[1];
+}
+
+template <int KT, int D>
+__device__ __forceinline__ void pf_dequant(const uint8_t* rb, uint8_t* k16, uint8_t* v16, int wave, int lane) {
+    pf_dequant_store<KT, D>(pf_dequant_load<KT, D>(rb, wave, lane), k16, v16, wave, lane);
 }
 
 __device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
@@ -424,15 +445,26 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         // (the round-1 phase stagger -- waves 4-7 dequantising after their
         // compute, FATTN_OPT_PF_STAGGER bit 0 -- measured neutral and was
         // removed: it kept the dequantisation's state live across the compute)
-        auto dequant_next = [&] {
-            if constexpr (!C::kDirect) {
-                if (s + 1 < ntiles)
-                    pf_dequant<KT, D>(raw_ptr(s + 1), smem + (P ^ 1) * C::pairBytes,
-                                      smem + (P ^ 1) * C::pairBytes + C::img, wave, lane);
-            }
-        };
-        dequant_next();
+#ifdef FATTN_PF_DEQ_INLINE
+        // diagnostic build only (A/B): reads, conversion and image writes of
+        // tile s + 1 in one piece before tile s's compute
+        if constexpr (!C::kDirect) {
+            if (s + 1 < ntiles)
+                pf_dequant<KT, D>(raw_ptr(s + 1), smem + (P ^ 1) * C::pairBytes,
+                                  smem + (P ^ 1) * C::pairBytes + C::img, wave, lane);
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PfRaw deq;
+        const bool deq_next = false;
+#else
+        // the raw words of tile s + 1 (this wave's half block): reads issued now,
+        // converted and written after the S^T chains (pf_dequant_load)
+        PfRaw deq;
+        const bool deq_next = !C::kDirect && s + 1 < ntiles;  // workgroup-uniform
+        if constexpr (!C::kDirect) {
+            if (deq_next) deq = pf_dequant_load<KT, D>(raw_ptr(s + 1), wave, lane);
+        }
+#endif
         PF_T(2);
         // quantised: raw tile s + 3 is issued during this tile's first S^T chain
         // (an issue that stalls on a full memory queue then waits beside the
@@ -547,6 +579,13 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         }
         __builtin_amdgcn_sched_barrier(0);
         }  // live, first half
+        // quantised: tile s + 1's images from the raw words read above (the
+        // conversion VALU runs under the tail of the S^T chains)
+        if constexpr (!C::kDirect) {
+            if (deq_next)
+                pf_dequant_store<KT, D>(deq, smem + (P ^ 1) * C::pairBytes, smem + (P ^ 1) * C::pairBytes + C::img, wave,
+                                        lane);
+        }
         // quantised: raw tile s + 3, issued while the S^T chains execute (a
         // skipped tile issues it here too)
         issue_raw();
