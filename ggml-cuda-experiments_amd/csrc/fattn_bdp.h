@@ -123,30 +123,53 @@ __device__ __forceinline__ void bdp_issue(const StepSrc& rs, int n0, uint32_t ld
 // build wave bw: half-blocks hb = bw, bw + 4, ... (< D / 16) of key `lane` --
 // half hb & 1 of ggml block hb >> 1 -- K into dim slice hb and V into dim
 // block hb >> 1, in the layouts fattn_bd.h / fattn_pf.h read (D = 96: waves 4
-// and 5 take two half-blocks, waves 6 and 7 one)
+// and 5 take two half-blocks, waves 6 and 7 one).  In two steps: the LDS reads
+// of the raw words (bdp_dequant_load) go before the wave's DMA issue of the
+// next raw tile, which stalls on a full memory pipeline (profiles/r04_c), so
+// their latency runs under that stall; bdp_dequant_store converts and writes.
+constexpr int kBdpHpw = 2;  // half-blocks per build wave, at most (D <= 128)
+struct BdpRaw {
+    HalfRaw k[kBdpHpw], v[kBdpHpw];
+};
 template <int KT, int D>
-__device__ __forceinline__ void bdp_dequant(const uint8_t* raw, uint8_t* k16, uint8_t* v16, int bw, int lane) {
+__device__ __forceinline__ BdpRaw bdp_dequant_load(const uint8_t* raw, int bw, int lane) {
+    using C = BdpCfg<KT, D>;
+    static_assert((D / 16 + 3) / 4 <= kBdpHpw, "");
+    BdpRaw r;
+#pragma unroll
+    for (int i = 0; i < (D / 16 + 3) / 4; i++) {
+        const int hb = bw + 4 * i;
+        if (hb >= D / 16) break;  // wave-uniform
+        r.k[i] = dequant_half_load<KT, D>(raw, lane, hb >> 1, hb & 1);
+        r.v[i] = dequant_half_load<KT, D>(raw + C::kvRaw, lane, hb >> 1, hb & 1);
+    }
+    return r;
+}
+template <int KT, int D>
+__device__ __forceinline__ void bdp_dequant_store(const BdpRaw& r, uint8_t* k16, uint8_t* v16, int bw, int lane) {
 #ifdef FATTN_MQ_NODEQ
     return;  // diagnostic build only
 #endif
-    using C = BdpCfg<KT, D>;
-    const int r = lane;
-    const int sk = (r >> 3) & 1, sv = (r >> 2) & 3;
+    const int sk = (lane >> 3) & 1, sv = (lane >> 2) & 3;
 #pragma unroll
     for (int i = 0; i < (D / 16 + 3) / 4; i++) {
         const int hb = bw + 4 * i;
         if (hb >= D / 16) break;  // wave-uniform
         const int b = hb >> 1, h = hb & 1;
         u32x4 ck[2], cv[2];
-        dequant_half<KT, D>(raw, r, b, h, ck);
-        dequant_half<KT, D>(raw + C::kvRaw, r, b, h, cv);
-        uint8_t* kd = k16 + (2 * b + h) * (kBdpKeys * 32) + r * 32;
+        dequant_half_cvt<KT>(r.k[i], h, ck);
+        dequant_half_cvt<KT>(r.v[i], h, cv);
+        uint8_t* kd = k16 + hb * (kBdpKeys * 32) + lane * 32;
         *(u32x4*)(kd + sk * 16) = ck[0];
         *(u32x4*)(kd + (sk ^ 1) * 16) = ck[1];
-        uint8_t* vd = v16 + b * (kBdpKeys * 64) + r * 64;
+        uint8_t* vd = v16 + b * (kBdpKeys * 64) + lane * 64;
         *(u32x4*)(vd + ((2 * h) ^ sv) * 16) = cv[0];
         *(u32x4*)(vd + ((2 * h + 1) ^ sv) * 16) = cv[1];
     }
+}
+template <int KT, int D>
+__device__ __forceinline__ void bdp_dequant(const uint8_t* raw, uint8_t* k16, uint8_t* v16, int bw, int lane) {
+    bdp_dequant_store<KT, D>(bdp_dequant_load<KT, D>(raw, bw, lane), k16, v16, bw, lane);
 }
 
 // build waves: at most n (0 .. nRaw - 1) raw groups issued after the awaited one in flight
@@ -342,17 +365,27 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
         // (s + 1) % 2 is free; raw s + 1 is complete (its build waves waited)
         __syncthreads();
         if (s < 4) FATTN_STAMP(3 + s);
+        // build waves: the raw words of tile s + 1 read first (their latency
+        // runs under the DMA issue below)
+        BdpRaw deq;
+#ifndef FATTN_BDP_READ_LATE
+        if (!compute && s + 1 < ntiles) deq = bdp_dequant_load<KT, D>(raw_ptr(s + 1), bw, lane);
+#endif
         // every wave: its pieces of raw s + nRaw into raw s's slot (every build
         // wave read it before this barrier)
         if (s == 2) FATTN_STAMP(14);
         if (s + C::nRaw < ntiles) bdp_issue<KT, D>(rs, c_lo + (s + C::nRaw) * kBdpKeys, raw_lds(s + C::nRaw), wave, lane);
         if (s == 2) FATTN_STAMP(15);
+#ifdef FATTN_BDP_READ_LATE
+        // diagnostic build only (A/B): the raw words read after the DMA issue
+        if (!compute && s + 1 < ntiles) deq = bdp_dequant_load<KT, D>(raw_ptr(s + 1), bw, lane);
+#endif
         if (!compute) {
             // ---- build: raw s + 1 -> pair (s + 1) % 2; then wait for this
             // wave's pieces of raw s + 2 (raw s + 3 .. s + nRaw may fly on)
             if (s + 1 < ntiles) {
-                bdp_dequant<KT, D>(raw_ptr(s + 1), smem + ((s + 1) & 1) * C::pair,
-                                   smem + ((s + 1) & 1) * C::pair + C::img, bw, lane);
+                bdp_dequant_store<KT, D>(deq, smem + ((s + 1) & 1) * C::pair, smem + ((s + 1) & 1) * C::pair + C::img, bw,
+                                         lane);
                 if (s + 2 < ntiles) bdp_build_wait<KT, D>(min(C::nRaw - 2, ntiles - 3 - s));
             }
             if (s < 4) FATTN_STAMP(7 + s);
