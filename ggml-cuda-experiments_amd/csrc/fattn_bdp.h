@@ -405,10 +405,12 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
                 mh[u] = *(const u32x2*)(ms + u * 512);
                 open |= (mh[u].x ^ 0xFC00FC00u) | (mh[u].y ^ 0xFC00FC00u);
             }
+#ifndef FATTN_BDP_MASK_LATE
             if (s + 2 < ntiles) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot has been read
                 mask_issue(s + 2);
             }
+#endif
         }
         // this wave's 32 keys past the chunk, or -inf for every valid row: nothing to add (exact)
         const bool live = c_lo + s * kBdpKeys + 32 * kh < c_hi &&
@@ -487,6 +489,15 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
                 for (int db = 0; db < NDB; db++) o[db] = mfma32(__builtin_bit_cast(f16x8, va[db]), pb[q], o[db]);
             }
         }
+#ifdef FATTN_BDP_MASK_LATE
+        // diagnostic build only (A/B): mask s + 2 issued after tile s's compute
+        if constexpr (HM) {
+            if (s + 2 < ntiles) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                mask_issue(s + 2);
+            }
+        }
+#endif
         // before the next barrier: mask s + 1 and this wave's pieces of raw s + 2
         // landed.  Issue order per tile: raw s + nRaw, then mask s + 2, so raw
         // s + 2 (issued with tile s + 2 - nRaw <= s - 1, or in the prologue) is

@@ -173,10 +173,9 @@ __device__ __forceinline__ void pf_vm_wait(int nraw, int nmask) {
 // raw tile -> f16 images: wave w dequantises half h = w & 1 of block b = w >> 1
 // of row `lane`, for K (into dim slice 2b + h) and V (dim block b, chunks 2h, 2h+1)
 // (D = 64: two blocks, waves 0-3; waves 4-7 -- the prioritised half -- skip it).
-// In two steps: pf_dequant_load issues the LDS reads of the raw words, and
-// pf_dequant_store converts them and writes the images -- the tile body
-// issues the reads of tile s + 1 before its own S^T operand reads, so their
-// latency runs under those reads and the S^T chains instead of in front of them.
+// In two steps (pf_dequant_load: the LDS reads of the raw words;
+// pf_dequant_store: conversion and image writes), so an A/B build can split
+// them around the S^T chains (FATTN_PF_DEQ_EARLY).
 struct PfRaw {
     HalfRaw k, v;
 };
@@ -445,9 +444,12 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         // (the round-1 phase stagger -- waves 4-7 dequantising after their
         // compute, FATTN_OPT_PF_STAGGER bit 0 -- measured neutral and was
         // removed: it kept the dequantisation's state live across the compute)
-#ifdef FATTN_PF_DEQ_INLINE
-        // diagnostic build only (A/B): reads, conversion and image writes of
-        // tile s + 1 in one piece before tile s's compute
+#ifndef FATTN_PF_DEQ_EARLY
+        // reads, conversion and image writes of tile s + 1 in one piece before
+        // tile s's compute.  (FATTN_PF_DEQ_EARLY, A/B builds: the raw words read
+        // before the S^T operand reads and converted after the S^T chains --
+        // Q8_0 zero mask 439-452 vs 439-449 us, random mask 458-480 vs 483-486,
+        // Q4_0 432-441 vs 419-434: no net gain for 14 more VGPRs, profiles/r04_i)
         if constexpr (!C::kDirect) {
             if (s + 1 < ntiles)
                 pf_dequant<KT, D>(raw_ptr(s + 1), smem + (P ^ 1) * C::pairBytes,
@@ -457,8 +459,8 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         PfRaw deq;
         const bool deq_next = false;
 #else
-        // the raw words of tile s + 1 (this wave's half block): reads issued now,
-        // converted and written after the S^T chains (pf_dequant_load)
+        // diagnostic build only: the raw words of tile s + 1 (this wave's half
+        // block) read now, converted and written after the S^T chains
         PfRaw deq;
         const bool deq_next = !C::kDirect && s + 1 < ntiles;  // workgroup-uniform
         if constexpr (!C::kDirect) {
