@@ -349,11 +349,25 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
             moff[k] = ok ? (uint32_t)q1 * (uint32_t)a.m_nb1 + 16 * pc : a.m_span;
         }
     }
+    // tile s's mask block is +-0 everywhere (flag 2; wave-uniform)
+    auto zero_of = [&](int s) { return s < 256 && ((zb[s >> 6] >> (s & 63)) & 1); };
+    // quantised K/V: such a tile's mask DMA is not issued at all (the counted
+    // waits below leave its group out); f16: it goes through an offset past the
+    // descriptor (no traffic, the instruction count unchanged).  Every DMA
+    // instruction occupies the CU's memory pipeline, whose issue stalls are a
+    // cost of their own
+#ifdef FATTN_PF_ZERO_DMA
+    constexpr bool kSkipZero = false;  // diagnostic build only (A/B)
+#else
+    constexpr bool kSkipZero = !C::kDirect;
+#endif
+    auto mask_groups = [&](int s) { return (HM && !(kSkipZero && zero_of(s))) ? 1 : 0; };
     auto mask_issue = [&](int s) {
         if constexpr (HM) {
 #ifndef FATTN_MQ_NOMEM
             const uint32_t n2 = (uint32_t)(t0 + s) * kPfKeys * 2;
-            const bool zero = s < 256 && ((zb[s >> 6] >> (s & 63)) & 1);  // wave-uniform
+            const bool zero = zero_of(s);
+            if (kSkipZero && zero) return;
 #pragma unroll
             for (int k = 0; k < C::NIM; k++) {
                 const uint32_t off = (moff[k] == a.m_span || zero) ? a.m_span : moff[k] + n2;
@@ -397,7 +411,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         for (int s = 0; s < 3 && s < ntiles; s++) pf_issue<KT, D>(rs, (t0 + s) * kPfKeys, raw_lds(s), wave, lane);
         if (ntiles > 0) mask_issue(0);
         // raw 0 landed (raw 1, 2 and mask 0 may fly on)
-        pf_vm_wait<KT, D>(min(2, ntiles - 1), ntiles > 0 ? NM : 0);
+        pf_vm_wait<KT, D>(min(2, ntiles - 1), ntiles > 0 ? mask_groups(0) : 0);
         __syncthreads();
         if (ntiles > 0) pf_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, wave, lane);
     }
@@ -432,7 +446,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         // quantised: raw s+1 landed (raw s+2 and mask s may fly on);
         // f16: image pair of tile s landed (tile s+1 and mask s may fly on)
         PF_T(7);
-        pf_vm_wait<KT, D>(s + C::ahead - 1 < ntiles ? 1 : 0, NM);
+        pf_vm_wait<KT, D>(s + C::ahead - 1 < ntiles ? 1 : 0, C::kDirect ? NM : mask_groups(s));
         __syncthreads();
         PF_T(0);
         if constexpr (C::kDirect) {
@@ -498,7 +512,7 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
         u32x2 mk[2][4];
         bool live = true;
         if constexpr (HM) {
-            const bool zero = s < 256 && ((zb[s >> 6] >> (s & 63)) & 1);  // workgroup-uniform
+            const bool zero = zero_of(s);  // workgroup-uniform
             if (!zero) {
                 pf_vm_wait<KT, D>(mask_younger, 0);
 #pragma unroll
