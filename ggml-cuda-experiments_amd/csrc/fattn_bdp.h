@@ -491,6 +491,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
         }
 #ifdef FATTN_BDP_MASK_LATE
         // diagnostic build only (A/B): mask s + 2 issued after tile s's compute
+        // (config 5: 24.6-25.2 vs 24.7-25.4 us, neutral, profiles/r04_j)
         if constexpr (HM) {
             if (s + 2 < ntiles) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -351,15 +351,15 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
     }
     // tile s's mask block is +-0 everywhere (flag 2; wave-uniform)
     auto zero_of = [&](int s) { return s < 256 && ((zb[s >> 6] >> (s & 63)) & 1); };
-    // quantised K/V: such a tile's mask DMA is not issued at all (the counted
-    // waits below leave its group out); f16: it goes through an offset past the
-    // descriptor (no traffic, the instruction count unchanged).  Every DMA
-    // instruction occupies the CU's memory pipeline, whose issue stalls are a
-    // cost of their own
-#ifdef FATTN_PF_ZERO_DMA
-    constexpr bool kSkipZero = false;  // diagnostic build only (A/B)
+    // such a tile's mask DMA goes through an offset past the descriptor (no
+    // traffic, the instruction count unchanged).  (FATTN_PF_ZERO_SKIP, A/B
+    // builds, quantised K/V: not issued at all, the counted waits leaving its
+    // group out -- Q8_0 zero mask 446-455 vs 430-453 us, causal 251 vs 245:
+    // slower, profiles/r04_j)
+#ifdef FATTN_PF_ZERO_SKIP
+    constexpr bool kSkipZero = !C::kDirect;  // diagnostic build only
 #else
-    constexpr bool kSkipZero = !C::kDirect;
+    constexpr bool kSkipZero = false;
 #endif
     auto mask_groups = [&](int s) { return (HM && !(kSkipZero && zero_of(s))) ? 1 : 0; };
     auto mask_issue = [&](int s) {
