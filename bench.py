@@ -292,6 +292,12 @@ def parse_args(argv=None):
                     help="N > 1: head = BASELINE config 5 as one problem head-sharded over the ranks, one gather "
                          "per step (strong scaling, the value line); batch = every rank decodes its own config-3 "
                          "sequence (weak scaling)")
+    ap.add_argument("--dist", action="store_true",
+                    help="N = 1: run the multi-rank path anyway, on a world-size-1 RCCL group (init_process_group "
+                         "'nccl', the per-step all_gather, its graph capture) -- the one-GPU rehearsal of the "
+                         "driver's N-GPU runs")
+    ap.add_argument("--eager-gather", action="store_true",
+                    help="process group: time only the eager (kernel, gather) loop, no graph capture")
     ap.add_argument("--no-side-line", action="store_true",
                     help="N > 1: skip the other mode's measurement reported beside the value line")
     ap.add_argument("--rotate", type=int, default=0,
@@ -313,6 +319,11 @@ def parse_args(argv=None):
     ap.add_argument("--bd", type=int, default=0, help="batched-decode kernel: 0 auto, 1 never, 2 all-waves form, 3 role form (fattn.h FATTN_OPT_BD)")
     ap.add_argument("--bd-xcd", type=int, default=0,
                     help="batched decode workgroup order: 0 auto, 1 plain, 2 XCD-grouped (fattn.h FATTN_OPT_BD_XCD)")
+    ap.add_argument("--split-xcd", type=int, default=0,
+                    help="split kernel workgroup order: 0 auto, 1 plain, 2 XCD-grouped (fattn.h FATTN_OPT_SPLIT_XCD)")
+    ap.add_argument("--split-spec", type=int, default=0,
+                    help="split kernel one-row merge: 0 auto, 1 drain + count + load, 2 speculative granules "
+                         "(fattn.h FATTN_OPT_SPLIT_SPEC)")
     ap.add_argument("--merge-in-kernel", type=int, default=0,
                     help="multi-row chunk merge: 0 second launch, 1 in-kernel when the grid is co-resident")
     ap.add_argument("--split-prio", type=int, default=0,
@@ -345,6 +356,7 @@ def apply_options(args):
     import fattn
     opts = [(args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT), (args.pf, fattn.OPT_PF),
             (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO), (args.bd, fattn.OPT_BD), (args.bd_xcd, fattn.OPT_BD_XCD),
+            (args.split_xcd, fattn.OPT_SPLIT_XCD), (args.split_spec, fattn.OPT_SPLIT_SPEC),
             (args.waves, fattn.OPT_SPLIT_WAVES)]
     fattn.set_option(fattn.OPT_SPLIT_SKIP, 1 if args.no_step_skip else 0)
     fattn.set_option(fattn.OPT_SPLIT_MERGE, 1 if args.fused_merge else 0)
@@ -373,27 +385,41 @@ def shape_of(args, workload):
 REHEARSE = os.environ.get("FATTN_BENCH_REHEARSE") == "1"
 
 
-def _gather(x, mode="head"):
+def _gather(x, mode="head", buf=None, out=None):
     """head: the ranks' head slices -> the full [.., H, D] output (gather_heads);
-    batch: the ranks' own sequences stacked on a leading [world] axis."""
+    batch: the ranks' own sequences stacked on a leading [world] axis.
+    `buf` / `out`: preallocated gather and result buffers (the form a captured
+    HIP graph replays); fresh tensors when None."""
     import torch
     import torch.distributed as dist
     from fattn.shard import gather_heads
-    y = x.cpu() if REHEARSE else x
+    world = dist.get_world_size()
+    if REHEARSE:  # gloo: staged through host memory
+        y = x.cpu()
+        if mode == "head":
+            res = gather_heads(y)
+        else:
+            res = torch.empty((world,) + tuple(y.shape), dtype=y.dtype)
+            dist.all_gather_into_tensor(res.view(world * y.shape[0], *y.shape[1:]), y.contiguous())
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res.to(x.device)
     if mode == "head":
-        out = gather_heads(y)
-    else:
-        world = dist.get_world_size()
-        out = torch.empty((world,) + tuple(y.shape), dtype=y.dtype, device=y.device)
-        dist.all_gather_into_tensor(out.view(world * y.shape[0], *y.shape[1:]), y.contiguous())
-    return out.to(x.device) if REHEARSE else out
+        return gather_heads(x, buf=buf, out=out)
+    if out is None:
+        out = torch.empty((world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out.view(world * x.shape[0], *x.shape[1:]), x.contiguous())
+    return out
 
 
-def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
+def run_decode(args, dev, shape, rank=0, world=1, mode="head", dist_on=False):
     """Time K steps of the decode workload `shape` (one FLASH_ATTN_EXT per step)
     over `world` ranks: mode "head" shards its heads (strong scaling, every rank
     a slice of one global problem), mode "batch" gives every rank a whole
     problem of its own -- its own sequence of the batch (weak scaling).
+    `dist_on`: a process group exists (world > 1, or --dist at world 1): every
+    timed step gathers its output over it.
     Returns the measurement dict (rank 0 holds the max over ranks)."""
     import torch
     import torch.distributed as dist
@@ -493,7 +519,7 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
         graph.replay()   # untimed warm replay
     torch.cuda.synchronize()
     last = (K - 1) % R  # the output buffer of the last timed step
-    if world > 1:
+    if dist_on:
         _gather(outs[last], mode)  # warm the communicator
         dist.barrier()
     torch.cuda.synchronize()
@@ -509,40 +535,91 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
     hip.hipEventElapsedTime(C.byref(f), ev0, ev1)
     kern_ms_avg = f.value / K
     kernel_only_elapsed = elapsed
-    if world > 1:
-        # 3) the timed job at world > 1: every step is one FLASH_ATTN_EXT on the
-        #    rank's slice followed by the RCCL gather over xGMI of THAT step's
-        #    output (head: + the permute into [1][NQ][H][D]; batch: stacked
-        #    [world][1][NQ][H][D]) -- a decode layer cannot start its next
-        #    step before the gathered output exists.  K gathers are timed.
+    res = {}
+    if dist_on:
+        # 3) the timed job with a process group: every step is one
+        #    FLASH_ATTN_EXT on the rank's slice followed by the RCCL gather over
+        #    xGMI of THAT step's output (head: + the permute into [1][NQ][H][D];
+        #    batch: stacked [world][1][NQ][H][D]) -- a decode layer cannot start
+        #    its next step before the gathered output exists.  K gathers are
+        #    timed.  Two forms: the K (kernel, all_gather, permute) triples
+        #    captured in ONE HIP graph and replayed (RCCL collectives capture
+        #    into the graph like kernels; the value line), and the same triples
+        #    launched eagerly from Python (beside it, and the value line if the
+        #    capture raises -- in the same process).
+        if mode == "head":
+            gbuf = torch.empty((world,) + tuple(outs[0].shape), dtype=torch.float32, device=dev)
+            full = torch.empty((1, NQ, H, D), dtype=torch.float32, device=dev)
+        else:
+            gbuf = None
+            full = torch.empty((world, 1, NQ, H, D), dtype=torch.float32, device=dev)
+
+        def gstep(i, stream=None):
+            step(i, stream)
+            _gather(outs[i % R], mode, gbuf, full)
+
+        ggraph, graph_err = None, None
+        if REHEARSE or args.eager_gather:
+            graph_err = "not attempted (" + ("gloo rehearsal" if REHEARSE else "--eager-gather") + ")"
+        else:
+            try:
+                ggraph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ggraph, stream=gs):
+                    for i in range(K):
+                        gstep(i)
+                with torch.cuda.stream(gs):
+                    ggraph.replay()  # untimed warm replay
+                torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001 -- any capture failure: time the eager form instead
+                graph_err = f"{type(e).__name__}: {e}"[:400]
+                ggraph = None
+                torch.cuda.synchronize()
+        # eager form
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         with torch.cuda.stream(gs):
             for i in range(K):
-                step(i, gs.cuda_stream)
-                full = _gather(outs[i % R], mode)
+                gstep(i, gs.cuda_stream)
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
+        eager_elapsed = time.perf_counter() - t0
+        elapsed, graph_dev_ms = eager_elapsed, float("nan")
+        if ggraph is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            hip.hipEventRecord(ev0, gs.cuda_stream)
+            with torch.cuda.stream(gs):
+                ggraph.replay()
+            hip.hipEventRecord(ev1, gs.cuda_stream)
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+            elapsed = time.perf_counter() - t0
+            hip.hipEventSynchronize(ev1)
+            hip.hipEventElapsedTime(C.byref(f), ev0, ev1)
+            graph_dev_ms = f.value / K
+        res.update(eager_elapsed=eager_elapsed, graph_dev_ms=graph_dev_ms, graph_err=graph_err,
+                   timing="graph" if ggraph is not None else "eager")
 
-    res = {"kernel": kname, "kernel_ms_avg": kern_ms_avg, "kernel_ms_median": kern_ms_median, "elapsed": elapsed,
-           "kernel_only_elapsed": kernel_only_elapsed}
+    res.update({"kernel": kname, "kernel_ms_avg": kern_ms_avg, "kernel_ms_median": kern_ms_median,
+                "elapsed": elapsed, "kernel_only_elapsed": kernel_only_elapsed})
     if args.dump_out and (rank == 0 or mode == "batch"):
         # the last step's inputs (rotation `last`) and the (gathered) output,
         # for the multi-rank parity test (tests/test_rehearsal.py checks them
         # against the oracle); batch mode: every rank its own inputs
         # (<dump>.rank<r>.npz), rank 0 the gathered outputs of all ranks
         if mode == "head":
-            out0 = (full if world > 1 else outs[last]).cpu().numpy()
+            out0 = (full if dist_on else outs[last]).cpu().numpy()
         else:
-            out0 = (full if world > 1 else outs[last][None]).cpu().numpy()
+            out0 = (full if dist_on else outs[last][None]).cpu().numpy()
         path = args.dump_out if rank == 0 else args.dump_out + f".rank{rank}.npz"
         np.savez(path, q=q.cpu().numpy(), k=kv_sets[last][0].cpu().numpy(), v=kv_sets[last][1].cpu().numpy(),
                  mask=masks[last].cpu().view(torch.int16).numpy().view(np.uint16), out=out0,
                  shape=np.array([D, NQ, H, Hkv, N, typ, world]), kernel=np.array(kname), mode=np.array(mode))
-    if world > 1:
+    if dist_on:
         assert tuple(full.shape) == ((1, NQ, H, D) if mode == "head" else (world, 1, NQ, H, D))
         # 3) per-step cost of the gather, and kernel + gather per step (eager),
         #    reported apart from the kernel (BASELINE.md multi-GPU rule)
@@ -565,12 +642,11 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head"):
             ets.append(time.perf_counter() - t)
         res["gather_ms_median"] = statistics.median(gts[5:]) * 1e3
         res["step_with_gather_ms_median"] = statistics.median(ets[5:]) * 1e3
-        t = torch.tensor([elapsed, kern_ms_avg, kern_ms_median, res["gather_ms_median"],
-                          res["step_with_gather_ms_median"], kernel_only_elapsed], dtype=torch.float64,
-                         device="cpu" if REHEARSE else dev)
+        keys = ("elapsed", "kernel_ms_avg", "kernel_ms_median", "gather_ms_median", "step_with_gather_ms_median",
+                "kernel_only_elapsed", "eager_elapsed", "graph_dev_ms")
+        t = torch.tensor([res[k] for k in keys], dtype=torch.float64, device="cpu" if REHEARSE else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        (res["elapsed"], res["kernel_ms_avg"], res["kernel_ms_median"], res["gather_ms_median"],
-         res["step_with_gather_ms_median"], res["kernel_only_elapsed"]) = (float(x) for x in t.tolist())
+        res.update(zip(keys, (float(x) for x in t.tolist())))
     for e in evs:
         hip.hipEventDestroy(e)
 
@@ -624,8 +700,18 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     if "WORLD_SIZE" in os.environ and args.gpus not in (1, world):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dist and "WORLD_SIZE" not in os.environ:
+        # --dist without a launcher: a world-size-1 group of our own (nothing
+        # here has touched the GPU yet)
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # a process group exists: every rank of N > 1, or --dist at N = 1 (the RCCL
+    # path executed on a one-GPU box: init, the per-step all_gather, capture)
+    multi = world > 1 or args.dist
 
     import torch
     import torch.distributed as dist
@@ -636,12 +722,12 @@ def main():
         local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    if multi:
         if REHEARSE:
             dist.init_process_group("gloo", init_method="env://")
         else:
             dist.init_process_group("nccl", init_method="env://", device_id=dev)
-    if args.prefill_only and world == 1:
+    if args.prefill_only and not multi:
         # (profiling passes: the prefill launches alone)
         hip, evs = hip_events(2)
         r = prefill_measure(dev, hip, evs, args.prefill_kv, args.prefill_mask)
@@ -652,22 +738,22 @@ def main():
                           "roofline": {**r["roofline"], "kernel": r["kernel"]}, "source_hash": source_hash()}),
               flush=True)
         return
-    mode = args.multi if world > 1 else "head"
-    workload = args.workload if args.workload != "auto" else ("config5" if mode == "head" and world > 1 else "config3")
+    mode = args.multi if multi else "head"
+    workload = args.workload if args.workload != "auto" else ("config5" if mode == "head" and multi else "config3")
     shape = shape_of(args, workload)
-    res = run_decode(args, dev, shape, rank, world, mode)
+    res = run_decode(args, dev, shape, rank, world, mode, multi)
     side = None
-    if world > 1 and not args.no_side_line:
+    if multi and not args.no_side_line:
         # the other multi-GPU reading beside the value line: head mode (the line)
         # -> the weak-scaling batch of config-3 sequences; batch -> the config-5 head shard
         other = "batch" if mode == "head" else "head"
         wl = "config3" if other == "batch" else "config5"
         side = run_decode(args, dev, shape_of(argparse.Namespace(**{k: None for k in WORKLOADS[wl]}), wl),
-                          rank, world, other)
+                          rank, world, other, multi)
 
     if rank == 0:
-        traffic = committed_traffic(res["workload"], res["kernel"]) if world == 1 else None
-        peaks = None if args.no_copy_peak or world > 1 else measured_hbm_peaks()
+        traffic = committed_traffic(res["workload"], res["kernel"]) if not multi else None
+        peaks = None if args.no_copy_peak or multi else measured_hbm_peaks()
         sh = res["shard"]
         K = args.steps
         value = res["job_bytes"] * K / res["elapsed"] / 1e9
@@ -687,7 +773,7 @@ def main():
             "config": {"workload": res["workload"], "heads": shape["heads"], "kv_heads": shape["kv_heads"],
                        "head_dim": shape["head_dim"], "kv_len": shape["kv_len"], "n_q": shape["n_q"],
                        "kv_type": shape["kv_type"], "kv_layout": args.layout, "kv_rotation": res["R"],
-                       "parallelism": ("single_gpu" if world == 1 else
+                       "parallelism": ("single_gpu" if not multi else
                                        f"batch_shard_1seq_per_rank_x{world}" if mode == "batch" else
                                        f"head_shard_{sh.n_heads}heads_per_rank_x{world}"),
                        "bytes_per_step": res["job_bytes"], "flops_per_step": res["flops"]},
@@ -699,15 +785,29 @@ def main():
             "roofline": roofline(res, args, traffic, peaks),
             "source_hash": source_hash(),
         }
-        if world > 1:
+        if multi:
             if REHEARSE:
                 line["rehearsal"] = "FATTN_BENCH_REHEARSE: all ranks on one GPU, gloo, not a measurement"
+            if world == 1:
+                line["world1"] = ("--dist: the multi-rank path on a world-size-1 RCCL group (one GPU): "
+                                  "init_process_group('nccl'), one all_gather per step, graph capture")
             line["per_rank"] = {"heads": sh.n_heads, "kv_heads": sh.n_kv, "bytes": res["rank_bytes"],
                                 "sequences": 1 if mode == "batch" else f"1/{world} of the heads"}
             line["gather"] = {"collective": "all_gather_into_tensor (RCCL over xGMI) of every step's output"
                                             + (" + permute into the ggml dst layout" if mode == "head" else "")
-                                            + ", K gathers inside the timed region (eager: kernel, gather, ...)",
+                                            + ", K gathers inside the timed region",
                               "gathers_timed": K,
+                              "timing": res["timing"],
+                              "timing_note": ("graph: the K (kernel, all_gather, permute) triples captured in one HIP "
+                                              "graph, replayed, wall clock between barriers, max over ranks"
+                                              if res["timing"] == "graph" else
+                                              "eager: kernel, gather, permute launched from Python per step"),
+                              "graph_capture_error": res["graph_err"],
+                              "device_ms_per_step": (round(res["graph_dev_ms"], 5)
+                                                     if res["graph_dev_ms"] == res["graph_dev_ms"] else None),
+                              "wall_ms_per_step": round(res["elapsed"] / K * 1e3, 5),
+                              "eager_value": round(res["job_bytes"] * K / res["eager_elapsed"] / 1e9, 2),
+                              "eager_ms_per_step": round(res["eager_elapsed"] / K * 1e3, 5),
                               "per_step_gather_ms_median": round(res["gather_ms_median"], 4),
                               "per_step_kernel_plus_gather_ms_median": round(res["step_with_gather_ms_median"], 4)}
             # kernel-only scaling ("near-linear" applies to the kernel
@@ -725,7 +825,7 @@ def main():
                     "parallelism": (f"batch_shard_1seq_per_rank_x{world}" if side["mode"] == "batch" else
                                     f"head_shard_{shs.n_heads}heads_per_rank_x{world}"),
                     "value": round(side["job_bytes"] * K / side["elapsed"] / 1e9, 2), "unit": "GB/s",
-                    "ms_per_step": round(side["elapsed"] / K * 1e3, 5),
+                    "ms_per_step": round(side["elapsed"] / K * 1e3, 5), "timing": side["timing"],
                     "kernel_only_value": round(side["job_bytes"] * K / side["kernel_only_elapsed"] / 1e9, 2),
                     "kernel_ms_avg": round(side["kernel_ms_avg"], 5), "kernel": side["kernel"],
                     "per_step_gather_ms_median": round(side["gather_ms_median"], 4),
@@ -734,10 +834,10 @@ def main():
                              "the ranks' outputs per step; weak-scaling efficiency = value / (N * the N=1 value)"
                              if side["mode"] == "batch" else
                              "one config-5 problem (n_q 64) sliced by kv heads over the ranks, one gather per step")}
-        if world > 1:
+        if multi:
             print(json.dumps(line), flush=True)
 
-    if world == 1:
+    if not multi:
         if not args.no_scale_ref and workload == "config3":
             # the strong-scaling reference: config 5 (the multi-GPU workload) on this one GPU
             r5 = run_decode(args, dev, shape_of(argparse.Namespace(**{k: None for k in WORKLOADS["config5"]}),
@@ -760,7 +860,7 @@ def main():
             if "prefill" in line:
                 line["prefill"]["cpu_baseline"] = cpu_baseline_prefill()
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 

@@ -61,6 +61,8 @@ std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and compute
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
+std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto (off), 1 off, 2 on
+std::atomic<int> g_opt_split_spec{0};       // split kernel one-row merge: 0 auto (off), 1 off, 2 speculative granules
 std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
 std::atomic<uint32_t> g_epoch{0};
@@ -228,7 +230,17 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     a.merge_launch = (a.n_chunks >= 4 && a.wave_merge == 0 && !g_opt_split_fused_merge)
                          ? ((resident && g_opt_merge_in_kernel) ? 2 : 1) : 0;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
-    if (a.n_chunks > 1 && a.wave_merge) {
+    // XCD-grouped order (tile_coords): a tile's chunk workgroups on one XCD
+    a.xcd_group = g_opt_split_xcd == 2 && (a.n_chunks * Y * S) % 8 == 0 ? 1 : 0;
+    // speculative granule merge of one-row tiles (spec_row_merge; D = 64 / 128 / 256)
+    a.spec_merge = g_opt_split_spec == 2 && a.wave_merge == 2 && a.n_chunks > 1 && 64 % (pl.D / 4) == 0 ? 1 : 0;
+    if (a.n_chunks > 1 && a.spec_merge) {
+        // [arrival counters][granules: per tile [chunk][D + 2] x 8 B]
+        const size_t parts = (size_t)S * Y * a.n_chunks;
+        pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
+        pl.ml_bytes = 0;
+        pl.ws_bytes = pl.cnt_bytes + parts * (size_t)(pl.D + 2) * 8;
+    } else if (a.n_chunks > 1 && a.wave_merge) {
         // [arrival counters][(m, l) per part][row-0 O per part]; parts = waves
         // (wave_merge 1) or workgroups (2)
         const size_t parts = (size_t)S * Y * a.n_chunks * (a.wave_merge == 1 ? nwv : 1);
@@ -281,6 +293,10 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     // at most 64 chunks: one (m, l) pair per lane); FATTN_OPT_SPLIT_MERGE = 1:
     // in the tile's last-arriving workgroup (at most 16 chunks per 16-row subtile)
     const bool fused = g_opt_split_fused_merge != 0;
+    // the merge launch's grid.y is Y x the 16-row subtiles per tile: where that
+    // would pass the 65535 grid limit the KV sequence is not split (so many
+    // tiles fill the chip without it; a requested kv_chunk is a hint)
+    if (!fused && Y * (pl.nw == 8 ? 16 : 4) > 65535) tpc = tiles;
     for (;;) {
         nch = (tiles + tpc - 1) / tpc;
         if (nch == 1 || (fused ? combine_ok(nch, kRows, pl.D) : nch <= kWaveMergeParts)) break;
@@ -289,9 +305,6 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     a.chunk_len = (int)(tpc * kStep);
     a.n_chunks = (int)nch;
     a.merge_launch = (nch > 1 && !fused) ? 1 : 0;
-    // the merge launch's grid.y is Y x the 16-row subtiles per tile: refuse a
-    // plan whose merge could not launch (nothing is launched on an error)
-    if (a.merge_launch && Y * (pl.nw == 8 ? 16 : 4) > 65535) return FATTN_ERR_INVALID_ARG;
     a.ncp = 1;
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     a.nbuf = 0;
@@ -316,11 +329,23 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
 int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     SplitArgs& a = pl.a;
     const int64_t tiles = (N + kBdKeys - 1) / kBdKeys;
+    const bool q8 = pl.kt == FATTN_TYPE_Q8_0;
+    pl.lds = pl.bdp && pl.D == 64 ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 64>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 64>::ldsBytes)
+             : pl.bdp && pl.D == 96 ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 96>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 96>::ldsBytes)
+             : pl.bdp             ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes)
+             : pl.kt == FATTN_TYPE_Q8_0 ? BdCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
+             : pl.kt == FATTN_TYPE_Q4_0 ? BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes
+             : pl.D == 64               ? BdCfg<FATTN_TYPE_F16, 64>::ldsBytes
+             : pl.D == 96               ? BdCfg<FATTN_TYPE_F16, 96>::ldsBytes
+                                        : BdCfg<FATTN_TYPE_F16, 128>::ldsBytes;
+    // workgroups per CU by LDS (the f16 D = 64 form fits two): the KV split
+    // fills every resident slot, not one per CU
+    const int64_t per_cu = std::max<int64_t>(1, kLdsPerCU / pl.lds);
     int64_t nch;
     if (kv_chunk > 0) {
         nch = (N + kv_chunk - 1) / kv_chunk;
     } else {
-        nch = (pl.cus + Y * S - 1) / (Y * S);
+        nch = (pl.cus * per_cu + Y * S - 1) / (Y * S);
     }
     nch = std::max<int64_t>(1, std::min<int64_t>(nch, tiles));
     int64_t tpc = (tiles + nch - 1) / nch;
@@ -335,15 +360,6 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     a.nbuf = 0;
     a.wave_bytes = 0;
-    const bool q8 = pl.kt == FATTN_TYPE_Q8_0;
-    pl.lds = pl.bdp && pl.D == 64 ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 64>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 64>::ldsBytes)
-             : pl.bdp && pl.D == 96 ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 96>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 96>::ldsBytes)
-             : pl.bdp             ? (q8 ? BdpCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes : BdpCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes)
-             : pl.kt == FATTN_TYPE_Q8_0 ? BdCfg<FATTN_TYPE_Q8_0, 128>::ldsBytes
-             : pl.kt == FATTN_TYPE_Q4_0 ? BdCfg<FATTN_TYPE_Q4_0, 128>::ldsBytes
-             : pl.D == 64               ? BdCfg<FATTN_TYPE_F16, 64>::ldsBytes
-             : pl.D == 96               ? BdCfg<FATTN_TYPE_F16, 96>::ldsBytes
-                                        : BdCfg<FATTN_TYPE_F16, 128>::ldsBytes;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     // XCD-grouped workgroup order (bd_tile_coords): whole tiles per XCD, so a
     // tile's Q rows come from HBM once (config 5: 49.7 vs 53.4 MB per launch,
@@ -352,7 +368,6 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     // the chunk partials merge inside the launch (bd_tile_merge: the tile's
     // workgroups wait for each other, so only when the whole grid is
     // co-resident -- one workgroup per CU by LDS) or in a second launch
-    const int64_t per_cu = std::max<int64_t>(1, kLdsPerCU / pl.lds);
     const bool resident = nch * Y * S <= (int64_t)pl.cus * per_cu;
     a.merge_launch = nch == 1 ? 0 : (resident && g_opt_merge_in_kernel) ? 2 : 1;
     if (nch > 1) {
@@ -510,7 +525,10 @@ int make_plan(const fattn_params* p, Plan& pl) {
     // (f16 K/V rows, not transposed V: the same kernel, images filled by DMA)
     pl.pf = false;
     // (D = 80: f16 only, its images padded to 96 dims)
-    if ((quant_ok || f16_ok) && g_opt_pf != 1 && (D == 64 || D == 96 || D == 128 || (D == 80 && f16_ok)) &&
+    // (D = 80's padding dims are DMA'd from 0x80000000 past the row offset,
+    // outside the descriptor only while the spans stay within 2 GiB: fattn_pf.h)
+    const bool d80_ok = f16_ok && k_span <= (int64_t)0x80000000 && v_span <= (int64_t)0x80000000;
+    if ((quant_ok || f16_ok) && g_opt_pf != 1 && (D == 64 || D == 96 || D == 128 || (D == 80 && d80_ok)) &&
         p->kv_chunk <= 0 &&
         N % kPfKeys == 0 &&
         p->scale > 0.0f && (g_opt_pf == 2 || Hkv * S * ((NQ * a.rk2 + kPfRows - 1) / kPfRows) >= pl.cus)) {
@@ -666,6 +684,14 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_bd_xcd = value;
             return FATTN_OK;
+        case FATTN_OPT_SPLIT_XCD:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_xcd = value;
+            return FATTN_OK;
+        case FATTN_OPT_SPLIT_SPEC:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_spec = value;
+            return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:
             if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
             g_opt_split_nbuf = value;
@@ -733,8 +759,9 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,
                       pl.a.merge_launch ? " + fattn_mq_merge_kernel" : "");
     else
-        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>%s", tn(pl.kt), tn(pl.vt),
-                      pl.D, pl.gran, hm, pl.nwv,
+        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>%s%s%s", tn(pl.kt), tn(pl.vt),
+                      pl.D, pl.gran, hm, pl.nwv, pl.a.xcd_group ? " (xcd order)" : "",
+                      pl.a.spec_merge ? " (spec merge)" : "",
                       pl.a.merge_launch == 1 ? " + fattn_merge_kernel" : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     const int n = std::snprintf(out, cap, "%s grid(%u,%u,%u) lds %d chunk %d steps/slots %d ws %zu", kern, pl.grid.x,
                                 pl.grid.y, pl.grid.z, pl.lds, pl.a.chunk_len, pl.a.nbuf, pl.ws_bytes);

@@ -354,28 +354,6 @@ __device__ __forceinline__ void bd_finish(const SplitArgs& a, uint8_t* smem, con
 #endif
 }
 
-// workgroup -> (KV chunk, tile y, sequence iq3).  Blocks are dealt round-robin
-// over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch: observed placement,
-// used for speed only), so in the plain order the chunks of one kv head sit on
-// 8 different L2s and each fetches the head's Q rows (32 KB f32) from HBM.  The
-// XCD-grouped order (a.xcd_group) gives each XCD whole tiles -- all their
-// chunks: Q comes from HBM once per tile.  Any bijection is correct; the
-// planner sets xcd_group only for grids of a multiple of 8 workgroups.
-__device__ __forceinline__ void bd_tile_coords(const SplitArgs& a, int& chunk, int& y, int& iq3) {
-    chunk = blockIdx.x;
-    y = blockIdx.y;
-    iq3 = blockIdx.z;
-    if (a.xcd_group) {
-        const uint32_t gx = gridDim.x, gy = gridDim.y;
-        const uint32_t G = gx * gy * gridDim.z;
-        const uint32_t L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-        const uint32_t L2 = (L % 8) * (G / 8) + L / 8;
-        chunk = (int)(L2 % gx);
-        y = (int)((L2 / gx) % gy);
-        iq3 = (int)(L2 / (gx * gy));
-    }
-}
-
 template <int KT, int D, bool HM>
 __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const SplitArgs a) {
     using C = BdCfg<KT, D>;
@@ -397,7 +375,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
 
     // ---- tile decode: y -> (kv head, 64-row query tile); R = rk2
     int chunk, y, iq3;
-    bd_tile_coords(a, chunk, y, iq3);
+    tile_coords(a, chunk, y, iq3);
     // in-kernel merge: stamp the tile's arrival word with this launch's epoch
     // (no return; it is older than every counted DMA wait below, which it
     // therefore only joins)

@@ -226,7 +226,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
 
     // ---- tile decode (fattn_bd.h)
     int chunk, y, iq3;
-    bd_tile_coords(a, chunk, y, iq3);
+    tile_coords(a, chunk, y, iq3);
     if (a.merge_launch == 2 && tid == 0) arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
     int qt = 0, ik2 = y, ik3 = iq3;
     if (a.n_qt != 1) {

@@ -81,13 +81,24 @@ def assemble_heads(parts):
     return x.reshape(*lead, S, NQ, world * Hl, D)
 
 
-def gather_heads(local, group=None):
+def gather_heads(local, group=None, buf=None, out=None):
     """local: this rank's output [..., S, n_q, H/world, D] (contiguous).  Returns
     the full [..., S, n_q, H, D] on every rank via ONE all_gather_into_tensor
-    (RCCL over xGMI on the GPU box, gloo on the CPU) and assemble_heads."""
+    (RCCL over xGMI on the GPU box, gloo on the CPU) and assemble_heads.
+    `buf` ([world, *local.shape]) and `out` (the full shape), when given, are
+    used instead of fresh allocations -- the form a captured HIP graph replays
+    (the gather lands in `buf`, the permute writes `out`)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    buf = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+    if buf is None:
+        buf = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(buf.view(world * local.shape[0], *local.shape[1:]), local.contiguous(), group=group)
-    return assemble_heads(buf)
+    if out is None:
+        return assemble_heads(buf)
+    # one strided copy: out seen as [..., S, n_q, world, H/world, D]
+    *lead, S, NQ, Hl, D = buf.shape[1:]
+    nl = len(lead)
+    perm = tuple(range(1, 1 + nl)) + (1 + nl, 2 + nl, 0, 3 + nl, 4 + nl)
+    out.view(*lead, S, NQ, world, Hl, D).copy_(buf.permute(*perm))
+    return out

@@ -169,11 +169,14 @@ enum {
                                        merge one wave per (tile, row), in a second launch or in-kernel
                                        (FATTN_OPT_MERGE_IN_KERNEL) (default), 1 = the last-arriving workgroup merges
                                        the whole tile (combine_tile) */
-    FATTN_OPT_BD = 22               /* batched-decode kernels (64-row workgroups, D = 128 Q8_0 / Q4_0 / f16 K/V
-                                       and D = 64 Q8_0 / Q4_0, 16-B rows): 0 = auto (from 64 packed rows per kv
-                                       head, below the prefill shapes; Q8_0 / Q4_0 in the compute / build-role
-                                       form), 1 = never, 2 = the all-waves form whenever eligible (D = 128),
-                                       3 = the role form whenever eligible (quantised K/V) */,
+    FATTN_OPT_BD = 22               /* batched-decode kernels (64-row workgroups, 16-B rows): the compute /
+                                       build-role form fattn_bdp_kernel for Q8_0 / Q4_0 K/V at D = 64, 96, 128;
+                                       the all-waves form fattn_bd_kernel for Q8_0 / Q4_0 at D = 128 (value 2
+                                       only) and for f16 K/V at D = 64, 96, 128 (always: f16 has no role form).
+                                       0 = auto (from 64 packed rows per kv head, below the prefill shapes),
+                                       1 = never, 2 = the all-waves form whenever eligible (quantised D = 64 / 96:
+                                       the multi-query kernel instead), 3 = the role form whenever eligible --
+                                       on f16 K/V 3 runs the all-waves form */,
     /* 23: a removed experiment (one-row partials as data-tagged granules), rejected */
     FATTN_OPT_MERGE_IN_KERNEL = 24  /* chunk partials of multi-row tiles (split kernel with 4+ chunks, batched-
                                        decode kernel): 0 = merged in a second launch (default); 1 = inside the
@@ -186,7 +189,13 @@ enum {
     FATTN_OPT_BD_XCD = 25           /* batched-decode kernels: workgroup order. 0 = auto (XCD-grouped), 1 = plain
                                        (chunk fastest), 2 = XCD-grouped: each of the 8 XCDs takes whole (kv head x
                                        row tile)s, so a tile's Q rows come from HBM once, not once per chunk
-                                       (needs a grid of a multiple of 8 workgroups; otherwise plain) */
+                                       (needs a grid of a multiple of 8 workgroups; otherwise plain) */,
+    FATTN_OPT_SPLIT_XCD = 26        /* split kernel: workgroup order. 0 = auto (plain), 1 = plain, 2 = XCD-grouped:
+                                       a tile's chunk workgroups on one XCD (grid a multiple of 8 workgroups) */,
+    FATTN_OPT_SPLIT_SPEC = 27       /* split kernel, one-row tiles merged across chunks (wg_row_merge): 0 = auto
+                                       (drain + count + load), 1 = the same, 2 = speculative: chunk rows published
+                                       as tagged 8-B granules and swept before the arrival count returns (one
+                                       round trip fewer; the last arriver re-reads stale granules) */
 };
 int fattn_set_option(int option, int value);
 

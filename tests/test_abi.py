@@ -209,10 +209,29 @@ def test_mq_min_rows_explicit_default_lifts_the_wide_gate():
 
 def test_mq_merge_launch_grid_limit():
     """A forced small KV chunk with many 64-row query tiles: the merge launch's
-    grid.y (tiles x 4 subtiles) would pass 65535 -- refused at planning."""
+    grid.y (tiles x 4 subtiles) would pass 65535, so the plan does not split
+    the KV sequence (one chunk, no merge launch, no workspace) instead of
+    refusing; below the limit the requested chunk stands."""
     p = _params(NQ=64 * 20000, H=1, Hkv=1, N=1024, kv_chunk=256)
     with fattn.options({fattn.OPT_PF: 1, fattn.OPT_BD: 1}):
+        d = fattn.describe(p)
+        assert d.startswith("fattn_mq_kernel") and "merge" not in d, d
+        assert "grid(1,5000,1)" in d, d  # (256-row tiles: 5000 x 16 subtiles)
         assert fattn.workspace_size(p) == 0
+        small = _params(NQ=64 * 100, H=1, Hkv=1, N=1024, kv_chunk=256)
+        d2 = fattn.describe(small)
+        assert "fattn_mq_merge_kernel" in d2 and "grid(4,100,1)" in d2, d2
+
+
+def test_pf_d80_needs_spans_within_2gib():
+    """D = 80 prefill reads its padding dims from 2 GiB past the row offset:
+    a cache whose head span passes 2 GiB takes the multi-query / split path."""
+    ok = _params(D=80, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16)
+    assert "fattn_pf_kernel<f16,D80" in fattn.describe(ok)
+    big = _params(D=80, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16)
+    nb1 = (1 << 19) + 256  # rows 512.25 KiB apart: the span passes 2 GiB
+    big.k = fattn.View(1 << 20, fattn.TYPE_F16, (80, 4096, 32, 1), (2, nb1, 160, nb1 * 4096)).c()
+    assert "fattn_pf_kernel" not in fattn.describe(big), fattn.describe(big)
 
 
 def test_single_chunk_needs_no_workspace():

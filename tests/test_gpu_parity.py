@@ -82,6 +82,34 @@ def test_config3_q8_0(dev, layout):
     assert attn_elem_err(got, ref) <= 1.0
 
 
+@pytest.mark.parametrize("case", [
+    dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", layout="pos"),            # config 3, llama.cpp rows
+    dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", mask="tail"),             # whole chunks -inf
+    dict(D=128, NQ=1, H=32, N=2048, kv_type="f16"),                           # config 2's f16
+    dict(D=64, NQ=1, H=16, N=16384, kv_type="q4_0"),                          # D = 64, 16+ chunks
+    dict(D=256, NQ=1, H=8, N=8192, kv_type="q8_0"),                           # D = 256
+], ids=["cfg3_pos", "cfg3_tail", "f16", "d64_q4", "d256"])
+@pytest.mark.parametrize("xcd", [0, 2], ids=["plain", "xcd"])
+def test_row_merge_spec_and_xcd_bit_identical(dev, case, xcd):
+    """One-row tiles: the speculative granule merge (FATTN_OPT_SPLIT_SPEC = 2)
+    and the XCD-grouped workgroup order (FATTN_OPT_SPLIT_XCD = 2) give the
+    oracle's answer and the default form's bits (fixed merge order, the last
+    arriver's own row taken from registers in its slot)."""
+    p = make_problem(seed=33, **case)
+    ref = p.oracle()
+    base = run_gpu(p)
+    with fattn.options({fattn.OPT_SPLIT_SPEC: 2, fattn.OPT_SPLIT_XCD: xcd}):
+        t = upload(p)
+        att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+        assert "(spec merge)" in att.describe(), att.describe()
+        for _ in range(3):
+            t["dst"].fill_(float("nan"))
+            att()
+            got = t["dst"].cpu().numpy()
+            assert np.array_equal(got, base, equal_nan=True)
+    assert attn_rel_err(got, ref) <= RTOL
+
+
 def test_config4_q4_0_gqa(dev):
     p = make_problem(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0", seed=40)
     got, ref = run_gpu(p), p.oracle()
@@ -795,9 +823,9 @@ def test_pf_f16_prefill_full(dev):
 
 def test_pf_prefill_full_matches_mq(dev):
     """The prefill shape at full size (n_q = N = 4096, 32 heads, Q8_0, random mask):
-    the prefill kernel (auto-selected) against the multi-query kernel, and two
-    heads x three query-row blocks (start, middle, end of the sequence)
-    against the oracle."""
+    the prefill kernel (auto-selected) against the multi-query kernel, and all
+    32 heads x three query-row blocks of 128 rows (start, middle, end of the
+    sequence) against the oracle."""
     p = make_problem(D=128, NQ=4096, H=32, N=4096, kv_type="q8_0", seed=29)
     a = run_gpu(p)
     fattn.set_option(fattn.OPT_PF, 1)

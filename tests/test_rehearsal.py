@@ -85,3 +85,59 @@ def test_bench_rehearsal_two_ranks_matches_oracle(tmp_path):
     ref = _oracle_of(d)
     got = d["out"].reshape(ref.shape)
     assert attn_rel_err(got, ref) <= 1e-3
+
+
+def _world1_nccl(tmp_path, mode, extra=()):
+    """bench.py --dist under torch.distributed.run with one rank: a real RCCL
+    group (init_process_group("nccl", device_id=...)), the per-step
+    all_gather_into_tensor on device tensors and its HIP-graph capture -- the
+    calls the driver's N-GPU runs make, executed on the one-GPU box."""
+    import socket
+    out = tmp_path / "rank0.npz"
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("FATTN_BENCH_REHEARSE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py", "--dist", "--steps", "6",
+           "--warmup", "2", "--rotate", "3", "--no-side-line", "--multi", mode, "--dump-out", str(out), *extra]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    print(lines[0])
+    return json.loads(lines[0]), out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("eager", [False, True])
+def test_bench_nccl_world1_head_matches_oracle(tmp_path, eager):
+    line, out = _world1_nccl(tmp_path, "head", ["--eager-gather"] if eager else [])
+    assert "rehearsal" not in line and line["n_gpus"] == 1 and "world1" in line
+    assert line["config"]["parallelism"] == "head_shard_32heads_per_rank_x1"
+    assert line["config"]["bytes_per_step"] == 38273024
+    g = line["gather"]
+    assert g["gathers_timed"] == line["steps"]
+    if eager:
+        assert g["timing"] == "eager" and g["device_ms_per_step"] is None
+    else:
+        # RCCL's all_gather captures into the HIP graph; the line reports the
+        # device-side per-step time next to the wall time
+        assert g["timing"] == "graph", g["graph_capture_error"]
+        assert 0 < g["device_ms_per_step"] <= g["wall_ms_per_step"] * 1.05
+    d = np.load(out)
+    D, NQ, H, Hkv, N, typ, world = (int(x) for x in d["shape"])
+    assert world == 1 and (D, NQ, H, Hkv, N, typ) == (128, 64, 32, 32, 4096, orc.TYPE_Q8_0)
+    ref = _oracle_of(d)
+    assert attn_rel_err(d["out"].reshape(ref.shape), ref) <= 1e-3
+
+
+@pytest.mark.gpu
+def test_bench_nccl_world1_batch_matches_oracle(tmp_path):
+    line, out = _world1_nccl(tmp_path, "batch")
+    assert line["scaling"] == "weak" and line["gather"]["timing"] == "graph"
+    d = np.load(out)
+    got = d["out"]  # [world=1][1][NQ][H][D]
+    ref = _oracle_of(d)
+    assert attn_rel_err(got[0].reshape(ref.shape), ref) <= 1e-3

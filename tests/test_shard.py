@@ -80,6 +80,11 @@ def _worker(rank, world, port, kv_type, q):
         sh = shard_heads(prob.H, prob.Hkv, world, rank)
         local = torch.from_numpy(_slice_problem(prob, sh).oracle(n_threads=2))
         full = gather_heads(local)
+        # the preallocated form bench.py captures into a HIP graph: same bytes
+        buf = torch.full((world,) + tuple(local.shape), float("nan"), dtype=local.dtype)
+        out = torch.full(tuple(full.shape), float("nan"), dtype=local.dtype)
+        assert gather_heads(local, buf=buf, out=out) is out
+        assert torch.equal(out, full)
         if rank == 0:
             q.put(full.numpy())
     finally:
