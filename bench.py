@@ -321,6 +321,9 @@ def parse_args(argv=None):
                     help="batched decode workgroup order: 0 auto, 1 plain, 2 XCD-grouped (fattn.h FATTN_OPT_BD_XCD)")
     ap.add_argument("--split-xcd", type=int, default=0,
                     help="split kernel workgroup order: 0 auto, 1 plain, 2 XCD-grouped (fattn.h FATTN_OPT_SPLIT_XCD)")
+    ap.add_argument("--pf-stage", type=int, default=0,
+                    help="prefill over Q8_0 / Q4_0: 0 auto (staged to f16), 1 in-kernel dequantisation, 2 staged "
+                         "(fattn.h FATTN_OPT_PF_STAGE)")
     ap.add_argument("--split-spec", type=int, default=0,
                     help="split kernel one-row merge: 0 auto, 1 drain + count + load, 2 speculative granules "
                          "(fattn.h FATTN_OPT_SPLIT_SPEC)")
@@ -357,6 +360,7 @@ def apply_options(args):
     opts = [(args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT), (args.pf, fattn.OPT_PF),
             (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO), (args.bd, fattn.OPT_BD), (args.bd_xcd, fattn.OPT_BD_XCD),
             (args.split_xcd, fattn.OPT_SPLIT_XCD), (args.split_spec, fattn.OPT_SPLIT_SPEC),
+            (args.pf_stage, fattn.OPT_PF_STAGE),
             (args.waves, fattn.OPT_SPLIT_WAVES)]
     fattn.set_option(fattn.OPT_SPLIT_SKIP, 1 if args.no_step_skip else 0)
     fattn.set_option(fattn.OPT_SPLIT_MERGE, 1 if args.fused_merge else 0)
@@ -853,7 +857,13 @@ def main():
             line["prefill"] = prefill_measure(dev, hip, evs, args.prefill_kv, args.prefill_mask)
             if args.prefill_mask != "random":
                 r = prefill_measure(dev, hip, evs, args.prefill_kv, "random")
-                line["prefill_random_mask"] = {k: r[k] for k in ("workload", "kernel_ms_avg", "roofline")}
+                line["prefill_random_mask"] = {k: r[k] for k in ("workload", "kernel", "kernel_ms_avg", "roofline")}
+            if args.prefill_kv != "f16" and not args.pf_stage:
+                # beside it: the same prefill with the K/V dequantised inside the
+                # kernel, tile by tile (FATTN_OPT_PF_STAGE = 1; the round-4 form)
+                with fattn.options({fattn.OPT_PF_STAGE: 1}):
+                    r = prefill_measure(dev, hip, evs, args.prefill_kv, args.prefill_mask)
+                line["prefill_inkernel_dequant"] = {k: r[k] for k in ("workload", "kernel", "kernel_ms_avg", "roofline")}
         if not args.no_cpu_baseline and shape["n_q"] == 1:  # kernel_test.h's CPU path is one query row
             threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads)

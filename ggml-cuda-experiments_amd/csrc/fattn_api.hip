@@ -62,6 +62,7 @@ std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge 
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
 std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto (off), 1 off, 2 on
+std::atomic<int> g_opt_pf_stage{0};         // prefill over Q8_0 / Q4_0: 0 auto (staged to f16), 1 in-kernel dequantisation, 2 staged
 std::atomic<int> g_opt_split_spec{0};       // split kernel one-row merge: 0 auto (off), 1 off, 2 speculative granules
 std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
@@ -571,6 +572,25 @@ int make_plan(const fattn_params* p, Plan& pl) {
         a.n_chunks = 1;
         a.ncp = 1;
         pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
+        // Q8_0 / Q4_0: staged to f16 rows in the workspace, then the f16 kernel
+        // (each K/V tile is otherwise dequantised once per 256-row query tile)
+        pl.pf_stage = is_quant(pl.kt) && g_opt_pf_stage != 1;
+        if (pl.pf_stage) {
+            pl.stage_kt = pl.kt;
+            pl.kt = pl.vt = FATTN_TYPE_F16;
+            pl.stage_k = (const uint8_t*)k.data;
+            pl.stage_v = (const uint8_t*)v.data;
+            pl.stage_k_nb2 = k.nb[2]; pl.stage_k_nb3 = k.nb[3];
+            pl.stage_v_nb2 = v.nb[2]; pl.stage_v_nb3 = v.nb[3];
+            pl.stage_hkv = (int)Hkv;
+            pl.stage_skv = (int)Skv;
+            pl.stage_bytes = (size_t)Skv * Hkv * N * D * 2;
+            // the staged rows: [Skv][Hkv][N][D] f16, contiguous
+            a.k_nb1 = a.v_nb1 = D * 2;
+            a.k_nb2 = a.v_nb2 = N * D * 2;
+            a.k_nb3 = a.v_nb3 = Hkv * N * D * 2;
+            a.k_span = a.v_span = (uint32_t)(N * D * 2);
+        }
         auto pf_lds = [&](auto d) {
             constexpr int DD = decltype(d)::value;
             return pl.kt == FATTN_TYPE_F16    ? PfCfg<FATTN_TYPE_F16, DD>::ldsBytes
@@ -589,6 +609,10 @@ int make_plan(const fattn_params* p, Plan& pl) {
         pl.pf_flags = has_mask && !g_opt_pf_no_skip;
         if (pl.pf_flags) pl.cnt_bytes = ((size_t)a.n_qt * (N / kPfKeys) + 255) / 256 * 256;
         pl.ws_bytes = pl.cnt_bytes;
+        if (pl.pf_stage) {
+            pl.stage_off = pl.cnt_bytes;
+            pl.ws_bytes = pl.stage_off + 2 * pl.stage_bytes;
+        }
         return FATTN_OK;
     }
     pl.nwv = 4;
@@ -688,6 +712,10 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_split_xcd = value;
             return FATTN_OK;
+        case FATTN_OPT_PF_STAGE:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_pf_stage = value;
+            return FATTN_OK;
         case FATTN_OPT_SPLIT_SPEC:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_split_spec = value;
@@ -749,8 +777,10 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
     char kern[160];
     const char* hm = pl.a.has_mask ? "mask" : "nomask";
     if (pl.pf)
-        std::snprintf(kern, sizeof kern, "%sfattn_pf_kernel<%s,D%d,%s>", pl.pf_flags ? "pf_mask_flags_kernel + " : "",
-                      tn(pl.kt), pl.D, hm);
+        std::snprintf(kern, sizeof kern, "%s%sfattn_pf_kernel<%s,D%d,%s>",
+                      pl.pf_stage ? (pl.stage_kt == FATTN_TYPE_Q8_0 ? "kv_stage_f16<q8_0> + " : "kv_stage_f16<q4_0> + ")
+                                  : "",
+                      pl.pf_flags ? "pf_mask_flags_kernel + " : "", tn(pl.kt), pl.D, hm);
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,
                       hm, pl.a.xcd_group ? " (xcd order)" : "",
@@ -784,6 +814,10 @@ int fattn_ext_events(const fattn_params* p, void* stream, void* ev_begin, void* 
         pl.a.ws_ml = (float*)(w + pl.cnt_bytes);
         pl.a.ws_o = (float*)(w + pl.cnt_bytes + pl.ml_bytes);  // (prefill pre-pass: the f16 rows)
         if (pl.pf && pl.pf_flags) pl.a.pf_flags = w;
+        if (pl.pf_stage) {
+            pl.a.k = w + pl.stage_off;
+            pl.a.v = w + pl.stage_off + pl.stage_bytes;
+        }
     }
     hipStream_t st = (hipStream_t)stream;
     Events ev;

@@ -35,7 +35,15 @@ struct Plan {
     bool pf;  // prefill kernel (fattn_pf.h)
     bool bd;  // batched-decode kernel (fattn_bd.h)
     bool bdp; // ... in its compute / build-role form (fattn_bdp.h; Q8_0 / Q4_0)
-    bool pf_flags;          // masked prefill: live-block flags pre-pass (tile-range skipping)
+    bool pf_flags = false;  // masked prefill: live-block flags pre-pass (tile-range skipping)
+    // prefill over Q8_0 / Q4_0: the rows staged to f16 in the workspace first
+    // (kv_stage_f16_kernel), then the f16 prefill kernel (kt = vt = F16 then)
+    bool pf_stage = false;
+    int stage_kt = 0;                                  // the cache's type
+    const uint8_t *stage_k = nullptr, *stage_v = nullptr;  // the cache's K / V
+    int64_t stage_k_nb2 = 0, stage_k_nb3 = 0, stage_v_nb2 = 0, stage_v_nb3 = 0;
+    int stage_hkv = 0, stage_skv = 0;
+    size_t stage_off = 0, stage_bytes = 0;             // per K (or V): Skv * Hkv * N * D * 2
     int nw;   // mq kernel: waves per workgroup: 4 (16 rows each) or 8 (32 rows each)
 };
 
@@ -171,6 +179,18 @@ template <int KT, int D, bool HM>
 int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     auto kern = fattn_pf_kernel<KT, D, HM>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
+        if constexpr (KT == FATTN_TYPE_F16 && D % QK == 0) {
+            if (pl.pf_stage) {  // the quantised cache's rows -> f16 rows in the workspace
+                const int64_t nblk = (int64_t)pl.a.N * D / QK;
+                const dim3 g((unsigned)((4 * nblk + 255) / 256), (unsigned)pl.stage_hkv, (unsigned)pl.stage_skv);
+                auto sk = pl.stage_kt == FATTN_TYPE_Q8_0 ? kv_stage_f16_kernel<FATTN_TYPE_Q8_0>
+                                                         : kv_stage_f16_kernel<FATTN_TYPE_Q4_0>;
+                hipLaunchKernelGGL(sk, g, dim3(256), 0, st, pl.stage_k, pl.stage_k_nb2, pl.stage_k_nb3,
+                                   (uint16_t*)pl.a.k, nblk);
+                hipLaunchKernelGGL(sk, g, dim3(256), 0, st, pl.stage_v, pl.stage_v_nb2, pl.stage_v_nb3,
+                                   (uint16_t*)pl.a.v, nblk);
+            }
+        }
         if (HM && pl.a.pf_flags)
             hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,
                                pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);

@@ -162,4 +162,44 @@ __global__ __launch_bounds__(256) void cpy_f32_kernel(const CpyArgs a, int64_t u
     }
 }
 
+// Prefill K/V staging (the prefill planner's default for Q8_0 / Q4_0 caches):
+// the quantised rows of every (sequence, kv head) -- contiguous blocks, head
+// base at ik3 * nb3 + ik2 * nb2 -- become f16 rows [Skv][Hkv][N][D] in the
+// caller's workspace, h(q * d) with one f16 rounding: the value the in-kernel
+// dequantisation of every other kernel produces (src/utils.h:10-11), so the
+// f16 prefill kernel over the staged rows computes the same attention.  The
+// prefill re-reads each K/V tile once per 256-row query tile (16 times at
+// n_q = 4096); staging converts it once (35.7 MB read, 67 MB written at the
+// prefill shape) instead of 16 times in the MFMA loop.  Thread = 8 values of
+// one block (16 B of f16 written); grid (blocks * 4 / 256, Hkv, Skv).
+template <int KT>
+__global__ __launch_bounds__(256) void kv_stage_f16_kernel(const uint8_t* __restrict__ src, int64_t nb2, int64_t nb3,
+                                                           uint16_t* __restrict__ dst, int64_t nblk) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= 4 * nblk) return;
+    const int64_t b = t >> 2;
+    const int j = (int)(t & 3);
+    constexpr int BB = KT == FATTN_TYPE_Q8_0 ? kQ8Bytes : kQ4Bytes;
+    const uint8_t* blk = src + (int64_t)blockIdx.z * nb3 + (int64_t)blockIdx.y * nb2 + b * BB;
+    const float d = (float)__builtin_bit_cast(f16, *(const uint16_t*)blk);  // (blocks are 2-byte aligned)
+    const uint16_t* qw = (const uint16_t*)(blk + 2 + (KT == FATTN_TYPE_Q8_0 ? 8 * j : 8 * (j & 1)));
+    uint32_t by[8];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const uint32_t w = qw[e];
+        by[2 * e] = w & 0xFF;
+        by[2 * e + 1] = w >> 8;
+    }
+    f16x8 h;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        float q;
+        if constexpr (KT == FATTN_TYPE_Q8_0) q = (float)(int8_t)by[e];
+        else q = (float)((int)(j < 2 ? by[e] & 0x0F : by[e] >> 4) - 8);  // elements 0-15 low nibbles, 16-31 high
+        h[e] = (f16)(q * d);  // exact product (<= 19 significant bits), one rounding to f16
+    }
+    uint16_t* y = dst + (((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * nblk + b) * QK + 8 * j;
+    *(f16x8*)y = h;
+}
+
 }  // namespace fattn

@@ -195,7 +195,11 @@ enum {
     FATTN_OPT_SPLIT_SPEC = 27       /* split kernel, one-row tiles merged across chunks (wg_row_merge): 0 = auto
                                        (drain + count + load), 1 = the same, 2 = speculative: chunk rows published
                                        as tagged 8-B granules and swept before the arrival count returns (one
-                                       round trip fewer; the last arriver re-reads stale granules) */
+                                       round trip fewer; the last arriver re-reads stale granules) */,
+    FATTN_OPT_PF_STAGE = 28         /* prefill kernel over Q8_0 / Q4_0 K/V: 0 = auto (staged), 1 = dequantised in
+                                       the kernel, tile by tile, once per 256-row query tile; 2 = staged: the rows
+                                       converted once to f16 in the workspace (kv_stage_f16, + 2 * Skv * Hkv * N *
+                                       D * 2 bytes of fattn_workspace_size), then the f16 prefill kernel */
 };
 int fattn_set_option(int option, int value);
 

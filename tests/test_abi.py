@@ -78,8 +78,8 @@ def test_workspace_size_config3():
     (dict(NQ=64, H=24, Hkv=4), ["fattn_bdp_kernel<q8_0", "grid(8,28,1)"]),                  # GQA 6: 7 tiles of 10 queries
     (dict(NQ=64, H=4, Hkv=4, kt=fattn.TYPE_F16), ["fattn_split_kernel<f16,f16"]),           # f16, 8-rank shard
     (dict(NQ=8, H=32, Hkv=8), ["fattn_split_kernel", "+ fattn_merge_kernel"]),              # < 64 rows per kv head
-    (dict(D=64, NQ=4096, H=32, Hkv=32), ["fattn_pf_kernel<q8_0,D64"]),                       # D = 64 prefill
-    (dict(D=96, NQ=4096, H=32, Hkv=32), ["fattn_pf_kernel<q8_0,D96"]),                       # D = 96 prefill
+    (dict(D=64, NQ=4096, H=32, Hkv=32), ["kv_stage_f16<q8_0> +", "fattn_pf_kernel<f16,D64"]),  # D = 64 prefill (staged)
+    (dict(D=96, NQ=4096, H=32, Hkv=32), ["kv_stage_f16<q8_0> +", "fattn_pf_kernel<f16,D96"]),  # D = 96 prefill
     (dict(D=96, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16), ["fattn_pf_kernel<f16,D96"]),
     (dict(D=80, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16), ["fattn_pf_kernel<f16,D80"]),      # D = 80 prefill (f16)
     (dict(D=256, NQ=4096, H=16, Hkv=16), ["fattn_mq_kernel<q8_0,D256,4waves"]),              # D = 256 prefill
@@ -205,6 +205,26 @@ def test_mq_min_rows_explicit_default_lifts_the_wide_gate():
         d = fattn.describe(p)
     assert d.startswith("fattn_mq_kernel"), d
     assert fattn.describe(p).startswith("fattn_split_kernel")  # restored
+
+
+def test_pf_stage_option_and_workspace():
+    """Prefill over Q8_0 / Q4_0: staged to f16 rows in the workspace by default
+    (2 x Hkv x N x D x 2 bytes more), dequantised in the kernel with
+    FATTN_OPT_PF_STAGE = 1; f16 caches are never staged."""
+    p = _params(NQ=4096)
+    d = fattn.describe(p)
+    assert d.startswith("kv_stage_f16<q8_0> + pf_mask_flags_kernel + fattn_pf_kernel<f16,D128"), d
+    ws = fattn.workspace_size(p)
+    with fattn.options({fattn.OPT_PF_STAGE: 1}):
+        d1 = fattn.describe(p)
+        ws1 = fattn.workspace_size(p)
+    assert d1.startswith("pf_mask_flags_kernel + fattn_pf_kernel<q8_0,D128"), d1
+    assert ws == ws1 + 2 * 32 * 4096 * 128 * 2
+    with fattn.options({fattn.OPT_PF_STAGE: 2}):
+        assert fattn.describe(_params(NQ=4096, kt=fattn.TYPE_Q4_0)).startswith("kv_stage_f16<q4_0>")
+        assert "kv_stage" not in fattn.describe(_params(NQ=4096, kt=fattn.TYPE_F16))
+    with pytest.raises(Exception):
+        fattn.set_option(fattn.OPT_PF_STAGE, 3)
 
 
 def test_mq_merge_launch_grid_limit():

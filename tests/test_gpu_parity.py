@@ -631,11 +631,45 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
 @pytest.fixture
-def pf_force():
-    """The prefill kernel (fattn_pf.h, 8 waves x 32 rows) on every eligible problem."""
+@pytest.fixture(params=[0, 1], ids=["staged", "inkernel_deq"])
+def pf_force(request):
+    """The prefill kernel (fattn_pf.h, 8 waves x 32 rows) on every eligible
+    problem; Q8_0 / Q4_0 K/V staged to f16 first (the default) or dequantised
+    inside the kernel (FATTN_OPT_PF_STAGE = 1)."""
     fattn.set_option(fattn.OPT_PF, 2)
+    fattn.set_option(fattn.OPT_PF_STAGE, request.param)
     yield
     fattn.set_option(fattn.OPT_PF, 0)
+    fattn.set_option(fattn.OPT_PF_STAGE, 0)
+
+
+@pytest.mark.parametrize("case", [
+    dict(kv_type="q8_0", NQ=256, H=4, Hkv=4, N=512, mask="random"),
+    dict(kv_type="q4_0", NQ=512, H=4, Hkv=2, N=256, mask="causal"),
+    dict(kv_type="q8_0", NQ=256, H=2, Hkv=2, N=512, D=96, mask="none"),
+    dict(kv_type="q4_0", NQ=256, H=2, Hkv=2, N=256, D=64, mask="random"),
+    dict(kv_type="q8_0", NQ=256, H=2, Hkv=2, N=256, S=2, mask="random"),
+], ids=["q8", "q4_causal_gqa", "q8_d96", "q4_d64", "q8_seq2"])
+def test_pf_staged_equals_inkernel_dequant(dev, case):
+    """kv_stage_f16 writes h(q * d) -- the value the prefill kernel's own
+    dequantisation puts in its f16 images -- so the staged prefill (default)
+    and the in-kernel form give the same bits, and the oracle's answer."""
+    p = make_problem(seed=77, **case)
+    fattn.set_option(fattn.OPT_PF, 2)
+    try:
+        outs = {}
+        for st in (2, 1):
+            fattn.set_option(fattn.OPT_PF_STAGE, st)
+            t = upload(p)
+            att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+            assert ("kv_stage_f16" in att.describe()) == (st == 2), att.describe()
+            att()
+            outs[st] = t["dst"].cpu().numpy()
+    finally:
+        fattn.set_option(fattn.OPT_PF, 0)
+        fattn.set_option(fattn.OPT_PF_STAGE, 0)
+    assert np.array_equal(outs[1], outs[2], equal_nan=True)
+    assert attn_rel_err(outs[2], p.oracle()) <= RTOL
 
 
 PF_CASES = [
