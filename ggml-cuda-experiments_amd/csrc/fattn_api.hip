@@ -62,6 +62,7 @@ std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge 
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
 std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto (off), 1 off, 2 on
+std::atomic<int> g_opt_pf_form{0};          // prefill body: 0 auto, 1 the 8-wave form, 2 one wave per SIMD (fattn_pf4.h)
 std::atomic<int> g_opt_pf_stage{0};         // prefill over Q8_0 / Q4_0: 0 auto (staged to f16), 1 in-kernel dequantisation, 2 staged
 std::atomic<int> g_opt_split_spec{0};       // split kernel one-row merge: 0 auto (off), 1 off, 2 speculative granules
 std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
@@ -601,6 +602,9 @@ int make_plan(const fattn_params* p, Plan& pl) {
                  : D == 80 ? PfCfg<FATTN_TYPE_F16, 80>::ldsBytes
                  : D == 96 ? pf_lds(std::integral_constant<int, 96>())
                            : pf_lds(std::integral_constant<int, 128>());
+        // f16 rows (native or staged) at D = 128: the one-wave-per-SIMD body
+        pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && g_opt_pf_form == 2;
+        if (pl.pf4) pl.lds = Pf4Cfg<128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
         // share the front of the workspace with the split-KV arrival words; a
@@ -712,6 +716,10 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_split_xcd = value;
             return FATTN_OK;
+        case FATTN_OPT_PF_FORM:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_pf_form = value;
+            return FATTN_OK;
         case FATTN_OPT_PF_STAGE:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_stage = value;
@@ -777,10 +785,11 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
     char kern[160];
     const char* hm = pl.a.has_mask ? "mask" : "nomask";
     if (pl.pf)
-        std::snprintf(kern, sizeof kern, "%s%sfattn_pf_kernel<%s,D%d,%s>",
+        std::snprintf(kern, sizeof kern, "%s%s%s<%s,D%d,%s>",
                       pl.pf_stage ? (pl.stage_kt == FATTN_TYPE_Q8_0 ? "kv_stage_f16<q8_0> + " : "kv_stage_f16<q4_0> + ")
                                   : "",
-                      pl.pf_flags ? "pf_mask_flags_kernel + " : "", tn(pl.kt), pl.D, hm);
+                      pl.pf_flags ? "pf_mask_flags_kernel + " : "", pl.pf4 ? "fattn_pf4_kernel" : "fattn_pf_kernel",
+                      tn(pl.kt), pl.D, hm);
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,
                       hm, pl.a.xcd_group ? " (xcd order)" : "",

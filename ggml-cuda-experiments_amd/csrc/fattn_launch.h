@@ -13,6 +13,7 @@
 #include "fattn_quant.h"
 #include "fattn_mq.h"
 #include "fattn_pf.h"
+#include "fattn_pf4.h"
 #include "fattn_bd.h"
 #include "fattn_bdp.h"
 #include "fattn_split.h"
@@ -38,6 +39,7 @@ struct Plan {
     bool pf_flags = false;  // masked prefill: live-block flags pre-pass (tile-range skipping)
     // prefill over Q8_0 / Q4_0: the rows staged to f16 in the workspace first
     // (kv_stage_f16_kernel), then the f16 prefill kernel (kt = vt = F16 then)
+    bool pf4 = false;       // the prefill's one-wave-per-SIMD body (fattn_pf4.h; f16 rows, D = 128)
     bool pf_stage = false;
     int stage_kt = 0;                                  // the cache's type
     const uint8_t *stage_k = nullptr, *stage_v = nullptr;  // the cache's K / V
@@ -178,7 +180,11 @@ int launch_mq(const Plan& pl, hipStream_t st, const Events& ev) {
 template <int KT, int D, bool HM>
 int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     auto kern = fattn_pf_kernel<KT, D, HM>;
-    return launch_kernel((const void*)kern, pl, st, ev, [&] {
+    const void* main_kern = (const void*)kern;
+    if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
+        if (pl.pf4) main_kern = (const void*)fattn_pf4_kernel<D, HM>;
+    }
+    return launch_kernel(main_kern, pl, st, ev, [&] {
         if constexpr (KT == FATTN_TYPE_F16 && D % QK == 0) {
             if (pl.pf_stage) {  // the quantised cache's rows -> f16 rows in the workspace
                 const int64_t nblk = (int64_t)pl.a.N * D / QK;
@@ -194,6 +200,12 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
         if (HM && pl.a.pf_flags)
             hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,
                                pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
+        if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
+            if (pl.pf4) {
+                hipLaunchKernelGGL((fattn_pf4_kernel<D, HM>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
+                return;
+            }
+        }
         hipLaunchKernelGGL(kern, pl.grid, dim3(kPfWaves * kWave), pl.lds, st, pl.a);
     });
 }

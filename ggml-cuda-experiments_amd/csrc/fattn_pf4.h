@@ -1,0 +1,475 @@
+// fattn_pf4.h -- prefill attention, one wave per SIMD (gfx950).
+//
+// The f16 prefill body (f16 K/V rows; Q8_0 / Q4_0 caches arrive here staged
+// to f16 by kv_stage_f16_kernel).  Same math as fattn_pf_kernel (scale * q.k
+// + mask, online softmax with the deferred max, f16 operands, f32
+// accumulation; src/flash-llama.h:5-438 is the reference's form of it), laid
+// out for one wave per SIMD instead of two:
+//
+//  * one workgroup = 4 waves = 256 packed (query row x q-head) rows of one kv
+//    head, 64 per wave as two 32-row blocks (rb 0, 1); __launch_bounds__(256, 1):
+//    each wave owns its SIMD's whole 512-entry register file, so O (2 x 64
+//    f32), Q^T (2 x 32 f16x2) and a tile's K or V operands stay in registers;
+//  * K and V operands are read from LDS ONCE per wave and tile and used for
+//    both row blocks (the 8-wave form reads them once per 32 rows: twice the
+//    LDS traffic, which bounded it);
+//  * per 64-key tile j, three phases, the vector work of one row block under
+//    the matrix work of the other (cdna_hip_programming.md 'Fused attention
+//    prefill', 4-wave structure):
+//      A_j: S1 = K_j . Q1^T (16 MFMA)       || softmax of rb 0 (scores, max, exp)
+//      B_j: O0 += V_j^T . P0^T (16 MFMA)    || softmax of rb 1
+//      C_j: O1 += V_j^T . P1^T, S0 = K_{j+1} . Q0^T (32 MFMA) || operand reads, DMA issue
+//    with S0 of tile j computed in C_{j-1}; one workgroup barrier per tile (at
+//    the start of C_j);
+//  * HBM -> LDS by LDS-DMA straight into the f16 images (the swizzles of
+//    fattn_pf.h, 16-B granular, so each lane's source offset carries them):
+//    K and V rings of 3 tiles, per-wave mask rings of 2: at C_j, K j+3 (two
+//    tiles of latency), V j+2 and mask j+2 (one tile) into the slots their
+//    tiles j, j-1 and j freed; K and V operands are re-read from LDS per
+//    phase (256 B/clk: LDS has the bandwidth, the register file not the room).
+//
+// LDS (D = 128): K ring 3 x 16 KiB, V ring 3 x 16 KiB, mask [4 waves][2][64
+// rows][128 B] = 64 KiB: 160 KiB.  The epilogue parks each wave's 64
+// normalised rows there ([256 rows][D + 4] f32) and stores whole rows.
+#pragma once
+
+#include "fattn_pf.h"
+
+namespace fattn {
+
+constexpr int kPf4Waves = 4;
+constexpr int kPf4RowsW = 64;  // packed rows per wave (two 32-row blocks)
+
+template <int D>
+struct Pf4Cfg {
+    static_assert(D == 128, "the one-wave-per-SIMD prefill body is D = 128 (other head dims: fattn_pf_kernel)");
+    static constexpr int img = kPfKeys * D * 2;            // one f16 image (16 KiB)
+    static constexpr int KS = 3, VS = 3, MS = 2;           // ring depths
+    static constexpr int kOff = 0;
+    static constexpr int vOff = KS * img;
+    static constexpr int maskSlot = kPf4RowsW * kPfKeys * 2;  // 8 KiB: 64 rows x 64 keys f16
+    static constexpr int mOff = vOff + VS * img;
+    static constexpr int loopBytes = mOff + kPf4Waves * MS * maskSlot;
+    static constexpr int parkBytes = kPf4Waves * kPf4RowsW * (D + 4) * 4;
+    static constexpr int ldsBytes = loopBytes > parkBytes ? loopBytes : parkBytes;
+    static constexpr int NJ = img / 1024;                  // 1-KiB DMA pieces per image (16)
+    static constexpr int NKI = NJ / kPf4Waves;             // K (and V) DMA instructions per wave and tile (4)
+    static constexpr int NMI = maskSlot / 1024;            // mask DMA instructions per wave and tile (8)
+    static_assert(ldsBytes <= 163840, "");
+};
+
+// one v_add_f32: hipcc's SLP vectoriser would pair adjacent f32 adds into
+// v_pk_add_f32, which costs more than two scalar adds between MFMAs
+// (MI355X_MICROARCH.md, per-instruction constants)
+__device__ __forceinline__ float add_f32(float x, float y) {
+    float r;
+    asm("v_add_f32_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
+template <int D, bool HM>
+__global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const SplitArgs a) {
+    using C = Pf4Cfg<D>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NK = D / 16;   // 16-dim k-steps of S^T = K.Q^T
+    constexpr int NDB = D / 32;  // 32-dim blocks of O^T
+    constexpr float kNegInf = -__builtin_inff();
+    constexpr float kDeferLog2 = 8.0f;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5;    // k-group of the MFMA operands
+    const int c32 = lane & 31;  // MFMA column: this lane's row within a 32-row block
+
+    // ---- tile decode (as fattn_pf_kernel): y -> (kv head, query tile)
+    const int y = blockIdx.y;
+    const int iq3 = blockIdx.z;
+    int qt = 0, ik2 = y, ik3 = iq3;
+    if (a.pf_flags) {  // masked: longest-first dispatch (the last query tile of every head first)
+        const int nh = gridDim.y / a.n_qt;
+        qt = a.n_qt - 1 - y / nh;
+        ik2 = y % nh;
+    } else if (a.n_qt != 1) {
+        qt = y % a.n_qt;
+        ik2 = y / a.n_qt;
+    }
+    if (a.rk3 != 1) ik3 = iq3 / a.rk3;
+    auto row_of = [&](int p, int& iq1, int& iq2) {  // packed row -> (query row, q head)
+        const int mq = div_R(a, p);
+        iq1 = qt * a.QPT + mq;
+        iq2 = ik2 * a.rk2 + (p - mq * a.R);
+        return mq < a.QPT && iq1 < a.NQ;
+    };
+    // live KV tile range [t0, t0 + nt) and the +-0 mask blocks (flags 2), from
+    // pf_mask_flags_kernel (fattn_pf.h)
+    int t0 = 0, nt = a.N / kPfKeys;
+    uint64_t zb[4] = {0, 0, 0, 0};
+    if (a.pf_flags) {
+        const uint8_t* fl = a.pf_flags + (int64_t)qt * nt;
+        int lo = nt, hi = -1;
+        for (int b = 0; b < nt; b += kWave) {  // wave-uniform
+            const bool f = b + lane < nt && fl[b + lane] != 0;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(f);
+            if (m) {
+                lo = min(lo, b + (int)__builtin_ctzll(m));
+                hi = b + 63 - (int)__builtin_clzll(m);
+            }
+        }
+        t0 = lo;
+        const int all = nt;
+        nt = hi >= lo ? hi - lo + 1 : 0;
+        const uint8_t* fz = a.pf_flags + (int64_t)qt * all + t0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) zb[w] = __builtin_amdgcn_ballot_w64(64 * w + lane < nt && fz[64 * w + lane] == 2);
+    }
+    auto zero_of = [&](int s) { return s < 256 && ((zb[s >> 6] >> (s & 63)) & 1); };
+
+    StepSrc rs;
+    rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
+    rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
+    rs.m = make_srd(a.mask, HM ? a.m_span : 0);
+    const uint32_t lds0 = lds_addr(smem);
+
+    // ---- Q^T operands of both row blocks, rounded to f16 (src/utils.h:10)
+    f16x8 qop[2][NK];
+    {
+        const auto qs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.q + (int64_t)iq3 * a.q_nb3), 0,
+                                                          a.q_span, 0x00020000);
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++) {
+            int q1, q2;
+            const bool ok = row_of(kPf4RowsW * wave + 32 * rb + c32, q1, q2);
+            const uint32_t qoff = ok ? (uint32_t)q1 * (uint32_t)a.q_nb1 + (uint32_t)q2 * (uint32_t)a.q_nb2 + 32 * h
+                                     : a.q_span;
+#pragma unroll
+            for (int kk = 0; kk < NK; kk++) {
+                const f32x4 x0 =
+                    __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qoff + 64 * kk, 0, 0));
+                const f32x4 x1 =
+                    __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qoff + 64 * kk + 16, 0, 0));
+                f16x8 hq;
+                hq.s0 = (f16)x0.x; hq.s1 = (f16)x0.y; hq.s2 = (f16)x0.z; hq.s3 = (f16)x0.w;
+                hq.s4 = (f16)x1.x; hq.s5 = (f16)x1.y; hq.s6 = (f16)x1.z; hq.s7 = (f16)x1.w;
+                qop[rb][kk] = hq;
+            }
+        }
+    }
+
+    // ---- DMA source offsets (tile-relative; + n0 * nb1 per tile): piece
+    // j = wave + 4i of the K image and of the V image, laid out as the image
+    // swizzles of fattn_pf.h (K [8 slices][64 keys][32 B], 16-B halves swapped
+    // on rows with bit 3 set; V [4 dim blocks][64 keys][64 B], chunk c of row r
+    // at c ^ ((r >> 2) & 3))
+    // piece j = wave + 4i of an image: the K pieces of one wave share their
+    // rows (32 (wave & 1) + lane / 2) and step 2 slices (64 B) per i; the V
+    // pieces share their rows (16 wave + lane / 4) and step one dim block (64
+    // B) per i -- one offset per image and lane, the rest immediates
+    static_assert(kPf4Waves == 4 && C::NKI == 4, "");
+    uint32_t koff0, voff0;
+    {
+        const int r = 32 * (wave & 1) + (lane >> 1), hh = lane & 1;
+        koff0 = (uint32_t)r * (uint32_t)a.k_nb1 + (wave >> 1) * 32 + (hh ^ ((r >> 3) & 1)) * 16;
+    }
+    {
+        const int r = 16 * wave + (lane >> 2), pc = lane & 3;
+        voff0 = (uint32_t)r * (uint32_t)a.v_nb1 + (pc ^ ((r >> 2) & 3)) * 16;
+    }
+    // mask: instruction k fills rows 8k .. 8k+7 of the wave's 64 (row pr:
+    // 16-B piece pc stored at pc ^ ((pr >> 1) & 7)); rows past the mask fall
+    // outside its descriptor (zeros, no traffic)
+    uint32_t moff[C::NMI];
+    if constexpr (HM) {
+#pragma unroll
+        for (int k = 0; k < C::NMI; k++) {
+            const int rr = 8 * k + (lane >> 3);
+            int q1, q2;
+            const bool ok = row_of(kPf4RowsW * wave + rr, q1, q2);
+            const int pc = (lane & 7) ^ ((rr >> 1) & 7);
+            moff[k] = ok ? (uint32_t)q1 * (uint32_t)a.m_nb1 + 16 * pc : a.m_span;
+        }
+    }
+    auto k_issue = [&](int s) {  // tile s (relative to t0) into K slot s % KS
+        const uint32_t nk = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.k_nb1;
+        const uint32_t dst = lds0 + C::kOff + (s % C::KS) * C::img;
+#pragma unroll
+        for (int i = 0; i < C::NKI; i++) dma<16>(rs.k, dst + (wave + kPf4Waves * i) * 1024, nk + koff0 + 64 * i);
+    };
+    auto v_issue = [&](int s) {
+        const uint32_t nv = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.v_nb1;
+        const uint32_t dst = lds0 + C::vOff + (s % C::VS) * C::img;
+#pragma unroll
+        for (int i = 0; i < C::NKI; i++) dma<16>(rs.v, dst + (wave + kPf4Waves * i) * 1024, nv + voff0 + 64 * i);
+    };
+    auto m_issue = [&](int s) {  // (a +-0 block: through an offset past the descriptor -- no traffic, same count)
+        if constexpr (HM) {
+            const uint32_t n2 = (uint32_t)(t0 + s) * kPfKeys * 2;
+            const bool zero = zero_of(s);
+            const uint32_t dst = lds0 + C::mOff + (wave * C::MS + s % C::MS) * C::maskSlot;
+#pragma unroll
+            for (int k = 0; k < C::NMI; k++)
+                dma<16>(rs.m, dst + k * 1024, (moff[k] == a.m_span || zero) ? a.m_span : moff[k] + n2);
+        }
+    };
+
+    // per-lane LDS read offsets within an image: K slice kk, row 32t + c32,
+    // half h; V^T gather (ds_read_b64_tr_b16) as fattn_pf.h
+    const uint32_t kbase = c32 * 32 + ((h ^ ((c32 >> 3) & 1)) * 16);
+    const int gi = lane & 15, dh = (lane >> 4) & 1;
+    uint32_t vbase[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int row = 8 * e + 4 * h + (gi >> 2);
+        const int ch = (2 * dh + ((gi & 3) >> 1)) ^ ((h + 2 * e) & 3);
+        vbase[e] = row * 64 + ch * 16 + (gi & 1) * 8;
+    }
+    // mask read offsets: row c32 of the wave's slot, piece 4t + u (keys
+    // 32t + 8u .. +7), half h
+    // (row block 1: + 32 rows; (pr >> 1) & 7 is the same for both)
+    uint32_t mrd[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) mrd[t][u] = c32 * 128 + (((4 * t + u) ^ ((c32 >> 1) & 7)) * 16) + 8 * h;
+    }
+
+    // ---- prologue: mask 0, V 0, K 0, mask 1, V 1, K 1, K 2 (the steady
+    // state's issue order -- mask s+2, V s+2, K s+3 at C_s -- so that a
+    // counted wait can leave the youngest K in flight)
+    for (int s = 0; s < 2 && s < nt; s++) {
+        m_issue(s);
+        v_issue(s);
+        k_issue(s);
+    }
+    if (nt > 2) k_issue(2);
+
+    const float log2e = 1.4426950408889634f;
+    const float scale = a.scale_log2 / log2e;
+    const float cexp = HM ? log2e : a.scale_log2;  // exponent argument x * c - m (log2 domain)
+    float m_run[2] = {kNegInf, kNegInf};
+    f32x2 l2[2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
+    f32x16 o[2][NDB];
+#pragma unroll
+    for (int rb = 0; rb < 2; rb++) {
+#pragma unroll
+        for (int db = 0; db < NDB; db++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) o[rb][db][j] = 0.0f;
+        }
+    }
+    f32x16 s0[2], s1[2];  // S^T of rb 0 (computed in C_{s-1}) and rb 1 (A_s), per subtile
+
+    // S^T of row block rb over tile s: per subtile one chain of NK MFMAs (one
+    // accumulator chain runs at full rate, MI355X_MICROARCH.md constants);
+    // the K operands are read here, per phase, not held across phases (the
+    // register file holds O, Q^T and one tile's V^T operands)
+    auto qk = [&](int s, int rb, f32x16 (&st)[2]) {
+        const uint8_t* img = smem + C::kOff + (s % C::KS) * C::img;
+        f16x8 ka[2][NK];
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+#pragma unroll
+            for (int kk = 0; kk < NK; kk++) ka[t][kk] = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) st[t][j] = 0.0f;
+#pragma unroll
+            for (int kk = 0; kk < NK; kk++) st[t] = mfma32(ka[t][kk], qop[rb][kk], st[t]);
+        }
+    };
+    // mask values of row block rb for tile s (a +-0 block's slot holds the
+    // zeros its empty DMA wrote)
+    auto mask_reads = [&](int s, int rb, u32x2 (&mk)[2][4]) {
+        if constexpr (HM) {
+            const uint8_t* slot = smem + C::mOff + (wave * C::MS + s % C::MS) * C::maskSlot + rb * (32 * 128);
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) mk[t][u] = *(const u32x2*)(slot + mrd[t][u]);
+            }
+        }
+    };
+    // softmax of one row block's tile: scores u = scale * s + mask (natural
+    // units), the tile max (in-lane + one permlane32 swap), the deferred-max
+    // rescale of that block's O and l, then p = exp2(u * c - m) to f16 P^T
+    // fragments in the accumulator's own key order (element j of subtile t is
+    // key 32t + 8(j/4) + 4h + (j%4)); row sums as scalar f32 adds
+    auto softmax = [&](int rb, const f32x16 (&st)[2], const u32x2 (&mk)[2][4], f16x8 (&pb)[2][2]) {
+        float us[2][16];
+        float tmax = kNegInf;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    float x = st[t][4 * u + e];
+                    if constexpr (HM) {
+                        const f16x2 mm = as_h2(e < 2 ? mk[t][u].x : mk[t][u].y);
+                        x = fmaf(x, scale, (float)(e & 1 ? mm.y : mm.x));
+                    }
+                    us[t][4 * u + e] = x;
+                    tmax = fmaxf(tmax, x);
+                }
+            }
+        }
+        tmax = xor32_pair(tmax, true) * cexp;
+        if (__builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2)) {  // (T13; rare after the first tiles)
+            const float m_new = fmaxf(m_run[rb], tmax);
+            const float alpha = (m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
+            l2[rb] *= alpha;
+#pragma unroll
+            for (int db = 0; db < NDB; db++) o[rb][db] *= alpha;
+            m_run[rb] = m_new;
+        }
+        const float nm = (m_run[rb] == kNegInf) ? 0.0f : -m_run[rb];
+        float la = l2[rb].x, lb = l2[rb].y;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                f16x8 x;
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    const float pa = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e], cexp, nm));
+                    const float pb2 = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e + 1], cexp, nm));
+                    la = add_f32(la, pa);  // (scalar: packed f32 adds cost more beside MFMAs)
+                    lb = add_f32(lb, pb2);
+                    x[e] = (f16)pa;
+                    x[e + 1] = (f16)pb2;
+                }
+                pb[t][q] = x;
+            }
+        }
+        l2[rb] = f32x2{la, lb};
+    };
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    // O_rb^T += V_s^T . P_rb^T: per subtile t, its V^T operands (gathered by
+    // ds_read_b64_tr_b16 in the accumulator's key order) then 2 x NDB MFMAs;
+    // the V^T operands are read per phase (B for rb 0, C for rb 1), not held
+    auto pv = [&](int s, int rb, const f16x8 (&pb)[2][2]) {
+        const uint8_t* img = smem + C::vOff + (s % C::VS) * C::img;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            u32x4 va[2][NDB];
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+#pragma unroll
+                for (int db = 0; db < NDB; db++) {
+                    const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[0] + off));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[1] + off));
+                    const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                    va[q][db] = u32x4{a2.x, a2.y, b2.x, b2.y};
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+#pragma unroll
+                for (int db = 0; db < NDB; db++) o[rb][db] = mfma32(__builtin_bit_cast(f16x8, va[q][db]), pb[t][q], o[rb][db]);
+            }
+        }
+    };
+
+    // ---- S0 of tile 0 (the loop's C phase computes it for the next tile):
+    // K 0 landed (mask 0 and V 0 before it; mask 1, V 1, K 1, K 2 may fly)
+    if (nt > 0) {
+        const int later = (HM && nt > 1 ? C::NMI : 0) + (nt > 1 ? 2 * C::NKI : 0) + (nt > 2 ? C::NKI : 0);
+        static_assert(C::NMI == 2 * C::NKI, "the prologue's wait counts: 0, 8, 12, 16, 20");
+        switch (__builtin_amdgcn_readfirstlane(later)) {  // (wave-uniform)
+            case 5 * C::NKI: wait_vmcnt_c<5 * C::NKI>(); break;
+            case 4 * C::NKI: wait_vmcnt_c<4 * C::NKI>(); break;
+            case 3 * C::NKI: wait_vmcnt_c<3 * C::NKI>(); break;
+            case 2 * C::NKI: wait_vmcnt_c<2 * C::NKI>(); break;
+            default: wait_vmcnt_c<0>(); break;
+        }
+        __syncthreads();
+        qk(0, 0, s0);
+    }
+
+    for (int s = 0; s < nt; s++) {
+        // ---- A: S1 = K_s . Q1^T  ||  softmax of rb 0
+        u32x2 mk0[2][4], mk1[2][4];
+        f16x8 p0[2][2], p1[2][2];
+        mask_reads(s, 0, mk0);
+        qk(s, 1, s1);
+        softmax(0, s0, mk0, p0);
+        __builtin_amdgcn_sched_group_barrier(0x100, NK + (HM ? 8 : 0), 0);  // subtile 0's K operands, the mask
+#pragma unroll
+        for (int i = 0; i < 2 * NK; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // up to five VALU
+            if (i < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // subtile 1's K operands
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- B: O0 += V_s^T . P0^T  ||  softmax of rb 1
+        mask_reads(s, 1, mk1);
+        pv(s, 0, p0);
+        softmax(1, s1, mk1, p1);
+        // the mask and subtile 0's V^T reads, then per MFMA up to five VALU
+        // and one of subtile 1's V^T reads
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB + (HM ? 8 : 0), 0);
+#pragma unroll
+        for (int i = 0; i < 4 * NDB; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            if (i < 4 * NDB) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- C: barrier (every wave is done with tile s's K and mask and
+        // tile s-1's V; tile s+1's mask and V and K landed), refill, O1 +=
+        // V_s^T . P1^T, S0 = K_{s+1} . Q0^T
+        {
+            // issued at C_{s-1} (or in the prologue): mask s+1, V s+1, K s+2 --
+            // K s+2 may fly on
+            if (s + 2 < nt) wait_vmcnt_c<C::NKI>();
+            else wait_vmcnt_c<0>();
+        }
+        __syncthreads();
+        if (s + 2 < nt) {
+            m_issue(s + 2);
+            v_issue(s + 2);
+        }
+        if (s + 3 < nt) k_issue(s + 3);
+        pv(s, 1, p1);
+        if (s + 1 < nt) qk(s + 1, 0, s0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+    // ---- normalise, park the wave's 64 rows in LDS, store whole rows
+    // (one instruction = 1 KiB of contiguous row bytes: fattn_pf.h's epilogue)
+    constexpr int kStride = D + 4;
+    __syncthreads();  // every wave is done with the rings
+    float* park = (float*)smem + wave * (kPf4RowsW * kStride);
+#pragma unroll
+    for (int rb = 0; rb < 2; rb++) {
+        const float l_tot = xor32_pair(l2[rb].x + l2[rb].y, false);
+        const float inv = 1.0f / l_tot;  // fully masked row -> NaN like the reference
+        float* pk = park + (32 * rb + c32) * kStride + 4 * h;
+#pragma unroll
+        for (int db = 0; db < NDB; db++) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; r++) v[r] = l_tot == 0.0f ? __builtin_nanf("") : o[rb][db][4 * u + r] * inv;
+                *(f32x4*)(pk + 32 * db + 8 * u) = v;
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the wave reads back only its own rows)
+    constexpr int CPR = D / 4;  // 16-B chunks of a dst row
+#pragma unroll
+    for (int i = 0; i < kPf4RowsW * CPR / kWave; i++) {
+        const int g = kWave * i + lane;
+        const int r = g / CPR, c = g % CPR;
+        int q1, q2;
+        if (row_of(kPf4RowsW * wave + r, q1, q2)) {
+            const f32x4 v = *(const f32x4*)(park + r * kStride + 4 * c);
+            *(f32x4*)(a.dst + (((int64_t)iq3 * a.NQ + q1) * a.H + q2) * D + 4 * c) = v;
+        }
+    }
+}
+
+}  // namespace fattn

@@ -631,16 +631,53 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
 @pytest.fixture
-@pytest.fixture(params=[0, 1], ids=["staged", "inkernel_deq"])
+@pytest.fixture(params=[(0, 1), (1, 1), (0, 2)], ids=["staged", "inkernel_deq", "staged_pf4"])
 def pf_force(request):
-    """The prefill kernel (fattn_pf.h, 8 waves x 32 rows) on every eligible
-    problem; Q8_0 / Q4_0 K/V staged to f16 first (the default) or dequantised
-    inside the kernel (FATTN_OPT_PF_STAGE = 1)."""
+    """The prefill kernels on every eligible problem: Q8_0 / Q4_0 K/V staged
+    to f16 first (the default) or dequantised inside the kernel
+    (FATTN_OPT_PF_STAGE = 1); the f16 body in its 8-wave form (fattn_pf.h)
+    or one wave per SIMD (fattn_pf4.h, D = 128; FATTN_OPT_PF_FORM = 2)."""
+    stage, form = request.param
     fattn.set_option(fattn.OPT_PF, 2)
-    fattn.set_option(fattn.OPT_PF_STAGE, request.param)
+    fattn.set_option(fattn.OPT_PF_STAGE, stage)
+    fattn.set_option(fattn.OPT_PF_FORM, form)
     yield
     fattn.set_option(fattn.OPT_PF, 0)
     fattn.set_option(fattn.OPT_PF_STAGE, 0)
+    fattn.set_option(fattn.OPT_PF_FORM, 0)
+
+
+@pytest.mark.parametrize("case", [
+    dict(kv_type="f16", NQ=256, H=4, Hkv=4, N=512, mask="random"),
+    dict(kv_type="q8_0", NQ=512, H=4, Hkv=2, N=256, mask="causal"),           # staged, GQA, causal
+    dict(kv_type="q4_0", NQ=300, H=2, Hkv=2, N=384, mask="none"),             # ragged query tiles, no mask
+    dict(kv_type="f16", NQ=256, H=2, Hkv=2, N=256, S=2, mask="random", layout="pos"),  # two sequences, [N][Hkv]
+    dict(kv_type="q8_0", NQ=256, H=2, Hkv=2, N=1024, mask="random", extreme=True),     # rescales
+    dict(kv_type="f16", NQ=256, H=2, Hkv=2, N=128, mask="random"),            # two tiles (prologue paths)
+    dict(kv_type="f16", NQ=256, H=2, Hkv=2, N=64, mask="random"),             # one tile
+], ids=["f16", "q8_causal_gqa", "q4_nomask_ragged", "f16_seq2_pos", "q8_extreme", "two_tiles", "one_tile"])
+def test_pf4_bit_identical_to_pf(dev, case):
+    """The one-wave-per-SIMD prefill body (fattn_pf4_kernel) runs the 8-wave
+    body's arithmetic in the same order -- per 64-key tile the same S^T
+    chains, tile max, deferred-rescale rule, exponentials, row-sum pairing and
+    P.V accumulation order -- so its output has the same bits, and the
+    oracle's answer."""
+    p = make_problem(seed=88, **case)
+    outs = {}
+    fattn.set_option(fattn.OPT_PF, 2)
+    try:
+        for form in (1, 2):
+            fattn.set_option(fattn.OPT_PF_FORM, form)
+            t = upload(p)
+            att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+            assert ("fattn_pf4_kernel" in att.describe()) == (form == 2), att.describe()
+            att()
+            outs[form] = t["dst"].cpu().numpy()
+    finally:
+        fattn.set_option(fattn.OPT_PF, 0)
+        fattn.set_option(fattn.OPT_PF_FORM, 0)
+    assert np.array_equal(outs[1], outs[2], equal_nan=True)
+    assert attn_rel_err(outs[2], p.oracle()) <= RTOL
 
 
 @pytest.mark.parametrize("case", [
