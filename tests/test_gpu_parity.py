@@ -630,7 +630,6 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture
 @pytest.fixture(params=[(0, 1), (1, 1), (0, 2)], ids=["staged", "inkernel_deq", "staged_pf4"])
 def pf_force(request):
     """The prefill kernels on every eligible problem: Q8_0 / Q4_0 K/V staged
