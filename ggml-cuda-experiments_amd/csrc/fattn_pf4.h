@@ -129,6 +129,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
     rs.m = make_srd(a.mask, HM ? a.m_span : 0);
     const uint32_t lds0 = lds_addr(smem);
+    typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
     // ---- Q^T operands of both row blocks, rounded to f16 (src/utils.h:10)
     f16x8 qop[2][NK];
@@ -263,12 +264,14 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     // the K operands are read here, per phase, not held across phases (the
     // register file holds O, Q^T and one tile's V^T operands)
     auto qk = [&](int s, int rb, f32x16 (&st)[2]) {
-        const uint8_t* img = smem + C::kOff + (s % C::KS) * C::img;
+        uint32_t kb = (uint32_t)(C::kOff + (s % C::KS) * C::img) + kbase;
+        asm volatile("" : "+v"(kb));  // (see pv: keeps the reads' offsets immediate)
+        const lds_u8* img = (const lds_u8*)smem + kb;
         f16x8 ka[2][NK];
 #pragma unroll
         for (int t = 0; t < 2; t++) {
 #pragma unroll
-            for (int kk = 0; kk < NK; kk++) ka[t][kk] = *(const f16x8*)(img + kbase + kk * (kPfKeys * 32) + t * 1024);
+            for (int kk = 0; kk < NK; kk++) ka[t][kk] = *(const __attribute__((address_space(3))) f16x8*)(img + kk * (kPfKeys * 32) + t * 1024);
         }
 #pragma unroll
         for (int t = 0; t < 2; t++) {
@@ -282,11 +285,13 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     // zeros its empty DMA wrote)
     auto mask_reads = [&](int s, int rb, u32x2 (&mk)[2][4]) {
         if constexpr (HM) {
-            const uint8_t* slot = smem + C::mOff + (wave * C::MS + s % C::MS) * C::maskSlot + rb * (32 * 128);
+            uint32_t mb = (uint32_t)(C::mOff + (wave * C::MS + s % C::MS) * C::maskSlot + rb * (32 * 128));
+            asm volatile("" : "+s"(mb));
+            const lds_u8* slot = (const lds_u8*)smem + mb;
 #pragma unroll
             for (int t = 0; t < 2; t++) {
 #pragma unroll
-                for (int u = 0; u < 4; u++) mk[t][u] = *(const u32x2*)(slot + mrd[t][u]);
+                for (int u = 0; u < 4; u++) mk[t][u] = *(const __attribute__((address_space(3))) u32x2*)(slot + mrd[t][u]);
             }
         }
     };
@@ -295,7 +300,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     // rescale of that block's O and l, then p = exp2(u * c - m) to f16 P^T
     // fragments in the accumulator's own key order (element j of subtile t is
     // key 32t + 8(j/4) + 4h + (j%4)); row sums as scalar f32 adds
-    auto softmax = [&](int rb, const f32x16 (&st)[2], const u32x2 (&mk)[2][4], f16x8 (&pb)[2][2]) {
+    // Branch-free inside the phase (a branch would split the phase into
+    // basic blocks, and the exponentials could no longer sit between the
+    // MFMAs): the rescale decision and l's factor are selects; O's factor is
+    // applied at the next phase boundary (rescale_o), before that block's P.V.
+    auto softmax = [&](int rb, const f32x16 (&st)[2], const u32x2 (&mk)[2][4], f16x8 (&pb)[2][2], float& alpha,
+                       bool& resc) {
         float us[2][16];
         float tmax = kNegInf;
 #pragma unroll
@@ -315,16 +325,13 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             }
         }
         tmax = xor32_pair(tmax, true) * cexp;
-        if (__builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2)) {  // (T13; rare after the first tiles)
-            const float m_new = fmaxf(m_run[rb], tmax);
-            const float alpha = (m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
-            l2[rb] *= alpha;
-#pragma unroll
-            for (int db = 0; db < NDB; db++) o[rb][db] *= alpha;
-            m_run[rb] = m_new;
-        }
-        const float nm = (m_run[rb] == kNegInf) ? 0.0f : -m_run[rb];
-        float la = l2[rb].x, lb = l2[rb].y;
+        // deferred max (T13; rare after the first tiles): wave-uniform decision
+        resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
+        const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
+        alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
+        m_run[rb] = m_new;
+        const float nm = (m_new == kNegInf) ? 0.0f : -m_new;
+        float la = l2[rb].x * alpha, lb = l2[rb].y * alpha;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
 #pragma unroll
@@ -344,12 +351,31 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         }
         l2[rb] = f32x2{la, lb};
     };
+    // (the empty asm keeps hipcc from if-converting the rare branch into an
+    // unconditional multiply of O by alpha = 1: 128 VALU + AGPR moves a tile)
+    auto rescale_o = [&](int rb, bool resc, float alpha) {  // (at a phase boundary; resc: wave-uniform)
+        if (__builtin_expect(resc, 0)) {
+            asm volatile("; rescale O" ::: "memory");
+#pragma unroll
+            for (int db = 0; db < NDB; db++) o[rb][db] *= alpha;
+        }
+    };
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    // (LDS-space arithmetic: the per-read offsets fold into the instructions'
+    // immediate; through a generic pointer every read got its own v_add)
+    lds_u8* const lsm = (lds_u8*)smem;
     // O_rb^T += V_s^T . P_rb^T: per subtile t, its V^T operands (gathered by
     // ds_read_b64_tr_b16 in the accumulator's key order) then 2 x NDB MFMAs;
     // the V^T operands are read per phase (B for rb 0, C for rb 1), not held
     auto pv = [&](int s, int rb, const f16x8 (&pb)[2][2]) {
-        const uint8_t* img = smem + C::vOff + (s % C::VS) * C::img;
+        // (the per-tile base through an empty asm: otherwise hipcc hoists
+        // vbase + every read's offset out of the loop -- 32 loop-invariant
+        // addresses, spilled to AGPRs -- and no offset folds into a read)
+        uint32_t b0 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[0];
+        uint32_t b1 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[1];
+        asm volatile("" : "+v"(b0), "+v"(b1));
+        lds_u8* const img0 = lsm + b0;
+        lds_u8* const img1 = lsm + b1;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
             u32x4 va[2][NDB];
@@ -358,8 +384,8 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
 #pragma unroll
                 for (int db = 0; db < NDB; db++) {
                     const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
-                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[0] + off));
-                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + vbase[1] + off));
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img1 + off));
                     const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
                     va[q][db] = u32x4{a2.x, a2.y, b2.x, b2.y};
                 }
@@ -392,9 +418,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         // ---- A: S1 = K_s . Q1^T  ||  softmax of rb 0
         u32x2 mk0[2][4], mk1[2][4];
         f16x8 p0[2][2], p1[2][2];
+        float al0, al1;
+        bool rs0, rs1;
         mask_reads(s, 0, mk0);
         qk(s, 1, s1);
-        softmax(0, s0, mk0, p0);
+        softmax(0, s0, mk0, p0, al0, rs0);
         __builtin_amdgcn_sched_group_barrier(0x100, NK + (HM ? 8 : 0), 0);  // subtile 0's K operands, the mask
 #pragma unroll
         for (int i = 0; i < 2 * NK; i++) {
@@ -403,10 +431,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             if (i < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // subtile 1's K operands
         }
         __builtin_amdgcn_sched_barrier(0);
+        rescale_o(0, rs0, al0);
         // ---- B: O0 += V_s^T . P0^T  ||  softmax of rb 1
         mask_reads(s, 1, mk1);
         pv(s, 0, p0);
-        softmax(1, s1, mk1, p1);
+        softmax(1, s1, mk1, p1, al1, rs1);
         // the mask and subtile 0's V^T reads, then per MFMA up to five VALU
         // and one of subtile 1's V^T reads
         __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB + (HM ? 8 : 0), 0);
@@ -432,6 +461,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             v_issue(s + 2);
         }
         if (s + 3 < nt) k_issue(s + 3);
+        rescale_o(1, rs1, al1);
         pv(s, 1, p1);
         if (s + 1 < nt) qk(s + 1, 0, s0);
     }
