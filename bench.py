@@ -324,9 +324,6 @@ def parse_args(argv=None):
     ap.add_argument("--pf-stage", type=int, default=0,
                     help="prefill over Q8_0 / Q4_0: 0 auto (staged to f16), 1 in-kernel dequantisation, 2 staged "
                          "(fattn.h FATTN_OPT_PF_STAGE)")
-    ap.add_argument("--split-spec", type=int, default=0,
-                    help="split kernel one-row merge: 0 auto, 1 drain + count + load, 2 speculative granules "
-                         "(fattn.h FATTN_OPT_SPLIT_SPEC)")
     ap.add_argument("--merge-in-kernel", type=int, default=0,
                     help="multi-row chunk merge: 0 second launch, 1 in-kernel when the grid is co-resident")
     ap.add_argument("--split-prio", type=int, default=0,
@@ -359,7 +356,7 @@ def apply_options(args):
     import fattn
     opts = [(args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT), (args.pf, fattn.OPT_PF),
             (int(args.no_mq), fattn.OPT_MQ_DISABLE), (args.split_prio, fattn.OPT_SPLIT_PRIO), (args.bd, fattn.OPT_BD), (args.bd_xcd, fattn.OPT_BD_XCD),
-            (args.split_xcd, fattn.OPT_SPLIT_XCD), (args.split_spec, fattn.OPT_SPLIT_SPEC),
+            (args.split_xcd, fattn.OPT_SPLIT_XCD),
             (args.pf_stage, fattn.OPT_PF_STAGE),
             (args.waves, fattn.OPT_SPLIT_WAVES)]
     fattn.set_option(fattn.OPT_SPLIT_SKIP, 1 if args.no_step_skip else 0)

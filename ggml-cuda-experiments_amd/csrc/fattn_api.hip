@@ -61,10 +61,9 @@ std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and compute
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
-std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto (off), 1 off, 2 on
+std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto, 1 off, 2 on
 std::atomic<int> g_opt_pf_form{0};          // prefill body: 0 auto, 1 the 8-wave form, 2 one wave per SIMD (fattn_pf4.h)
 std::atomic<int> g_opt_pf_stage{0};         // prefill over Q8_0 / Q4_0: 0 auto (staged to f16), 1 in-kernel dequantisation, 2 staged
-std::atomic<int> g_opt_split_spec{0};       // split kernel one-row merge: 0 auto (off), 1 off, 2 speculative granules
 std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
 std::atomic<uint32_t> g_epoch{0};
@@ -232,17 +231,12 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     a.merge_launch = (a.n_chunks >= 4 && a.wave_merge == 0 && !g_opt_split_fused_merge)
                          ? ((resident && g_opt_merge_in_kernel) ? 2 : 1) : 0;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
-    // XCD-grouped order (tile_coords): a tile's chunk workgroups on one XCD
-    a.xcd_group = g_opt_split_xcd == 2 && (a.n_chunks * Y * S) % 8 == 0 ? 1 : 0;
-    // speculative granule merge of one-row tiles (spec_row_merge; D = 64 / 128 / 256)
-    a.spec_merge = g_opt_split_spec == 2 && a.wave_merge == 2 && a.n_chunks > 1 && 64 % (pl.D / 4) == 0 ? 1 : 0;
-    if (a.n_chunks > 1 && a.spec_merge) {
-        // [arrival counters][granules: per tile [chunk][D + 2] x 8 B]
-        const size_t parts = (size_t)S * Y * a.n_chunks;
-        pl.cnt_bytes = (size_t)S * Y * kCntStride * sizeof(uint32_t);
-        pl.ml_bytes = 0;
-        pl.ws_bytes = pl.cnt_bytes + parts * (size_t)(pl.D + 2) * 8;
-    } else if (a.n_chunks > 1 && a.wave_merge) {
+    // XCD-grouped order (tile_coords): a tile's chunk workgroups on one XCD.
+    // Default for the one-row tiles that merge in-kernel (wg_row_merge):
+    // config 3 11.80 vs 11.95 us, six alternating rounds (profiles/r05_a)
+    const bool xcd_auto = a.wave_merge == 2 && a.n_chunks > 1;
+    a.xcd_group = (g_opt_split_xcd == 2 || (g_opt_split_xcd == 0 && xcd_auto)) && (a.n_chunks * Y * S) % 8 == 0 ? 1 : 0;
+    if (a.n_chunks > 1 && a.wave_merge) {
         // [arrival counters][(m, l) per part][row-0 O per part]; parts = waves
         // (wave_merge 1) or workgroups (2)
         const size_t parts = (size_t)S * Y * a.n_chunks * (a.wave_merge == 1 ? nwv : 1);
@@ -724,10 +718,6 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_stage = value;
             return FATTN_OK;
-        case FATTN_OPT_SPLIT_SPEC:
-            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
-            g_opt_split_spec = value;
-            return FATTN_OK;
         case FATTN_OPT_SPLIT_INFLIGHT:
             if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
             g_opt_split_nbuf = value;
@@ -798,9 +788,8 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,
                       pl.a.merge_launch ? " + fattn_mq_merge_kernel" : "");
     else
-        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>%s%s%s", tn(pl.kt), tn(pl.vt),
+        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>%s%s", tn(pl.kt), tn(pl.vt),
                       pl.D, pl.gran, hm, pl.nwv, pl.a.xcd_group ? " (xcd order)" : "",
-                      pl.a.spec_merge ? " (spec merge)" : "",
                       pl.a.merge_launch == 1 ? " + fattn_merge_kernel" : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     const int n = std::snprintf(out, cap, "%s grid(%u,%u,%u) lds %d chunk %d steps/slots %d ws %zu", kern, pl.grid.x,
                                 pl.grid.y, pl.grid.z, pl.lds, pl.a.chunk_len, pl.a.nbuf, pl.ws_bytes);

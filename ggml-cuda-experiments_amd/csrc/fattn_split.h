@@ -93,8 +93,6 @@ struct SplitArgs {
     int merge_launch;   // chunk partials of multi-row tiles: 1 = merged by a second launch (fattn_merge_kernel,
                         // fattn_bd_merge_kernel), 2 = inside the launch (tile_arrive_wait: grid co-resident)
     int step_skip;      // split kernel: 1 = skip steps whose mask is all -inf for the tile (FATTN_OPT_SPLIT_SKIP)
-    int spec_merge;     // split kernel, one-row tiles (wg_row_merge): chunk rows as tagged granules, swept
-                        // speculatively before the arrival count returns (spec_row_merge)
     int xcd_group;      // workgroups in XCD-grouped order (tile_coords; grid size % 8 == 0): batched decode, split kernel
 };
 
@@ -318,11 +316,6 @@ __device__ __forceinline__ uint64_t* arrival_word(const SplitArgs& a, int64_t ti
 // by the lane that later calls arrive_last, before it (same-lane order)
 __device__ __forceinline__ void arrival_begin(const SplitArgs& a, int64_t tile) {
     (void)__hip_atomic_fetch_max(arrival_word(a, tile), a.arrival_stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// the same, returning the word as it was (spec_tag: this launch's generation)
-__device__ __forceinline__ uint64_t arrival_begin_ret(const SplitArgs& a, int64_t tile) {
-    return __hip_atomic_fetch_max(arrival_word(a, tile), a.arrival_stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // one lane: count this arrival; true for the tile's n-th (last) arriver,
@@ -821,136 +814,6 @@ __device__ __forceinline__ void merge_row_parts(const float* parts_o, const floa
     *(f32x4*)(out + d4) = acc * inv;
 }
 
-// Speculative one-row chunk merge (SplitArgs::spec_merge; the wg_row_merge
-// tail with one round trip fewer).  The drain + count + load form pays three
-// dependent round trips after the workgroup's LDS merge: the published row's
-// write-through drain and the arrival atomic (one vmcnt), then the last
-// arriver's loads of the other chunks' rows.  Here every chunk publishes its
-// row as 8-byte granules {value, tag} (cdna_hip_programming.md Guideline 16
-// R2: each granule ONE aligned sc1 store, no drain), and in the same breath
-// -- before its arrival atomic has returned -- issues the sc1 loads of every
-// other chunk's granules; one wait covers stores, loads and atomic.  The
-// workgroup the atomic names last then checks the tags: a granule of another
-// chunk that has not landed yet (its atomic came first, its stores need not
-// have) is re-read until its tag matches (bounded); everything else is
-// merged at once.  The others leave.  The tag is this launch's epoch and the
-// tile's arrival-word generation (read back by arrival_begin's atomic max:
-// re-armed per launch, so a graph replay's granules differ from the
-// previous replay's), top bit set (a zeroed workspace never matches).  Same
-// fa_reduce math and fixed summation order as merge_row_parts (own chunk's
-// row from registers in its slot): bit-identical whichever chunk is last.
-// Layout per tile: [chunk][D + 2 granules] (O dims, then M, L), 16-B rows.
-template <int D>
-constexpr int spec_gran() { return D + 2; }  // granules per chunk row (O dims, M, L)
-
-__device__ __forceinline__ uint32_t spec_tag(const SplitArgs& a, uint64_t old) {
-    const uint32_t ep = (uint32_t)(a.arrival_stamp >> kArrivalEpochShift);
-    const bool same = (old >> 56) == 0xFF && (uint32_t)(old >> kArrivalEpochShift) == ep;
-    const uint32_t gen = same ? (uint32_t)(old >> 16) & 0xFFu : 0u;  // (a new epoch: the stamp restarts at 0)
-    return 0x80000000u | (ep & 0x7FFFFFu) << 8 | gen;
-}
-
-template <int D, int kIt>  // kIt: parts per lane slot row (>= ceil(n_chunks / PPR))
-__device__ __forceinline__ void spec_row_merge(const SplitArgs& a, int64_t tile, int chunk, f32x4 own, float own_m,
-                                               float own_l, uint32_t tag, float* out, int lane) {
-    constexpr float kNegInf = -__builtin_inff();
-    constexpr int LPP = D / 4;
-    constexpr int PPR = merge_ppr<D>();
-    static_assert(64 % LPP == 0, "whole parts per lane row");
-    constexpr int G = spec_gran<D>();
-    const int NP = a.n_chunks;
-    const int h = lane / LPP, d4 = 4 * (lane % LPP);
-    auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
-    uint32_t* gt = (uint32_t*)a.ws_o + (size_t)tile * NP * G * 2;  // the tile's granules, 2 words each
-    // ---- publish this chunk's row: lane (0, dl) stores dims 4dl..4dl+3, lane 0 also (M, L)
-    uint32_t* gp = gt + (size_t)chunk * G * 2;
-    if (h == 0) {
-        st_sc1(gp + 2 * d4, u32x4{bits(own.x), tag, bits(own.y), tag});
-        st_sc1(gp + 2 * d4 + 4, u32x4{bits(own.z), tag, bits(own.w), tag});
-    }
-    if (lane == 0) st_sc1(gp + 2 * D, u32x4{bits(own_m), tag, bits(own_l), tag});
-    // ---- issue the sweep of every chunk row (parts past NP and this chunk's own
-    // slot fall outside the descriptor: zeros, no traffic)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (no instruction: keeps the stores above the loads)
-    const uint32_t rec = (uint32_t)(NP * G * 8);
-    const __amdgpu_buffer_rsrc_t srd = make_rsrc(gt, rec);
-    u32x4 lo[kIt], hi[kIt], ml;
-    auto sweep = [&]() {
-#pragma unroll
-        for (int i = 0; i < kIt; i++) {
-            const int p = PPR * i + h;
-            const uint32_t off = (p < NP && p != chunk) ? (uint32_t)((p * G + d4) * 8) : rec;
-            lo[i] = ld_sc1_buf(srd, off);
-            hi[i] = ld_sc1_buf(srd, off + 16);
-        }
-        ml = ld_sc1_buf(srd, (lane < NP && lane != chunk) ? (uint32_t)((lane * G + D) * 8) : rec);
-    };
-    sweep();
-    // ---- count this arrival (no drain: the last arriver checks the tags)
-    int last = 0;
-    if (lane == 0) last = arrive_last(a, tile, NP);
-    last = __builtin_amdgcn_readfirstlane(last);
-    if (!last) return;
-    // ---- the last arriver: every granule of the other chunks carries this tag
-    auto stale = [&]() {
-        bool bad = false;
-#pragma unroll
-        for (int i = 0; i < kIt; i++) {
-            const int p = PPR * i + h;
-            if (p < NP && p != chunk)
-                bad |= lo[i].y != tag || lo[i].w != tag || hi[i].y != tag || hi[i].w != tag;
-        }
-        if (lane < NP && lane != chunk) bad |= ml.y != tag || ml.w != tag;
-        return bad;
-    };
-    bool ok = true;
-    for (uint32_t spins = 0; __builtin_amdgcn_ballot_w64(stale()) != 0; spins++) {  // wave-uniform
-        if (spins == (1u << 16)) {
-            ok = false;
-            break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        sweep();
-    }
-    const float mp = lane < NP ? (lane == chunk ? own_m : __builtin_bit_cast(float, ml.x)) : kNegInf;
-    const float lp = lane == chunk ? own_l : __builtin_bit_cast(float, ml.z);
-    const float M = seg_reduce<true>(mp, 64);
-    const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M);
-    const float L = seg_reduce<false>(lane < NP ? w * lp : 0.0f, 64);
-    const int wi = __builtin_bit_cast(int, w);
-    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int i = 0; i < kIt; i++) {
-        float wp = 0.0f;
-#pragma unroll
-        for (int j = 0; j < PPR; j++) {
-            const float wj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(wi, (PPR * i + j) & 63));
-            wp = (h == j) ? wj : wp;
-        }
-        const int p = PPR * i + h;
-        const f32x4 v = p == chunk ? own
-                                   : f32x4{__builtin_bit_cast(float, lo[i].x), __builtin_bit_cast(float, lo[i].z),
-                                           __builtin_bit_cast(float, hi[i].x), __builtin_bit_cast(float, hi[i].z)};
-        acc += wp * v;
-    }
-    if constexpr (PPR == 4) {
-        acc.x = xor16_pair(acc.x, false);
-        acc.y = xor16_pair(acc.y, false);
-        acc.z = xor16_pair(acc.z, false);
-        acc.w = xor16_pair(acc.w, false);
-    }
-    if constexpr (PPR >= 2) {
-        acc.x = xor32_pair(acc.x, false);
-        acc.y = xor32_pair(acc.y, false);
-        acc.z = xor32_pair(acc.z, false);
-        acc.w = xor32_pair(acc.w, false);
-    }
-    if (h) return;
-    const float inv = L == 0.0f ? __builtin_nanf("") : 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
-    const float nan = __builtin_nanf("");
-    *(f32x4*)(out + d4) = ok ? acc * inv : f32x4{nan, nan, nan, nan};  // (a bounded wait that gave up: a fault)
-}
-
 // One-row tiles, NW waves per workgroup: every wave writes its row-0 state
 // (O, m, l) into its own LDS region (its steps have all landed), one barrier,
 // then wave 0 merges the NW states (lane (h, dl): states p = h mod PPR, dims
@@ -962,7 +825,7 @@ __device__ __forceinline__ void spec_row_merge(const SplitArgs& a, int64_t tile,
 template <int D, bool VQ8, int NW>
 __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o)[D / 16], float m_run, float l_tot,
                                              int chunk, int wave, int lane, int qt, int hs, int ik2, int iq3,
-                                             int y, uint8_t* smem, int region, uint32_t tag) {
+                                             int y, uint8_t* smem, int region) {
     constexpr int NB = D / QK;
     constexpr int NC = D / 16;
     constexpr float kNegInf = -__builtin_inff();
@@ -1039,17 +902,6 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
     return;
 #endif
     const int64_t tile = (int64_t)iq3 * gridDim.y + y;
-    if constexpr (64 % LPP == 0) {
-        if (a.spec_merge) {  // granules + speculative sweep (spec_row_merge)
-            tag = __builtin_amdgcn_readfirstlane(tag);
-            const int need = (a.n_chunks + PPR - 1) / PPR;
-            if (need <= 4) spec_row_merge<D, 4>(a, tile, chunk, acc, M, L, tag, out, lane);
-            else if (need <= 8) spec_row_merge<D, 8>(a, tile, chunk, acc, M, L, tag, out, lane);
-            else spec_row_merge<D, 16>(a, tile, chunk, acc, M, L, tag, out, lane);
-            FATTN_STAMP(13);
-            return;
-        }
-    }
     float* po = a.ws_o + (tile * a.n_chunks + chunk) * D;
     auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
     if (h == 0) st_sc1(po + d4, u32x4{bits(acc.x), bits(acc.y), bits(acc.z), bits(acc.w)});
@@ -1089,7 +941,7 @@ template <int KT, int VT, int D, int NW, int EPI>
 __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D / 16], float m_run, float l_run,
                                                float (&corr)[(D + QK - 1) / QK], int wave, int lane, int qt, int hs, int ik2,
                                                int iq3, int y, int chunk, uint8_t* smem, int region, bool active,
-                                               bool sync_first, uint32_t tag = 0) {
+                                               bool sync_first) {
     using C = SplitCfg<KT, VT, D>;
     constexpr int NB = D / QK;
     constexpr int NC = D / 16;
@@ -1116,7 +968,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
         wave_merge_epilogue<D, kVQ8, NW>(a, o, m_run, l_tot, chunk, wave, lane, qt, hs, ik2, iq3, y);
         return;
     } else if constexpr (EPI == 2) {
-        wg_row_merge<D, kVQ8, NW>(a, o, m_run, l_tot, chunk, wave, lane, qt, hs, ik2, iq3, y, smem, region, tag);
+        wg_row_merge<D, kVQ8, NW>(a, o, m_run, l_tot, chunk, wave, lane, qt, hs, ik2, iq3, y, smem, region);
         return;
     }
     constexpr int MS = C::kMergeStride;
@@ -1567,13 +1419,8 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     // this launch's stamp on the tile's arrival word, by each lane that will
     // count an arrival: issued after the prologue's DMA, so no wait is spent
     // on it (at most one DMA instruction's worth in the counted waits below)
-    uint32_t tag = 0;  // spec_merge: the granule tag (wave 0, lane 0)
-    if (a.n_chunks > 1 && a.merge_launch != 1 && lane == 0 && (EPI == 1 || wave == 0)) {
-        if (EPI == 2 && a.spec_merge)
-            tag = spec_tag(a, arrival_begin_ret(a, (int64_t)iq3 * gridDim.y + y));
-        else
-            arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
-    }
+    if (a.n_chunks > 1 && a.merge_launch != 1 && lane == 0 && (EPI == 1 || wave == 0))
+        arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
 
     FATTN_STAMP(1);
     if (a.split_prio == 2) __builtin_amdgcn_s_setprio(0);
@@ -1662,7 +1509,7 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
 #endif
     FATTN_STAMP(10);
     split_epilogue<KT, VT, D, NWV, EPI>(a, o, m_run, l_run, corr, wave, lane, qt, hs, ik2, iq3, y, chunk, smem, a.wave_bytes,
-                                   true, false, tag);
+                                   true, false);
 }
 
 // ---------------------------------------------------------------- merge launch

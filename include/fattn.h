@@ -190,12 +190,10 @@ enum {
                                        (chunk fastest), 2 = XCD-grouped: each of the 8 XCDs takes whole (kv head x
                                        row tile)s, so a tile's Q rows come from HBM once, not once per chunk
                                        (needs a grid of a multiple of 8 workgroups; otherwise plain) */,
-    FATTN_OPT_SPLIT_XCD = 26        /* split kernel: workgroup order. 0 = auto (plain), 1 = plain, 2 = XCD-grouped:
+    FATTN_OPT_SPLIT_XCD = 26        /* split kernel: workgroup order. 0 = auto (XCD-grouped for one-row tiles merged
+                                       in the launch, e.g. config 3; plain otherwise), 1 = plain, 2 = XCD-grouped:
                                        a tile's chunk workgroups on one XCD (grid a multiple of 8 workgroups) */,
-    FATTN_OPT_SPLIT_SPEC = 27       /* split kernel, one-row tiles merged across chunks (wg_row_merge): 0 = auto
-                                       (drain + count + load), 1 = the same, 2 = speculative: chunk rows published
-                                       as tagged 8-B granules and swept before the arrival count returns (one
-                                       round trip fewer; the last arriver re-reads stale granules) */,
+    /* 27: a removed experiment (speculative granule merge of one-row tiles: slower), rejected */
     FATTN_OPT_PF_STAGE = 28         /* prefill kernel over Q8_0 / Q4_0 K/V: 0 = auto (staged), 1 = dequantised in
                                        the kernel, tile by tile, once per 256-row query tile; 2 = staged: the rows
                                        converted once to f16 in the workspace (kv_stage_f16, + 2 * Skv * Hkv * N *

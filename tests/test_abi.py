@@ -119,7 +119,7 @@ def test_bd_xcd_option():
     kernels when the grid is a multiple of 8 workgroups; other plans unchanged."""
     with fattn.options({fattn.OPT_BD_XCD: 2}):
         assert "(xcd order)" in fattn.describe(_params(NQ=64))                   # grid(8,32,1)
-        assert "(xcd order)" not in fattn.describe(_params())                    # config 3: split kernel
+        assert "(xcd order)" in fattn.describe(_params())                        # config 3: split kernel (FATTN_OPT_SPLIT_XCD auto)
         d5 = fattn.describe(_params(NQ=64, H=5, Hkv=5, N=32768))             # grid(52,5,1): not a multiple of 8
         assert d5.startswith("fattn_bdp_kernel") and "(xcd order)" not in d5, d5
     with fattn.options({fattn.OPT_BD_XCD: 1}):
@@ -127,6 +127,20 @@ def test_bd_xcd_option():
     assert "(xcd order)" in fattn.describe(_params(NQ=64))  # (the default)
     with pytest.raises(Exception):
         fattn.set_option(fattn.OPT_BD_XCD, 3)
+
+
+def test_split_xcd_option():
+    """FATTN_OPT_SPLIT_XCD: one-row tiles merged in the launch (config 3) take
+    the XCD-grouped order by default; multi-row tiles (merge launch) stay
+    plain unless forced; 1 = plain everywhere."""
+    assert "(xcd order)" in fattn.describe(_params())                                   # config 3
+    assert "(xcd order)" not in fattn.describe(_params(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0))  # config 4
+    with fattn.options({fattn.OPT_SPLIT_XCD: 1}):
+        assert "(xcd order)" not in fattn.describe(_params())
+    with fattn.options({fattn.OPT_SPLIT_XCD: 2}):
+        assert "(xcd order)" in fattn.describe(_params(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0))
+    with pytest.raises(Exception):
+        fattn.set_option(27, 2)  # the removed speculative-merge option
 
 
 def test_merge_in_kernel_option():

@@ -196,9 +196,9 @@ def test_workspace_prefill_then_decode(dev):
     dict(D=128, NQ=16, H=4, N=4096, kv_type="q8_0"),                  # multi-row tiles, second-launch merge
     dict(D=128, NQ=64, H=32, Hkv=8, N=2048, kv_type="q8_0", mq=1, merge=1),  # multi-query kernel, fused
     dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0"),                  # batched-decode kernel (merge launch)
-    dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", spec=2),          # config 3, speculative granule merge
-    dict(D=64, NQ=1, H=32, N=8192, kv_type="q4_0", spec=2, xcd=2),    # the same at D = 64, XCD order
-], ids=["row_merge", "wave_merge", "combine", "merge_launch", "mq", "bd", "spec_merge", "spec_merge_d64_xcd"])
+    dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0", xcd=1),          # config 3, plain workgroup order
+    dict(D=64, NQ=1, H=32, N=8192, kv_type="q4_0"),                   # D = 64, XCD order (auto)
+], ids=["row_merge", "wave_merge", "combine", "merge_launch", "mq", "bd", "row_merge_plain", "row_merge_d64"])
 def test_workspace_not_zeroed(dev, case, fill):
     # (the multi-row case merges in a second launch and never reads the words;
     # it checks that the garbage does not leak into the partials either)
@@ -211,13 +211,11 @@ def test_workspace_not_zeroed(dev, case, fill):
     waves = case.pop("waves", 0)
     merge = case.pop("merge", 0)
     mq = case.pop("mq", 0)
-    spec = case.pop("spec", 0)
     xcd = case.pop("xcd", 0)
     p = make_problem(seed=71, **case)
     t = upload(p, dev)
     fattn.set_option(fattn.OPT_SPLIT_WAVES, waves)
     fattn.set_option(fattn.OPT_SPLIT_MERGE, merge)
-    fattn.set_option(fattn.OPT_SPLIT_SPEC, spec)
     fattn.set_option(fattn.OPT_SPLIT_XCD, xcd)
     if mq:
         fattn.set_option(fattn.OPT_BD, 1)
@@ -225,8 +223,8 @@ def test_workspace_not_zeroed(dev, case, fill):
     try:
         att = fattn.Attention(*views(p, t), t["dst"], p.scale)
         assert int(att.describe().split("grid(")[1].split(",")[0]) > 1, att.describe()  # several chunks
-        assert ("(spec merge)" in att.describe()) == (spec == 2), att.describe()
-        assert ("(xcd order)" in att.describe()) == (xcd == 2), att.describe()
+        if xcd == 1:
+            assert "(xcd order)" not in att.describe(), att.describe()
         ws = att.workspace
         if fill == "bytes5a":
             ws.fill_(0x5A)
@@ -494,16 +492,15 @@ def _replay_new_inputs(dev, shape, n_iter=12):
     return att.describe()
 
 
-@pytest.mark.parametrize("spec,xcd", [(0, 0), (2, 0), (2, 2), (0, 2)], ids=["drain", "spec", "spec_xcd", "xcd"])
-def test_row_merge_graph_replays_new_inputs(dev, spec, xcd):
+@pytest.mark.parametrize("xcd", [1, 0], ids=["plain", "xcd_auto"])
+def test_row_merge_graph_replays_new_inputs(dev, xcd):
     """Config 3 (one-row tiles, last-arriver merge): a captured launch replays
     with one epoch; the arrival words re-arm (count 0, generation + 1) so every
-    replay merges its own partials -- and, with the speculative granule merge
-    (FATTN_OPT_SPLIT_SPEC = 2), tags its granules with that generation, so a
-    replay never takes the previous replay's granules for its own."""
-    with fattn.options({fattn.OPT_SPLIT_SPEC: spec, fattn.OPT_SPLIT_XCD: xcd}):
+    replay merges its own partials -- in the plain and the XCD-grouped
+    workgroup order (the default for these tiles)."""
+    with fattn.options({fattn.OPT_SPLIT_XCD: xcd}):
         desc = _replay_new_inputs(dev, dict(D=128, NQ=1, H=32, N=4096, kv_type="q8_0"))
-    assert ("(spec merge)" in desc) == (spec == 2) and ("(xcd order)" in desc) == (xcd == 2), desc
+    assert ("(xcd order)" in desc) == (xcd == 0), desc
 
 
 @pytest.mark.parametrize("in_kernel", [1, 0], ids=["in_kernel", "second_launch"])

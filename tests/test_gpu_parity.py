@@ -89,24 +89,23 @@ def test_config3_q8_0(dev, layout):
     dict(D=64, NQ=1, H=16, N=16384, kv_type="q4_0"),                          # D = 64, 16+ chunks
     dict(D=256, NQ=1, H=8, N=8192, kv_type="q8_0"),                           # D = 256
 ], ids=["cfg3_pos", "cfg3_tail", "f16", "d64_q4", "d256"])
-@pytest.mark.parametrize("xcd", [0, 2], ids=["plain", "xcd"])
-def test_row_merge_spec_and_xcd_bit_identical(dev, case, xcd):
-    """One-row tiles: the speculative granule merge (FATTN_OPT_SPLIT_SPEC = 2)
-    and the XCD-grouped workgroup order (FATTN_OPT_SPLIT_XCD = 2) give the
-    oracle's answer and the default form's bits (fixed merge order, the last
-    arriver's own row taken from registers in its slot)."""
+def test_row_merge_xcd_order_bit_identical(dev, case):
+    """One-row tiles: the XCD-grouped workgroup order (FATTN_OPT_SPLIT_XCD,
+    the default for them) gives the plain order's bits and the oracle's
+    answer -- the chunk merge sums in a fixed order whichever workgroup
+    arrives last."""
     p = make_problem(seed=33, **case)
     ref = p.oracle()
-    base = run_gpu(p)
-    with fattn.options({fattn.OPT_SPLIT_SPEC: 2, fattn.OPT_SPLIT_XCD: xcd}):
-        t = upload(p)
-        att = fattn.Attention(*views(p, t), t["dst"], p.scale)
-        assert "(spec merge)" in att.describe(), att.describe()
-        for _ in range(3):
-            t["dst"].fill_(float("nan"))
-            att()
-            got = t["dst"].cpu().numpy()
-            assert np.array_equal(got, base, equal_nan=True)
+    with fattn.options({fattn.OPT_SPLIT_XCD: 1}):
+        base = run_gpu(p)
+    t = upload(p)
+    att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+    assert "(xcd order)" in att.describe(), att.describe()
+    for _ in range(3):
+        t["dst"].fill_(float("nan"))
+        att()
+        got = t["dst"].cpu().numpy()
+        assert np.array_equal(got, base, equal_nan=True)
     assert attn_rel_err(got, ref) <= RTOL
 
 
