@@ -40,6 +40,7 @@ struct Plan {
     // prefill over Q8_0 / Q4_0: the rows staged to f16 in the workspace first
     // (kv_stage_f16_kernel), then the f16 prefill kernel (kt = vt = F16 then)
     bool pf4 = false;       // the prefill's one-wave-per-SIMD body (fattn_pf4.h; f16 rows, D = 128)
+    int pf4_sched = 0;      // ... its schedule (fattn_pf4_kernel's SCHED)
     bool pf_stage = false;
     int stage_kt = 0;                                  // the cache's type
     const uint8_t *stage_k = nullptr, *stage_v = nullptr;  // the cache's K / V
@@ -182,7 +183,8 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     auto kern = fattn_pf_kernel<KT, D, HM>;
     const void* main_kern = (const void*)kern;
     if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
-        if (pl.pf4) main_kern = (const void*)fattn_pf4_kernel<D, HM>;
+        if (pl.pf4)
+            main_kern = pl.pf4_sched ? (const void*)fattn_pf4_kernel<D, HM, 1> : (const void*)fattn_pf4_kernel<D, HM, 0>;
     }
     return launch_kernel(main_kern, pl, st, ev, [&] {
         if constexpr (KT == FATTN_TYPE_F16 && D % QK == 0) {
@@ -202,7 +204,10 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
                                pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
         if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
             if (pl.pf4) {
-                hipLaunchKernelGGL((fattn_pf4_kernel<D, HM>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
+                if (pl.pf4_sched)
+                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 1>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
+                else
+                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 0>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
                 return;
             }
         }

@@ -67,7 +67,14 @@ __device__ __forceinline__ float add_f32(float x, float y) {
     return r;
 }
 
-template <int D, bool HM>
+// SCHED 0: per tile A (QK rb1 || softmax rb0), B (PV rb0 || softmax rb1),
+// C (PV rb1, QK rb0 of the next tile).  SCHED 1 (rebalanced): the softmax in
+// two parts -- smax (scores, max, rescale decision) and sexp (exponentials,
+// sums, f16 P) -- spread so that every 16-MFMA group carries some of it:
+//   A: QK rb1 || sexp rb0;  B: PV rb0 || smax rb1, sexp rb1 t0;
+//   C1: QK rb0 (next tile) || sexp rb1 t1;  C2: PV rb1 || smax rb0 (next tile).
+// Same arithmetic, same order per row block: both give the same bits.
+template <int D, bool HM, int SCHED>
 __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const SplitArgs a) {
     using C = Pf4Cfg<D>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -304,9 +311,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     // basic blocks, and the exponentials could no longer sit between the
     // MFMAs): the rescale decision and l's factor are selects; O's factor is
     // applied at the next phase boundary (rescale_o), before that block's P.V.
-    auto softmax = [&](int rb, const f32x16 (&st)[2], const u32x2 (&mk)[2][4], f16x8 (&pb)[2][2], float& alpha,
-                       bool& resc) {
-        float us[2][16];
+    // In two parts (the rebalanced schedule places them in different phases):
+    // smax -- scores, tile max, the rescale decision (wave-uniform), l's
+    // factor -- and sexp per subtile -- exponentials, row sums, f16 P^T.
+    auto smax = [&](int rb, const f32x16 (&st)[2], const u32x2 (&mk)[2][4], float (&us)[2][16], float& alpha,
+                    bool& resc) {
         float tmax = kNegInf;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
@@ -330,26 +339,33 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
         alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
         m_run[rb] = m_new;
-        const float nm = (m_new == kNegInf) ? 0.0f : -m_new;
-        float la = l2[rb].x * alpha, lb = l2[rb].y * alpha;
+        l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
+    };
+    auto sexp = [&](int rb, int t, const float (&us)[2][16], f16x8 (&pb)[2][2]) {
+        const float nm = (m_run[rb] == kNegInf) ? 0.0f : -m_run[rb];
+        float la = l2[rb].x, lb = l2[rb].y;
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
+        for (int q = 0; q < 2; q++) {
+            f16x8 x;
 #pragma unroll
-            for (int q = 0; q < 2; q++) {
-                f16x8 x;
-#pragma unroll
-                for (int e = 0; e < 8; e += 2) {
-                    const float pa = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e], cexp, nm));
-                    const float pb2 = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e + 1], cexp, nm));
-                    la = add_f32(la, pa);  // (scalar: packed f32 adds cost more beside MFMAs)
-                    lb = add_f32(lb, pb2);
-                    x[e] = (f16)pa;
-                    x[e + 1] = (f16)pb2;
-                }
-                pb[t][q] = x;
+            for (int e = 0; e < 8; e += 2) {
+                const float pa = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e], cexp, nm));
+                const float pb2 = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e + 1], cexp, nm));
+                la = add_f32(la, pa);  // (scalar: packed f32 adds cost more beside MFMAs)
+                lb = add_f32(lb, pb2);
+                x[e] = (f16)pa;
+                x[e + 1] = (f16)pb2;
             }
+            pb[t][q] = x;
         }
         l2[rb] = f32x2{la, lb};
+    };
+    auto softmax = [&](int rb, const f32x16 (&st)[2], const u32x2 (&mk)[2][4], f16x8 (&pb)[2][2], float& alpha,
+                       bool& resc) {
+        float us[2][16];
+        smax(rb, st, mk, us, alpha, resc);
+        sexp(rb, 0, us, pb);
+        sexp(rb, 1, us, pb);
     };
     // (the empty asm keeps hipcc from if-converting the rare branch into an
     // unconditional multiply of O by alpha = 1: 128 VALU + AGPR moves a tile)
@@ -367,7 +383,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     // O_rb^T += V_s^T . P_rb^T: per subtile t, its V^T operands (gathered by
     // ds_read_b64_tr_b16 in the accumulator's key order) then 2 x NDB MFMAs;
     // the V^T operands are read per phase (B for rb 0, C for rb 1), not held
-    auto pv = [&](int s, int rb, const f16x8 (&pb)[2][2]) {
+    auto pv_t = [&](int s, int rb, int t, const f16x8 (&pb)[2][2]) {
         // (the per-tile base through an empty asm: otherwise hipcc hoists
         // vbase + every read's offset out of the loop -- 32 loop-invariant
         // addresses, spilled to AGPRs -- and no offset folds into a read)
@@ -376,26 +392,27 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         asm volatile("" : "+v"(b0), "+v"(b1));
         lds_u8* const img0 = lsm + b0;
         lds_u8* const img1 = lsm + b1;
+        u32x4 va[2][NDB];
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
-            u32x4 va[2][NDB];
+        for (int q = 0; q < 2; q++) {
 #pragma unroll
-            for (int q = 0; q < 2; q++) {
-#pragma unroll
-                for (int db = 0; db < NDB; db++) {
-                    const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
-                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
-                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img1 + off));
-                    const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
-                    va[q][db] = u32x4{a2.x, a2.y, b2.x, b2.y};
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 2; q++) {
-#pragma unroll
-                for (int db = 0; db < NDB; db++) o[rb][db] = mfma32(__builtin_bit_cast(f16x8, va[q][db]), pb[t][q], o[rb][db]);
+            for (int db = 0; db < NDB; db++) {
+                const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img1 + off));
+                const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                va[q][db] = u32x4{a2.x, a2.y, b2.x, b2.y};
             }
         }
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+#pragma unroll
+            for (int db = 0; db < NDB; db++) o[rb][db] = mfma32(__builtin_bit_cast(f16x8, va[q][db]), pb[t][q], o[rb][db]);
+        }
+    };
+    auto pv = [&](int s, int rb, const f16x8 (&pb)[2][2]) {
+        pv_t(s, rb, 0, pb);
+        pv_t(s, rb, 1, pb);
     };
 
     // ---- S0 of tile 0 (the loop's C phase computes it for the next tile):
@@ -414,56 +431,138 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         qk(0, 0, s0);
     }
 
-    for (int s = 0; s < nt; s++) {
-        // ---- A: S1 = K_s . Q1^T  ||  softmax of rb 0
-        u32x2 mk0[2][4], mk1[2][4];
-        f16x8 p0[2][2], p1[2][2];
-        float al0, al1;
-        bool rs0, rs1;
-        mask_reads(s, 0, mk0);
-        qk(s, 1, s1);
-        softmax(0, s0, mk0, p0, al0, rs0);
-        __builtin_amdgcn_sched_group_barrier(0x100, NK + (HM ? 8 : 0), 0);  // subtile 0's K operands, the mask
+    if constexpr (SCHED == 0) {
+        for (int s = 0; s < nt; s++) {
+            // ---- A: S1 = K_s . Q1^T  ||  softmax of rb 0
+            u32x2 mk0[2][4], mk1[2][4];
+            f16x8 p0[2][2], p1[2][2];
+            float al0, al1;
+            bool rs0, rs1;
+            mask_reads(s, 0, mk0);
+            qk(s, 1, s1);
+            softmax(0, s0, mk0, p0, al0, rs0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NK + (HM ? 8 : 0), 0);  // subtile 0's K operands, the mask
 #pragma unroll
-        for (int i = 0; i < 2 * NK; i++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // up to five VALU
-            if (i < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // subtile 1's K operands
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        rescale_o(0, rs0, al0);
-        // ---- B: O0 += V_s^T . P0^T  ||  softmax of rb 1
-        mask_reads(s, 1, mk1);
-        pv(s, 0, p0);
-        softmax(1, s1, mk1, p1, al1, rs1);
-        // the mask and subtile 0's V^T reads, then per MFMA up to five VALU
-        // and one of subtile 1's V^T reads
-        __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB + (HM ? 8 : 0), 0);
+            for (int i = 0; i < 2 * NK; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // up to five VALU
+                if (i < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // subtile 1's K operands
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            rescale_o(0, rs0, al0);
+            // ---- B: O0 += V_s^T . P0^T  ||  softmax of rb 1
+            mask_reads(s, 1, mk1);
+            pv(s, 0, p0);
+            softmax(1, s1, mk1, p1, al1, rs1);
+            // the mask and subtile 0's V^T reads, then per MFMA up to five VALU
+            // and one of subtile 1's V^T reads
+            __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB + (HM ? 8 : 0), 0);
 #pragma unroll
-        for (int i = 0; i < 4 * NDB; i++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-            if (i < 4 * NDB) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            for (int i = 0; i < 4 * NDB; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+                if (i < 4 * NDB) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- C: barrier (every wave is done with tile s's K and mask and
+            // tile s-1's V; tile s+1's mask and V and K landed), refill, O1 +=
+            // V_s^T . P1^T, S0 = K_{s+1} . Q0^T
+            {
+                // issued at C_{s-1} (or in the prologue): mask s+1, V s+1, K s+2 --
+                // K s+2 may fly on
+                if (s + 2 < nt) wait_vmcnt_c<C::NKI>();
+                else wait_vmcnt_c<0>();
+            }
+            __syncthreads();
+            if (s + 2 < nt) {
+                m_issue(s + 2);
+                v_issue(s + 2);
+            }
+            if (s + 3 < nt) k_issue(s + 3);
+            rescale_o(1, rs1, al1);
+            pv(s, 1, p1);
+            if (s + 1 < nt) qk(s + 1, 0, s0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- C: barrier (every wave is done with tile s's K and mask and
-        // tile s-1's V; tile s+1's mask and V and K landed), refill, O1 +=
-        // V_s^T . P1^T, S0 = K_{s+1} . Q0^T
-        {
-            // issued at C_{s-1} (or in the prologue): mask s+1, V s+1, K s+2 --
-            // K s+2 may fly on
+    } else {
+        // the rebalanced schedule (see the kernel's comment)
+        float us0[2][16], us1[2][16];
+        float al0 = 1.0f, al1 = 1.0f;
+        bool rs0 = false, rs1 = false;
+        if (nt > 0) {
+            u32x2 mk[2][4];
+            mask_reads(0, 0, mk);
+            smax(0, s0, mk, us0, al0, rs0);
+        }
+        auto iter = [&](int s, auto has_next) {
+            constexpr bool NX = decltype(has_next)::value;
+            f16x8 p0[2][2], p1[2][2];
+            u32x2 mk1[2][4], mk0[2][4];
+            rescale_o(0, rs0, al0);
+            // ---- A: S1 = K_s . Q1^T  ||  rb 0's exponentials
+            mask_reads(s, 1, mk1);
+            qk(s, 1, s1);
+            sexp(0, 0, us0, p0);
+            sexp(0, 1, us0, p0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NK + (HM ? 8 : 0), 0);
+#pragma unroll
+            for (int i = 0; i < 2 * NK; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+                if (i < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- B: O0 += V_s^T . P0^T  ||  rb 1's scores and max, its first subtile's exponentials
+            pv(s, 0, p0);
+            smax(1, s1, mk1, us1, al1, rs1);
+            sexp(1, 0, us1, p1);
+            __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB, 0);
+#pragma unroll
+            for (int i = 0; i < 4 * NDB; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 9, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- C: barrier (as SCHED 0), refill
             if (s + 2 < nt) wait_vmcnt_c<C::NKI>();
             else wait_vmcnt_c<0>();
-        }
-        __syncthreads();
-        if (s + 2 < nt) {
-            m_issue(s + 2);
-            v_issue(s + 2);
-        }
-        if (s + 3 < nt) k_issue(s + 3);
-        rescale_o(1, rs1, al1);
-        pv(s, 1, p1);
-        if (s + 1 < nt) qk(s + 1, 0, s0);
+            __syncthreads();
+            if (s + 2 < nt) {
+                m_issue(s + 2);
+                v_issue(s + 2);
+            }
+            if (s + 3 < nt) k_issue(s + 3);
+            rescale_o(1, rs1, al1);
+            // ---- C1: S0 = K_{s+1} . Q0^T  ||  rb 1's second subtile's exponentials
+            if constexpr (NX) {
+                mask_reads(s + 1, 0, mk0);
+                qk(s + 1, 0, s0);
+            }
+            sexp(1, 1, us1, p1);
+            if constexpr (NX) {
+                __builtin_amdgcn_sched_group_barrier(0x100, NK + (HM ? 8 : 0), 0);
+#pragma unroll
+                for (int i = 0; i < 2 * NK; i++) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+                    if (i < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- C2: O1 += V_s^T . P1^T  ||  rb 0's scores and max of the next tile
+            pv(s, 1, p1);
+            if constexpr (NX) smax(0, s0, mk0, us0, al0, rs0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB, 0);
+#pragma unroll
+            for (int i = 0; i < 4 * NDB; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        for (int s = 0; s + 1 < nt; s++) iter(s, std::true_type());
+        if (nt > 0) iter(nt - 1, std::false_type());
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 

@@ -199,7 +199,8 @@ enum {
                                        converted once to f16 in the workspace (kv_stage_f16, + 2 * Skv * Hkv * N *
                                        D * 2 bytes of fattn_workspace_size), then the f16 prefill kernel */,
     FATTN_OPT_PF_FORM = 29          /* prefill body over f16 rows (native or staged) at D = 128: 0 = auto, 1 = the
-                                       8-wave form (fattn_pf_kernel), 2 = one wave per SIMD (fattn_pf4_kernel) */
+                                       8-wave form (fattn_pf_kernel), 2 = one wave per SIMD (fattn_pf4_kernel),
+                                       3 = the same with the rebalanced phase schedule */
 };
 int fattn_set_option(int option, int value);
 

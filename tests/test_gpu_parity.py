@@ -629,7 +629,7 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture(params=[(0, 1), (1, 1), (0, 2)], ids=["staged", "inkernel_deq", "staged_pf4"])
+@pytest.fixture(params=[(0, 1), (1, 1), (0, 2), (0, 3)], ids=["staged", "inkernel_deq", "staged_pf4", "staged_pf4s1"])
 def pf_force(request):
     """The prefill kernels on every eligible problem: Q8_0 / Q4_0 K/V staged
     to f16 first (the default) or dequantised inside the kernel
@@ -664,18 +664,20 @@ def test_pf4_bit_identical_to_pf(dev, case):
     outs = {}
     fattn.set_option(fattn.OPT_PF, 2)
     try:
-        for form in (1, 2):
+        for form in (1, 2, 3):
             fattn.set_option(fattn.OPT_PF_FORM, form)
             t = upload(p)
             att = fattn.Attention(*views(p, t), t["dst"], p.scale)
-            assert ("fattn_pf4_kernel" in att.describe()) == (form == 2), att.describe()
+            assert ("fattn_pf4_kernel" in att.describe()) == (form >= 2), att.describe()
+            assert ("(sched1)" in att.describe()) == (form == 3), att.describe()
             att()
             outs[form] = t["dst"].cpu().numpy()
     finally:
         fattn.set_option(fattn.OPT_PF, 0)
         fattn.set_option(fattn.OPT_PF_FORM, 0)
     assert np.array_equal(outs[1], outs[2], equal_nan=True)
-    assert attn_rel_err(outs[2], p.oracle()) <= RTOL
+    assert np.array_equal(outs[1], outs[3], equal_nan=True)
+    assert attn_rel_err(outs[3], p.oracle()) <= RTOL
 
 
 @pytest.mark.parametrize("case", [
