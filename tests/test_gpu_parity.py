@@ -98,14 +98,15 @@ def test_row_merge_xcd_order_bit_identical(dev, case):
     ref = p.oracle()
     with fattn.options({fattn.OPT_SPLIT_XCD: 1}):
         base = run_gpu(p)
-    t = upload(p)
-    att = fattn.Attention(*views(p, t), t["dst"], p.scale)
-    assert "(xcd order)" in att.describe(), att.describe()
-    for _ in range(3):
-        t["dst"].fill_(float("nan"))
-        att()
-        got = t["dst"].cpu().numpy()
-        assert np.array_equal(got, base, equal_nan=True)
+    with fattn.options({fattn.OPT_SPLIT_XCD: 2}):  # (the auto rule covers the 8-wave row merge only)
+        t = upload(p)
+        att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+        assert "(xcd order)" in att.describe(), att.describe()
+        for _ in range(3):
+            t["dst"].fill_(float("nan"))
+            att()
+            got = t["dst"].cpu().numpy()
+            assert np.array_equal(got, base, equal_nan=True)
     assert attn_rel_err(got, ref) <= RTOL
 
 
