@@ -58,14 +58,43 @@ struct Pf4Cfg {
     static_assert(ldsBytes <= 163840, "");
 };
 
-// one v_add_f32: hipcc's SLP vectoriser would pair adjacent f32 adds into
-// v_pk_add_f32, which costs more than two scalar adds between MFMAs
-// (MI355X_MICROARCH.md, per-instruction constants)
+// row-sum add.  Plain C: hipcc places the trans-use wait state after each
+// v_exp_f32 only for instructions it sees; an inline-asm v_add_f32 reading an
+// exponential one instruction after its v_exp read a stale register in some
+// lanes (rows scaled or sign-flipped; FATTN_PF4_ASM_ADD keeps that form for A/B
+// and hazard-checker tests only)
 __device__ __forceinline__ float add_f32(float x, float y) {
+#ifdef FATTN_PF4_ASM_ADD  // diagnostic build only: WRONG results (see above)
     float r;
     asm("v_add_f32_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
     return r;
+#else
+    // (not contracted with l's rescale multiply into one fma: the 8-wave
+    // body rounds the two separately, and the forms must give the same bits)
+#pragma clang fp contract(off)
+    return x + y;
+#endif
 }
+// diagnostic builds only: without the scheduling groups / the opaque bases
+#ifdef FATTN_PF4_NO_SGB
+#define PF4_SGB(m, n, id) ((void)0)
+#else
+#define PF4_SGB(m, n, id) __builtin_amdgcn_sched_group_barrier(m, n, id)
+#endif
+#ifdef FATTN_PF4_SHFL
+#define PF4_XOR32(x, mx) ((mx) ? fmaxf((x), __shfl_xor((x), 32)) : (x) + __shfl_xor((x), 32))
+#else
+#define PF4_XOR32(x, mx) xor32_pair((x), (mx))
+#endif
+#ifdef FATTN_PF4_NO_OPAQUE
+#define PF4_OPAQUE_V(x) ((void)0)
+#define PF4_OPAQUE_S(x) ((void)0)
+#define PF4_OPAQUE_V2(x, y) ((void)0)
+#else
+#define PF4_OPAQUE_V(x) asm volatile("" : "+v"(x))
+#define PF4_OPAQUE_S(x) asm volatile("" : "+s"(x))
+#define PF4_OPAQUE_V2(x, y) asm volatile("" : "+v"(x), "+v"(y))
+#endif
 
 // SCHED 0: per tile A (QK rb1 || softmax rb0), B (PV rb0 || softmax rb1),
 // C (PV rb1, QK rb0 of the next tile).  SCHED 1 (rebalanced): the softmax in
@@ -272,7 +301,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     // register file holds O, Q^T and one tile's V^T operands)
     auto qk = [&](int s, int rb, f32x16 (&st)[2]) {
         uint32_t kb = (uint32_t)(C::kOff + (s % C::KS) * C::img) + kbase;
-        asm volatile("" : "+v"(kb));  // (see pv: keeps the reads' offsets immediate)
+        PF4_OPAQUE_V(kb);  // (see pv: keeps the reads' offsets immediate)
         const lds_u8* img = (const lds_u8*)smem + kb;
         f16x8 ka[2][NK];
 #pragma unroll
@@ -293,7 +322,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     auto mask_reads = [&](int s, int rb, u32x2 (&mk)[2][4]) {
         if constexpr (HM) {
             uint32_t mb = (uint32_t)(C::mOff + (wave * C::MS + s % C::MS) * C::maskSlot + rb * (32 * 128));
-            asm volatile("" : "+s"(mb));
+            PF4_OPAQUE_S(mb);
             const lds_u8* slot = (const lds_u8*)smem + mb;
 #pragma unroll
             for (int t = 0; t < 2; t++) {
@@ -333,7 +362,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 }
             }
         }
-        tmax = xor32_pair(tmax, true) * cexp;
+        tmax = PF4_XOR32(tmax, true) * cexp;
         // deferred max (T13; rare after the first tiles): wave-uniform decision
         resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
         const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
@@ -351,7 +380,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             for (int e = 0; e < 8; e += 2) {
                 const float pa = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e], cexp, nm));
                 const float pb2 = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e + 1], cexp, nm));
-                la = add_f32(la, pa);  // (scalar: packed f32 adds cost more beside MFMAs)
+                la = add_f32(la, pa);
                 lb = add_f32(lb, pb2);
                 x[e] = (f16)pa;
                 x[e + 1] = (f16)pb2;
@@ -389,7 +418,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         // addresses, spilled to AGPRs -- and no offset folds into a read)
         uint32_t b0 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[0];
         uint32_t b1 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[1];
-        asm volatile("" : "+v"(b0), "+v"(b1));
+        PF4_OPAQUE_V2(b0, b1);
         lds_u8* const img0 = lsm + b0;
         lds_u8* const img1 = lsm + b1;
         u32x4 va[2][NDB];
@@ -441,12 +470,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             mask_reads(s, 0, mk0);
             qk(s, 1, s1);
             softmax(0, s0, mk0, p0, al0, rs0);
-            __builtin_amdgcn_sched_group_barrier(0x100, NK + (HM ? 8 : 0), 0);  // subtile 0's K operands, the mask
+            PF4_SGB(0x100, NK + (HM ? 8 : 0), 0);  // subtile 0's K operands, the mask
 #pragma unroll
             for (int i = 0; i < 2 * NK; i++) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // up to five VALU
-                if (i < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // subtile 1's K operands
+                PF4_SGB(0x008, 1, 0);  // one MFMA
+                PF4_SGB(0x002, 5, 0);  // up to five VALU
+                if (i < NK) PF4_SGB(0x100, 1, 0);  // subtile 1's K operands
             }
             __builtin_amdgcn_sched_barrier(0);
             rescale_o(0, rs0, al0);
@@ -456,12 +485,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             softmax(1, s1, mk1, p1, al1, rs1);
             // the mask and subtile 0's V^T reads, then per MFMA up to five VALU
             // and one of subtile 1's V^T reads
-            __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB + (HM ? 8 : 0), 0);
+            PF4_SGB(0x100, 4 * NDB + (HM ? 8 : 0), 0);
 #pragma unroll
             for (int i = 0; i < 4 * NDB; i++) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-                if (i < 4 * NDB) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                PF4_SGB(0x008, 1, 0);
+                PF4_SGB(0x002, 5, 0);
+                if (i < 4 * NDB) PF4_SGB(0x100, 1, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
             // ---- C: barrier (every wave is done with tile s's K and mask and
@@ -503,24 +532,24 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             qk(s, 1, s1);
             sexp(0, 0, us0, p0);
             sexp(0, 1, us0, p0);
-            __builtin_amdgcn_sched_group_barrier(0x100, NK + (HM ? 8 : 0), 0);
+            PF4_SGB(0x100, NK + (HM ? 8 : 0), 0);
 #pragma unroll
             for (int i = 0; i < 2 * NK; i++) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
-                if (i < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                PF4_SGB(0x008, 1, 0);
+                PF4_SGB(0x002, 7, 0);
+                if (i < NK) PF4_SGB(0x100, 1, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
             // ---- B: O0 += V_s^T . P0^T  ||  rb 1's scores and max, its first subtile's exponentials
             pv(s, 0, p0);
             smax(1, s1, mk1, us1, al1, rs1);
             sexp(1, 0, us1, p1);
-            __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB, 0);
+            PF4_SGB(0x100, 4 * NDB, 0);
 #pragma unroll
             for (int i = 0; i < 4 * NDB; i++) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 9, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                PF4_SGB(0x008, 1, 0);
+                PF4_SGB(0x002, 9, 0);
+                PF4_SGB(0x100, 1, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
             // ---- C: barrier (as SCHED 0), refill
@@ -540,24 +569,24 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             }
             sexp(1, 1, us1, p1);
             if constexpr (NX) {
-                __builtin_amdgcn_sched_group_barrier(0x100, NK + (HM ? 8 : 0), 0);
+                PF4_SGB(0x100, NK + (HM ? 8 : 0), 0);
 #pragma unroll
                 for (int i = 0; i < 2 * NK; i++) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-                    if (i < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    PF4_SGB(0x008, 1, 0);
+                    PF4_SGB(0x002, 4, 0);
+                    if (i < NK) PF4_SGB(0x100, 1, 0);
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
             // ---- C2: O1 += V_s^T . P1^T  ||  rb 0's scores and max of the next tile
             pv(s, 1, p1);
             if constexpr (NX) smax(0, s0, mk0, us0, al0, rs0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 4 * NDB, 0);
+            PF4_SGB(0x100, 4 * NDB, 0);
 #pragma unroll
             for (int i = 0; i < 4 * NDB; i++) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                PF4_SGB(0x008, 1, 0);
+                PF4_SGB(0x002, 6, 0);
+                PF4_SGB(0x100, 1, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
         };
@@ -573,7 +602,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     float* park = (float*)smem + wave * (kPf4RowsW * kStride);
 #pragma unroll
     for (int rb = 0; rb < 2; rb++) {
-        const float l_tot = xor32_pair(l2[rb].x + l2[rb].y, false);
+        const float l_tot = PF4_XOR32(l2[rb].x + l2[rb].y, false);
         const float inv = 1.0f / l_tot;  // fully masked row -> NaN like the reference
         float* pk = park + (32 * rb + c32) * kStride + 4 * h;
 #pragma unroll

@@ -37,3 +37,21 @@ __global__ void probe_early_copy(const uint8_t* p, uint32_t* out, uint32_t bytes
     reg_fence<kTagMaskWords>(v);
     out[threadIdx.x] = v.x + c;
 }
+
+// wait states the compiler cannot see (the checker's second audit): an asm
+// v_add_f32 reading a v_exp_f32 result the compiler placed right before it --
+// fattn_pf4.h's round-5 row sums -- and the same with the pad inside the asm
+__global__ void probe_trans_asm_use(const float* x, float* out) {
+    const float v = x[threadIdx.x];
+    const float e = __builtin_amdgcn_exp2f(v);
+    float r;
+    asm volatile("v_add_f32_e32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(e));
+    out[threadIdx.x] = r;
+}
+__global__ void probe_trans_asm_padded(const float* x, float* out) {
+    const float v = x[threadIdx.x];
+    const float e = __builtin_amdgcn_exp2f(v);
+    float r;
+    asm volatile("s_nop 0\n\tv_add_f32_e32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(e));
+    out[threadIdx.x] = r;
+}

@@ -10,6 +10,9 @@ translation unit of libfattn.so (`make isa`, the library's own flags).
 * The audit catches the hazard: a probe kernel with a deliberately injected
   early store and an early register copy of a pending load is flagged, the
   correct form of the same kernel is not.
+* Its second audit (asm wait states): an asm v_add_f32 that reads a v_exp_f32
+  result hipcc placed right before it is flagged; with the pad inside the asm
+  it is not.  The shipped ISA has none.
 """
 import os
 import subprocess
@@ -44,7 +47,7 @@ def test_shipped_isa_has_no_untracked_load_hazards(capsys):
     out = capsys.readouterr().out
     print(out[-4000:])
     assert rc == 0, out[-4000:]
-    assert "0 hazards" in out and "0 mismatches" in out
+    assert "0 hazards" in out and "0 mismatches" in out and "0 asm wait-state hazards" in out
     # the audit saw the loads it is about (the split kernel's Q / mask words)
     n_loads = int(out.split("functions in")[1].split(":")[1].split("untracked")[0])
     assert n_loads > 0
@@ -61,9 +64,16 @@ def test_audit_catches_injected_early_touch(tmp_path, capsys):
     by = {}
     for name, body in funcs.items():
         findings, loads, rets = ihc.check_function(name, body)
-        key = next(k for k in ("probe_clean", "probe_early_store", "probe_early_copy") if k in name)
-        by[key] = (findings, loads, rets)
-    assert set(by) == {"probe_clean", "probe_early_store", "probe_early_copy"}
+        key = next(k for k in ("probe_clean", "probe_early_store", "probe_early_copy", "probe_trans_asm_use",
+                               "probe_trans_asm_padded") if k in name)
+        by[key] = (findings, loads, rets, ihc.check_wait_states(name, body))
+    assert set(by) == {"probe_clean", "probe_early_store", "probe_early_copy", "probe_trans_asm_use",
+                       "probe_trans_asm_padded"}
+    ws = by["probe_trans_asm_use"][3]
+    assert ws and ws[0][0].mnem.startswith("v_exp") and ws[0][1].mnem.startswith("v_add"), ws
+    assert by["probe_trans_asm_padded"][3] == []
+    for k in ("probe_clean", "probe_early_store", "probe_early_copy"):
+        assert by[k][3] == [], k
     assert by["probe_clean"][0] == [] and by["probe_clean"][1] == 1 and by["probe_clean"][2] == 1
     store = by["probe_early_store"][0]
     assert store and any(ins.mnem.startswith("global_store") for ins, _, _ in store), store

@@ -23,6 +23,16 @@ May-analysis over the CFG of each kernel (labels and s_branch / s_cbranch_*
 edges), union at joins, to a fixpoint.  It also rejects any asm VMEM load with
 a VGPR destination that carries no UNTRACKED tag.
 
+Second audit (round 5): VALU wait states the compiler cannot see.  hipcc's
+hazard recognizer pads its own instructions, not the text of an asm
+statement, so an asm instruction that reads the result of a transcendental
+(v_exp/v_log/v_rcp/v_rsq/v_sqrt/v_sin/v_cos: 1 wait state before a VALU use),
+or a v_permlane*_swap that reads a VALU result (2 wait states), must carry its
+own padding.  Every such producer/consumer pair where either side is inside an
+asm statement is checked along straight-line code (a block and its
+fall-through), counting one wait state per instruction between and N + 1 per
+`s_nop N` (fattn_pf4.h's row sums once read a stale exponential this way).
+
 `--same-as LIB.so` additionally checks that the audited ISA is the shipped
 code: every function's instruction sequence (alignment nops aside) equals the
 disassembly of the gfx950 code objects inside the library.
@@ -247,6 +257,64 @@ def check_function(name, body):
     return list(findings.values()), loads, retires
 
 
+# ------------------------------------------------------------------ wait states around asm
+
+TRANS_RE = re.compile(r"^v_(exp|log|rcp|rsq|sqrt|sin|cos)(_legacy)?_f(16|32)(_e32|_e64)?$")
+
+
+def valu_dest_and_srcs(ins: Insn):
+    """(dest vregs, source vregs) of a VALU instruction (first operand = dest)."""
+    first, _, rest = ins.ops.partition(",")
+    return vregs(first), vregs(rest)
+
+
+def required_waits(prod: Insn, cons: Insn) -> int:
+    """Wait states `cons` needs after `prod` when it reads prod's result (0: none)."""
+    if not prod.mnem.startswith("v_") or prod.mnem.startswith("v_mfma") or prod.mnem.startswith("v_accvgpr"):
+        return 0
+    pd, _ = valu_dest_and_srcs(prod)
+    if cons.mnem.startswith("v_permlane") and "swap" in cons.mnem:
+        # both operands are read (and written)
+        if pd & vregs(cons.ops):
+            return 2
+        return 0
+    if TRANS_RE.match(prod.mnem) and cons.mnem.startswith("v_") and not TRANS_RE.match(cons.mnem):
+        _, cs = valu_dest_and_srcs(cons)
+        if pd & cs:
+            return 1
+    return 0
+
+
+def check_wait_states(name, body):
+    """Producer/consumer pairs with an asm side that lack their wait states."""
+    blocks, succ = build_blocks(body)
+    findings = []
+    for i, (_, insns) in enumerate(blocks):
+        seq = list(insns)
+        # straight-line continuation into the fall-through block
+        if insns and not (insns[-1].mnem.startswith("s_branch") or insns[-1].mnem == "s_endpgm") \
+                and i + 1 < len(blocks):
+            seq += blocks[i + 1][1][:4]
+        for a, prod in enumerate(insns):
+            if not prod.mnem.startswith("v_"):
+                continue
+            waits = 0
+            for cons in seq[a + 1:a + 6]:
+                need = required_waits(prod, cons)
+                if need and waits < need and (prod.in_asm or cons.in_asm):
+                    findings.append((prod, cons, need, waits))
+                if cons.mnem == "s_nop":
+                    try:
+                        waits += int(cons.ops.split()[0], 0) + 1
+                    except ValueError:
+                        waits += 1
+                else:
+                    waits += 1
+                if waits >= 2:
+                    break
+    return findings
+
+
 # ------------------------------------------------------------------ shipped-library comparison
 
 def code_objects(lib_path):
@@ -309,7 +377,7 @@ def main(argv=None):
     ap.add_argument("-q", action="store_true")
     args = ap.parse_args(argv)
     bad = 0
-    total_loads = total_ret = nfunc = 0
+    total_loads = total_ret = nfunc = nws = 0
     asm_seqs = {}
     for path in args.files:
         try:
@@ -327,6 +395,11 @@ def main(argv=None):
                 return 2
             total_loads += loads
             total_ret += rets
+            for prod, cons, need, got in check_wait_states(name, body):
+                bad += 1
+                nws += 1
+                print(f"WAITSTATE {os.path.basename(path)}:{cons.line} {name}: `{cons.text}` reads the result of "
+                      f"`{prod.text}` (line {prod.line}) after {got} of its {need} wait states (asm side unpadded)")
             for ins, reg, info in findings:
                 bad += 1
                 what = f"v{reg}" if reg is not None else info[0]
@@ -334,7 +407,7 @@ def main(argv=None):
                       f"(untracked load at line {info[1]}, tag {info[0]})")
     if not args.q:
         print(f"audited {nfunc} functions in {len(args.files)} files: {total_loads} untracked asm register loads, "
-              f"{total_ret} retiring waits, {bad} hazards")
+              f"{total_ret} retiring waits, {bad - nws} hazards; {nws} asm wait-state hazards")
     if args.same_as:
         import tempfile
         with tempfile.TemporaryDirectory() as td:
