@@ -203,7 +203,7 @@ def cpu_baseline_prefill(rows=256):
             "extrapolation": f"linear: x {NQ // rows} rows x {H} heads (not measured)"}
 
 
-def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5):
+def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5, D=128, H=32):
     """The MFMA-bound prefill shape of SURVEY.md §8d (n_q = N = 4096, 32 heads,
     head_dim 128, Q8_0 K/V, non-causal, an f16 mask of zeros -- "zero mask":
     every key visible; "random": U[-1,1) like kernel_test.h:48; "causal": 0 on
@@ -211,10 +211,11 @@ def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5):
     graph, HIP events around the replay on the launch stream.  Two rotated KV
     caches (compute-bound: the cache state barely matters).  The mask pre-pass
     (pf_mask_flags_kernel: live / all-zero block flags) is inside the timed
-    region."""
+    region.  (D / H: other head dims for tools/ab_prefill.py; the bench line
+    is D = 128, H = 32.)"""
     import torch
     import fattn
-    D, H, N, NQ, R = 128, 32, 4096, 4096, 2
+    N, NQ, R = 4096, 4096, 2
 
     typ = fattn.TYPE_NAMES[kvn]
     g = torch.Generator(device=dev)
@@ -568,12 +569,23 @@ def run_decode(args, dev, shape, rank=0, world=1, mode="head", dist_on=False):
                 with torch.cuda.graph(ggraph, stream=gs):
                     for i in range(K):
                         gstep(i)
-                with torch.cuda.stream(gs):
-                    ggraph.replay()  # untimed warm replay
                 torch.cuda.synchronize()
             except Exception as e:  # noqa: BLE001 -- any capture failure: time the eager form instead
                 graph_err = f"{type(e).__name__}: {e}"[:400]
                 ggraph = None
+                torch.cuda.synchronize()
+            # every rank replays, or none does: a replay's collectives on some
+            # ranks only would wait forever for the others (capture records
+            # them without communicating, so a failed capture left no
+            # collective half-done)
+            ok = torch.tensor([1 if ggraph is not None else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0 and ggraph is not None:
+                graph_err = "capture failed on another rank"
+                ggraph = None
+            if ggraph is not None:
+                with torch.cuda.stream(gs):
+                    ggraph.replay()  # untimed warm replay
                 torch.cuda.synchronize()
         # eager form
         dist.barrier()

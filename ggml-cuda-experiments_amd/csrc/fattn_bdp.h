@@ -128,9 +128,52 @@ __device__ __forceinline__ void bdp_issue(const StepSrc& rs, int n0, uint32_t ld
 // next raw tile, which stalls on a full memory pipeline (profiles/r04_c), so
 // their latency runs under that stall; bdp_dequant_store converts and writes.
 constexpr int kBdpHpw = 2;  // half-blocks per build wave, at most (D <= 128)
+// Image swizzles of this kernel's dequantised tiles (tools/lds_model_bdp.py):
+// K rows (32 B) hold their two 16-B halves swapped when bit 2 ^ bit 3 of the
+// key is set, V rows (64 B) hold chunk c at c ^ ((key >> 1) & 3).  Both make
+// the build waves' b128 image writes (8 consecutive keys per bank cycle) AND
+// the compute waves' operand reads conflict-free; fattn_bd.h / fattn_pf.h's
+// swizzles (bit 3; key >> 2) left the writes 2-way conflicted (27 % + 27 % of
+// the modelled excess cycles; round-4 counters: 36 % of LDS-active cycles in
+// conflicts).  FATTN_BDP_OLD_SWZ (A/B builds): the old ones.
+#ifdef FATTN_BDP_OLD_SWZ
+__host__ __device__ constexpr int bdp_kswz(int key) { return (key >> 3) & 1; }
+__host__ __device__ constexpr int bdp_vswz(int key) { return (key >> 2) & 3; }
+#else
+__host__ __device__ constexpr int bdp_kswz(int key) { return ((key >> 2) ^ (key >> 3)) & 1; }
+__host__ __device__ constexpr int bdp_vswz(int key) { return (key >> 1) & 3; }
+#endif
 struct BdpRaw {
     HalfRaw k[kBdpHpw], v[kBdpHpw];
 };
+// FATTN_BDP_RAW64 (A/B builds): a half block's raw words by three ds_read_b64
+// from the 8-B-aligned dword pair at or below the first qs byte (and the scale
+// by one b64), the dword window then picked by selects: rows of 136 / 72 B are
+// 34 / 18 dwords apart, so 32 lanes' b32 reads hit every bank twice, their
+// b64 reads each bank once (tools/lds_model_bdp.py: 71 % of the modelled
+// excess after the image swizzles)
+template <int KT, int D>
+__device__ __forceinline__ HalfRaw bdp_half_load64(const uint8_t* raw, int row, int b, int h) {
+    constexpr int RB = row_bytes<KT, D>();
+    constexpr int BB = TypeInfo<KT>::block_bytes;
+    HalfRaw r;
+    r.blk = row * RB + BB * b;
+    const uint32_t q0 = r.blk + 2 + (KT == FATTN_TYPE_Q8_0 ? 16 * h : 0);
+    const uint32_t q8 = q0 & ~7u;
+    uint32_t w[6];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const u32x2 x = *(const u32x2*)(raw + q8 + 8 * j);
+        w[2 * j] = x.x;
+        w[2 * j + 1] = x.y;
+    }
+    const bool up = (q0 & 4u) != 0;
+#pragma unroll
+    for (int j = 0; j < 5; j++) r.u[j] = up ? w[j + 1] : w[j];
+    const u32x2 sc = *(const u32x2*)(raw + (r.blk & ~7u));
+    r.dw = (r.blk & 4u) ? sc.y : sc.x;
+    return r;
+}
 template <int KT, int D>
 __device__ __forceinline__ BdpRaw bdp_dequant_load(const uint8_t* raw, int bw, int lane) {
     using C = BdpCfg<KT, D>;
@@ -140,8 +183,13 @@ __device__ __forceinline__ BdpRaw bdp_dequant_load(const uint8_t* raw, int bw, i
     for (int i = 0; i < (D / 16 + 3) / 4; i++) {
         const int hb = bw + 4 * i;
         if (hb >= D / 16) break;  // wave-uniform
+#ifdef FATTN_BDP_RAW64
+        r.k[i] = bdp_half_load64<KT, D>(raw, lane, hb >> 1, hb & 1);
+        r.v[i] = bdp_half_load64<KT, D>(raw + C::kvRaw, lane, hb >> 1, hb & 1);
+#else
         r.k[i] = dequant_half_load<KT, D>(raw, lane, hb >> 1, hb & 1);
         r.v[i] = dequant_half_load<KT, D>(raw + C::kvRaw, lane, hb >> 1, hb & 1);
+#endif
     }
     return r;
 }
@@ -150,7 +198,7 @@ __device__ __forceinline__ void bdp_dequant_store(const BdpRaw& r, uint8_t* k16,
 #ifdef FATTN_MQ_NODEQ
     return;  // diagnostic build only
 #endif
-    const int sk = (lane >> 3) & 1, sv = (lane >> 2) & 3;
+    const int sk = bdp_kswz(lane), sv = bdp_vswz(lane);
 #pragma unroll
     for (int i = 0; i < (D / 16 + 3) / 4; i++) {
         const int hb = bw + 4 * i;
@@ -341,15 +389,17 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
     }
     const float log2e = 1.4426950408889634f;
     const float scale = a.scale;
-    // per-lane K read base (key 32 kh + c32, half h; 16-B halves swapped on keys
-    // with bit 3 set) and V^T gather bases (fattn_bd.h, 64-key images)
-    const uint32_t kbase = kh * 1024 + c32 * 32 + ((h ^ ((c32 >> 3) & 1)) * 16);
+    // per-lane K read base (key 32 kh + c32, half h; halves swapped per
+    // bdp_kswz) and V^T gather bases (fattn_bd.h's gather, 64-key images,
+    // chunks swizzled per bdp_vswz: keys 32 kh + 16 q + row, the first two
+    // terms leave bits 1-2 alone)
+    const uint32_t kbase = kh * 1024 + c32 * 32 + ((h ^ bdp_kswz(c32)) * 16);
     const int gi = lane & 15, dh = (lane >> 4) & 1;
     uint32_t vbase[2];
 #pragma unroll
     for (int e = 0; e < 2; e++) {
         const int row = 8 * e + 4 * h + (gi >> 2);
-        const int ch = (2 * dh + ((gi & 3) >> 1)) ^ ((h + 2 * e) & 3);
+        const int ch = (2 * dh + ((gi & 3) >> 1)) ^ bdp_vswz(row);
         vbase[e] = C::img + kh * 2048 + row * 64 + ch * 16 + (gi & 1) * 8;
     }
 

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--mask", default="zero", choices=["zero", "random", "causal", "none"])
     ap.add_argument("--variant", action="append", default=[], help="name:OPT=val,... (OPT without OPT_)")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--D", type=int, default=128)
+    ap.add_argument("--H", type=int, default=32)
     args = ap.parse_args()
     import torch
     import fattn
@@ -40,12 +42,12 @@ def main():
     for r in range(args.rounds):
         for name, od in variants:
             with fattn.options(od):
-                m = prefill_measure(dev, hip, evs, args.kv, args.mask)
+                m = prefill_measure(dev, hip, evs, args.kv, args.mask, D=args.D, H=args.H)
             res[name].append(m["kernel_ms_avg"] * 1e3)
             print(f"round {r} {name:12s} {m['kernel_ms_avg'] * 1e3:8.1f} us  frac {m['roofline']['frac']:.4f}  "
                   f"{m['kernel']}", flush=True)
-    flops = 4 * 4096 * 4096 * 128 * 32 if args.mask != "causal" else 4 * (4096 * 4097 // 2) * 128 * 32
-    print(f"# prefill kv {args.kv} mask {args.mask}")
+    flops = 4 * (4096 * 4096 if args.mask != "causal" else 4096 * 4097 // 2) * args.D * args.H
+    print(f"# prefill kv {args.kv} mask {args.mask} D {args.D} H {args.H}")
     for name, v in res.items():
         med = statistics.median(v)
         print(f"{name:12s} median {med:8.1f} us  min {min(v):8.1f}  max {max(v):8.1f}  "
