@@ -598,7 +598,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
                            : pf_lds(std::integral_constant<int, 128>());
         // f16 rows (native or staged) at D = 128: the one-wave-per-SIMD body
         pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && g_opt_pf_form >= 2;
-        pl.pf4_sched = g_opt_pf_form == 3 ? 1 : 0;
+        pl.pf4_sched = g_opt_pf_form >= 3 ? g_opt_pf_form - 2 : 0;
         if (pl.pf4) pl.lds = Pf4Cfg<128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
@@ -712,7 +712,7 @@ int fattn_set_option(int option, int value) {
             g_opt_split_xcd = value;
             return FATTN_OK;
         case FATTN_OPT_PF_FORM:
-            if (value < 0 || value > 3) return FATTN_ERR_INVALID_ARG;
+            if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_form = value;
             return FATTN_OK;
         case FATTN_OPT_PF_STAGE:
@@ -780,7 +780,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
                       pl.pf_stage ? (pl.stage_kt == FATTN_TYPE_Q8_0 ? "kv_stage_f16<q8_0> + " : "kv_stage_f16<q4_0> + ")
                                   : "",
                       pl.pf_flags ? "pf_mask_flags_kernel + " : "",
-                      pl.pf4 ? (pl.pf4_sched ? "fattn_pf4_kernel(sched1)" : "fattn_pf4_kernel") : "fattn_pf_kernel",
+                      pl.pf4 ? (pl.pf4_sched == 2 ? "fattn_pf4_kernel(pipelined)" : pl.pf4_sched ? "fattn_pf4_kernel(sched1)" : "fattn_pf4_kernel") : "fattn_pf_kernel",
                       tn(pl.kt), pl.D, hm);
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,

@@ -146,34 +146,6 @@ __host__ __device__ constexpr int bdp_vswz(int key) { return (key >> 1) & 3; }
 struct BdpRaw {
     HalfRaw k[kBdpHpw], v[kBdpHpw];
 };
-// FATTN_BDP_RAW64 (A/B builds): a half block's raw words by three ds_read_b64
-// from the 8-B-aligned dword pair at or below the first qs byte (and the scale
-// by one b64), the dword window then picked by selects: rows of 136 / 72 B are
-// 34 / 18 dwords apart, so 32 lanes' b32 reads hit every bank twice, their
-// b64 reads each bank once (tools/lds_model_bdp.py: 71 % of the modelled
-// excess after the image swizzles)
-template <int KT, int D>
-__device__ __forceinline__ HalfRaw bdp_half_load64(const uint8_t* raw, int row, int b, int h) {
-    constexpr int RB = row_bytes<KT, D>();
-    constexpr int BB = TypeInfo<KT>::block_bytes;
-    HalfRaw r;
-    r.blk = row * RB + BB * b;
-    const uint32_t q0 = r.blk + 2 + (KT == FATTN_TYPE_Q8_0 ? 16 * h : 0);
-    const uint32_t q8 = q0 & ~7u;
-    uint32_t w[6];
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const u32x2 x = *(const u32x2*)(raw + q8 + 8 * j);
-        w[2 * j] = x.x;
-        w[2 * j + 1] = x.y;
-    }
-    const bool up = (q0 & 4u) != 0;
-#pragma unroll
-    for (int j = 0; j < 5; j++) r.u[j] = up ? w[j + 1] : w[j];
-    const u32x2 sc = *(const u32x2*)(raw + (r.blk & ~7u));
-    r.dw = (r.blk & 4u) ? sc.y : sc.x;
-    return r;
-}
 template <int KT, int D>
 __device__ __forceinline__ BdpRaw bdp_dequant_load(const uint8_t* raw, int bw, int lane) {
     using C = BdpCfg<KT, D>;
@@ -183,13 +155,8 @@ __device__ __forceinline__ BdpRaw bdp_dequant_load(const uint8_t* raw, int bw, i
     for (int i = 0; i < (D / 16 + 3) / 4; i++) {
         const int hb = bw + 4 * i;
         if (hb >= D / 16) break;  // wave-uniform
-#ifdef FATTN_BDP_RAW64
-        r.k[i] = bdp_half_load64<KT, D>(raw, lane, hb >> 1, hb & 1);
-        r.v[i] = bdp_half_load64<KT, D>(raw + C::kvRaw, lane, hb >> 1, hb & 1);
-#else
         r.k[i] = dequant_half_load<KT, D>(raw, lane, hb >> 1, hb & 1);
         r.v[i] = dequant_half_load<KT, D>(raw + C::kvRaw, lane, hb >> 1, hb & 1);
-#endif
     }
     return r;
 }

@@ -99,7 +99,10 @@ int launch_split_e(const Plan& pl, hipStream_t st, const Events& ev) {
             // as few load slots per lane as the chunk count allows (the slots
             // past it still cost issue cycles) -- unless they merge in-kernel (2)
             if (pl.a.merge_launch == 1) {
-                const dim3 g(kRows / 4, pl.grid.y, pl.grid.z);
+                // one wave per packed row a tile can hold (config 4's 4-row GQA
+                // tiles: one workgroup per tile, not four)
+                const int rows = pl.a.QPT * pl.a.R < kRows ? pl.a.QPT * pl.a.R : kRows;
+                const dim3 g((unsigned)((rows + 3) / 4), pl.grid.y, pl.grid.z);
                 const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
                 if (need <= 2) hipLaunchKernelGGL((fattn_merge_kernel<D, 2>), g, dim3(256), 0, st, pl.a);
                 else if (need <= 4) hipLaunchKernelGGL((fattn_merge_kernel<D, 4>), g, dim3(256), 0, st, pl.a);
@@ -184,7 +187,9 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     const void* main_kern = (const void*)kern;
     if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
         if (pl.pf4)
-            main_kern = pl.pf4_sched ? (const void*)fattn_pf4_kernel<D, HM, 1> : (const void*)fattn_pf4_kernel<D, HM, 0>;
+            main_kern = pl.pf4_sched == 2 ? (const void*)fattn_pf4_kernel<D, HM, 2>
+                        : pl.pf4_sched    ? (const void*)fattn_pf4_kernel<D, HM, 1>
+                                          : (const void*)fattn_pf4_kernel<D, HM, 0>;
     }
     return launch_kernel(main_kern, pl, st, ev, [&] {
         if constexpr (KT == FATTN_TYPE_F16 && D % QK == 0) {
@@ -204,7 +209,9 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
                                pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
         if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
             if (pl.pf4) {
-                if (pl.pf4_sched)
+                if (pl.pf4_sched == 2)
+                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 2>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
+                else if (pl.pf4_sched)
                     hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 1>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
                 else
                     hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 0>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);

@@ -75,6 +75,65 @@ __device__ __forceinline__ float add_f32(float x, float y) {
     return x + y;
 #endif
 }
+// O *= alpha on one accumulator block where it lives (AGPRs), in one asm
+// statement: v_accvgpr_read, v_mul_f32, v_accvgpr_write per element, inside
+// the rare rescale branch.  Written in C the multiply needs O in VGPRs, and
+// hipcc hoisted those AGPR -> VGPR copies (128 per tile) out of the branch onto
+// every tile.  The trailing s_nop covers the accumulator-write -> MFMA-read
+// wait states the compiler cannot see inside the asm (the next P.V MFMAs read
+// these registers as srcC).
+__device__ __forceinline__ void scale_acc16(f32x16& o, float alpha) {
+    float t;
+    asm volatile(
+        "v_accvgpr_read_b32 %16, %0\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %0, %16\n\t"
+        "v_accvgpr_read_b32 %16, %1\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %1, %16\n\t"
+        "v_accvgpr_read_b32 %16, %2\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %2, %16\n\t"
+        "v_accvgpr_read_b32 %16, %3\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %3, %16\n\t"
+        "v_accvgpr_read_b32 %16, %4\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %4, %16\n\t"
+        "v_accvgpr_read_b32 %16, %5\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %5, %16\n\t"
+        "v_accvgpr_read_b32 %16, %6\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %6, %16\n\t"
+        "v_accvgpr_read_b32 %16, %7\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %7, %16\n\t"
+        "v_accvgpr_read_b32 %16, %8\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %8, %16\n\t"
+        "v_accvgpr_read_b32 %16, %9\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %9, %16\n\t"
+        "v_accvgpr_read_b32 %16, %10\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %10, %16\n\t"
+        "v_accvgpr_read_b32 %16, %11\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %11, %16\n\t"
+        "v_accvgpr_read_b32 %16, %12\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %12, %16\n\t"
+        "v_accvgpr_read_b32 %16, %13\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %13, %16\n\t"
+        "v_accvgpr_read_b32 %16, %14\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %14, %16\n\t"
+        "v_accvgpr_read_b32 %16, %15\n\tv_mul_f32_e32 %16, %17, %16\n\tv_accvgpr_write_b32 %15, %16\n\t"
+        "s_nop 7"
+        : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]), "+a"(o[4]), "+a"(o[5]), "+a"(o[6]), "+a"(o[7]),
+          "+a"(o[8]), "+a"(o[9]), "+a"(o[10]), "+a"(o[11]), "+a"(o[12]), "+a"(o[13]), "+a"(o[14]), "+a"(o[15]),
+          "=&v"(t)
+        : "v"(alpha));
+}
+// registers through an empty volatile asm: code that reads them cannot move
+// above the asm (pins a phase's VALU below the branches at its start)
+__device__ __forceinline__ void pin16(float (&x)[16]) {
+    asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
+                 "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]),
+                 "+v"(x[14]), "+v"(x[15]));
+}
+__device__ __forceinline__ void pin16(f32x16& x) {
+    asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
+                 "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]),
+                 "+v"(x[14]), "+v"(x[15]));
+}
+
+// (P fragments of one row block: pinned at the end of the phase that made them,
+// so hipcc's machine sinking cannot move their exponentials next to the P.V
+// that uses them, into the next phase's block)
+__device__ __forceinline__ void pin_p(f16x8 (&p)[2][2]) {
+    u32x4 a = __builtin_bit_cast(u32x4, p[0][0]), b = __builtin_bit_cast(u32x4, p[0][1]);
+    u32x4 c = __builtin_bit_cast(u32x4, p[1][0]), d = __builtin_bit_cast(u32x4, p[1][1]);
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w), "+v"(b.x), "+v"(b.y), "+v"(b.z), "+v"(b.w),
+                 "+v"(c.x), "+v"(c.y), "+v"(c.z), "+v"(c.w), "+v"(d.x), "+v"(d.y), "+v"(d.z), "+v"(d.w));
+    p[0][0] = __builtin_bit_cast(f16x8, a);
+    p[0][1] = __builtin_bit_cast(f16x8, b);
+    p[1][0] = __builtin_bit_cast(f16x8, c);
+    p[1][1] = __builtin_bit_cast(f16x8, d);
+}
+
 // diagnostic builds only: without the scheduling groups / the opaque bases
 #ifdef FATTN_PF4_NO_SGB
 #define PF4_SGB(m, n, id) ((void)0)
@@ -272,12 +331,15 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     // ---- prologue: mask 0, V 0, K 0, mask 1, V 1, K 1, K 2 (the steady
     // state's issue order -- mask s+2, V s+2, K s+3 at C_s -- so that a
     // counted wait can leave the youngest K in flight)
-    for (int s = 0; s < 2 && s < nt; s++) {
-        m_issue(s);
-        v_issue(s);
-        k_issue(s);
+    // (SCHED 2: its own order, below)
+    if constexpr (SCHED != 2) {
+        for (int s = 0; s < 2 && s < nt; s++) {
+            m_issue(s);
+            v_issue(s);
+            k_issue(s);
+        }
+        if (nt > 2) k_issue(2);
     }
-    if (nt > 2) k_issue(2);
 
     const float log2e = 1.4426950408889634f;
     const float scale = a.scale_log2 / log2e;
@@ -446,7 +508,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
 
     // ---- S0 of tile 0 (the loop's C phase computes it for the next tile):
     // K 0 landed (mask 0 and V 0 before it; mask 1, V 1, K 1, K 2 may fly)
-    if (nt > 0) {
+    if (SCHED != 2 && nt > 0) {
         const int later = (HM && nt > 1 ? C::NMI : 0) + (nt > 1 ? 2 * C::NKI : 0) + (nt > 2 ? C::NKI : 0);
         static_assert(C::NMI == 2 * C::NKI, "the prologue's wait counts: 0, 8, 12, 16, 20");
         switch (__builtin_amdgcn_readfirstlane(later)) {  // (wave-uniform)
@@ -511,6 +573,267 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             rescale_o(1, rs1, al1);
             pv(s, 1, p1);
             if (s + 1 < nt) qk(s + 1, 0, s0);
+        }
+    } else if constexpr (SCHED == 2) {
+        // the pipelined schedule (cdna_hip_programming.md 'Fused attention
+        // prefill', 4-wave structure): per tile two phases of 32 MFMAs,
+        //   A_j: S_j = K_j . Q^T for both row blocks  ||  rb 1's exponentials
+        //        of tile j-1, rb 1's scores / max / rescale decision of tile j;
+        //   B_j: O += V_{j-1}^T . P_{j-1}^T for both row blocks (each V^T
+        //        operand read once, used twice)  ||  rb 0's scores / max /
+        //        decision and exponentials of tile j;
+        // so both phases carry one row block's exponentials (one v_exp per
+        // MFMA gap).  The O rescale a decision of tile j-1 asks for is applied
+        // at the start of A_j: after P_{j-2}.V (B_{j-1}), before P_{j-1}.V --
+        // the 8-wave body's order of operations on O and l, so the same bits.
+        // Rings: K_{j+3} and V_{j+1} are issued at B_j (after its barrier)
+        // into the slots of K_j (read in A_j) and V_{j-2} (B_{j-1}); the
+        // wave's mask j+2 after its reads of mask j.  A_j's counted wait leaves
+        // B_{j-1}'s issues in flight: K_{j+1}, V_{j-1} and mask j have landed
+        // (this wave's pieces; B_j's barrier then covers everyone's).
+        static_assert(C::NKI == 4 && C::NMI == 8, "the wait counts below are multiples of 4");
+        auto wait_dyn = [&](int n) {  // s_waitcnt vmcnt(n), n a multiple of 4 in [0, 28] (wave-uniform)
+            switch (__builtin_amdgcn_readfirstlane(n)) {
+                case 28: wait_vmcnt_c<28>(); break;
+                case 24: wait_vmcnt_c<24>(); break;
+                case 20: wait_vmcnt_c<20>(); break;
+                case 16: wait_vmcnt_c<16>(); break;
+                case 12: wait_vmcnt_c<12>(); break;
+                case 8: wait_vmcnt_c<8>(); break;
+                case 4: wait_vmcnt_c<4>(); break;
+                default: wait_vmcnt_c<0>(); break;
+            }
+        };
+        constexpr int MI = HM ? C::NMI : 0;
+        // prologue: K 0 | K 1, mask 0 | K 2, V 0, mask 1 (the last two groups as
+        // the steady state's B_{-2} and B_{-1})
+        if (nt > 0) k_issue(0);
+        if (nt > 1) k_issue(1);
+        if (nt > 0) m_issue(0);
+        if (nt > 2) k_issue(2);
+        if (nt > 0) v_issue(0);
+        if (nt > 1) m_issue(1);
+        // O_rb^T += V_s^T . P_rb^T for both row blocks, each V^T operand read
+        // once; per accumulator the 8-wave body's order (t, q)
+        auto pv2 = [&](int s, const f16x8 (&pa)[2][2], const f16x8 (&pb)[2][2]) {
+            uint32_t b0 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[0];
+            uint32_t b1 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[1];
+            PF4_OPAQUE_V2(b0, b1);
+            lds_u8* const img0 = lsm + b0;
+            lds_u8* const img1 = lsm + b1;
+            // every V^T operand of the tile first (64 VGPRs), so that no MFMA
+            // of the phase waits for its own read
+            f16x8 va[2][2][NDB];
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+#pragma unroll
+                    for (int db = 0; db < NDB; db++) {
+                        const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
+                        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img1 + off));
+                        const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                        va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+#pragma unroll
+                    for (int db = 0; db < NDB; db++) {
+                        o[0][db] = mfma32(va[t][q][db], pa[t][q], o[0][db]);
+                        o[1][db] = mfma32(va[t][q][db], pb[t][q], o[1][db]);
+                    }
+                }
+            }
+        };
+        // K_j's operands, read once per tile at the start of A_j for both row blocks
+        f16x8 kr[2][NK];
+        auto k_read = [&](int s) {
+            uint32_t kb = (uint32_t)(C::kOff + (s % C::KS) * C::img) + kbase;
+            PF4_OPAQUE_V(kb);
+            const lds_u8* img = (const lds_u8*)smem + kb;
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+#pragma unroll
+                for (int kk = 0; kk < NK; kk++)
+                    kr[t][kk] = *(const __attribute__((address_space(3))) f16x8*)(img + kk * (kPfKeys * 32) + t * 1024);
+            }
+        };
+        if (nt > 0) {
+            // K 0 landed: everything issued after it may fly
+            wait_dyn((nt > 1 ? C::NKI : 0) + MI + (nt > 2 ? C::NKI : 0) + C::NKI + (nt > 1 ? MI : 0));
+            __syncthreads();
+        }
+        float us0[2][16], us1[2][16];
+        float al0 = 1.0f, al1 = 1.0f;
+        bool rs0 = false, rs1 = false;
+        f16x8 p0[2][2], p1[2][2];
+        // (the first tile without rb 1's previous exponentials and without a
+        // P.V: a compile-time flag, so that no branch splits a phase -- a
+        // phase must stay one basic block for its VALU to sit between its MFMAs)
+        // O rescale (a decision of tile j-1: rb 0's made in B_{j-1}, rb 1's in
+        // A_{j-1}, kept as pending through A_j) at the start of B_j, after its
+        // barrier: after P_{j-2}.V, before P_{j-1}.V; in AGPRs (scale_acc16)
+        bool pr1 = false;
+        float pa1 = 1.0f;
+        auto rescale_acc = [&](int rb, bool resc, float alpha) {
+            if (__builtin_expect(resc, 0)) {
+#pragma unroll
+                for (int db = 0; db < NDB; db++) scale_acc16(o[rb][db], alpha);
+            }
+        };
+        // The phases are written as 32 explicit (MFMA, vector piece) steps, each
+        // its own scheduling region (sched_barrier): hipcc's scheduling groups
+        // left the exponentials behind the MFMA runs (in-order issue then
+        // serialises them).  A vector piece = two elements of one row block:
+        // scores + running max (smax_piece) or exponentials + row sums + f16
+        // pair (sexp_piece) -- the same operations in the same order per row
+        // as smax / sexp, so the same bits.
+        auto smax_piece = [&](const f32x16 (&st)[2], const u32x2 (&mk)[2][4], float (&us)[2][16], float& tmax, int pc) {
+            const int t = pc >> 3, k0 = 2 * (pc & 7);
+#pragma unroll
+            for (int k = k0; k < k0 + 2; k++) {
+                float x = st[t][k];
+                if constexpr (HM) {
+                    const int u = k >> 2, e = k & 3;
+                    const f16x2 mm = as_h2(e < 2 ? mk[t][u].x : mk[t][u].y);
+                    x = fmaf(x, scale, (float)(e & 1 ? mm.y : mm.x));
+                }
+                us[t][k] = x;
+                tmax = fmaxf(tmax, x);
+            }
+        };
+        auto smax_final = [&](int rb, float tmax, float& alpha, bool& resc) {
+            tmax = PF4_XOR32(tmax, true) * cexp;
+            resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
+            const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
+            alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
+            m_run[rb] = m_new;
+            l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
+        };
+        auto sexp_piece = [&](const float (&us)[2][16], f16x8 (&pb)[2][2], float nm, float& la, float& lb, int pc) {
+            const int t = pc >> 3, k = 2 * (pc & 7);
+            const float pa = __builtin_amdgcn_exp2f(fmaf(us[t][k], cexp, nm));
+            const float pq = __builtin_amdgcn_exp2f(fmaf(us[t][k + 1], cexp, nm));
+            la = add_f32(la, pa);
+            lb = add_f32(lb, pq);
+            pb[t][k >> 3][k & 7] = (f16)pa;
+            pb[t][k >> 3][(k & 7) + 1] = (f16)pq;
+        };
+        auto iter = [&](int j, auto first) {
+            constexpr bool F = decltype(first)::value;
+            // ---- A_j: S_j for rb 1 (steps 0-15) and rb 0 (16-31); rb 1's
+            // exponentials of tile j-1 beside steps 0-15, its scores and max of
+            // tile j beside 16-31 (its S chains done by then)
+            wait_dyn((j + 2 < nt ? C::NKI : 0) + C::NKI + (j + 1 < nt ? MI : 0));
+            pr1 = rs1;  // rb 1's decision of tile j-1, applied at B_j
+            pa1 = al1;
+            u32x2 mk1[2][4], mk0[2][4];
+            k_read(j);
+            mask_reads(j, 1, mk1);
+            mask_reads(j, 0, mk0);  // (rb 0's, for B_j: this wave's slot, no barrier needed)
+            const float nm1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];
+            float la1 = l2[1].x, lb1 = l2[1].y, tmax1 = kNegInf;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 32; i++) {
+                const int t = (i >> 3) & 1, kk = i & 7;
+                if (i < 16) {
+                    if (kk == 0) s1[t] = f32x16{};
+                    s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
+                    if constexpr (!F) sexp_piece(us1, p1, nm1, la1, lb1, i);
+                } else {
+                    if (kk == 0) s0[t] = f32x16{};
+                    s0[t] = mfma32(kr[t][kk], qop[0][kk], s0[t]);
+                    if (i >= 18) smax_piece(s1, mk1, us1, tmax1, i - 18);  // (S1's last chain lands ~2 steps late)
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            smax_piece(s1, mk1, us1, tmax1, 14);
+            smax_piece(s1, mk1, us1, tmax1, 15);
+            if constexpr (!F) l2[1] = f32x2{la1, lb1};
+            smax_final(1, tmax1, al1, rs1);
+            // (the phase's results pinned here: hipcc's machine sinking would
+            // otherwise move their exponentials next to their uses in B)
+            if constexpr (!F) pin_p(p1);
+            pin16(us1[0]);
+            pin16(us1[1]);
+            // ---- B_j: P_{j-1}.V for both row blocks (each V^T operand read
+            // once); rb 0's scores and max of tile j beside steps 0-15, its
+            // exponentials beside 16-31
+            __syncthreads();
+            if (j + 3 < nt) k_issue(j + 3);
+            if (j + 1 < nt) v_issue(j + 1);
+            rescale_acc(0, rs0, al0);  // decisions of tile j-1
+            rescale_acc(1, pr1, pa1);
+            f16x8 va[2][2][NDB];
+            if constexpr (!F) {
+                uint32_t b0 = (uint32_t)(C::vOff + ((j - 1) % C::VS) * C::img) + vbase[0];
+                uint32_t b1 = (uint32_t)(C::vOff + ((j - 1) % C::VS) * C::img) + vbase[1];
+                PF4_OPAQUE_V2(b0, b1);
+                lds_u8* const img0 = lsm + b0;
+                lds_u8* const img1 = lsm + b1;
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+#pragma unroll
+                        for (int db = 0; db < NDB; db++) {
+                            const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
+                            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img1 + off));
+                            const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                            va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
+                        }
+                    }
+                }
+            }
+            float tmax0 = kNegInf, nm0 = 0.0f, la0 = 0.0f, lb0 = 0.0f;
+            f16x8 p0n[2][2];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 32; i++) {
+                if constexpr (!F) {
+                    const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
+                    o[rb][db] = mfma32(va[t][q][db], rb ? p1[t][q] : p0[t][q], o[rb][db]);
+                }
+                if (i < 16) smax_piece(s0, mk0, us0, tmax0, i);
+                if (i == 16) {
+                    smax_final(0, tmax0, al0, rs0);
+                    nm0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
+                    la0 = l2[0].x;
+                    lb0 = l2[0].y;
+                }
+                if (i >= 16) sexp_piece(us0, p0n, nm0, la0, lb0, i - 16);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            l2[0] = f32x2{la0, lb0};
+            pin_p(p0n);
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+#pragma unroll
+                for (int q = 0; q < 2; q++) p0[t][q] = p0n[t][q];
+            }
+            if (HM && j + 2 < nt) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's mask j has been read
+                m_issue(j + 2);
+            }
+        };
+        if (nt > 0) iter(0, std::true_type());
+        for (int j = 1; j < nt; j++) iter(j, std::false_type());
+        if (nt > 0) {
+            // ---- A_nt, B_nt: rb 1's exponentials of the last tile, its P.V
+            wait_vmcnt_c<0>();
+            sexp(1, 0, us1, p1);
+            sexp(1, 1, us1, p1);
+            __syncthreads();  // every wave's pieces of V nt-1 landed
+            rescale_acc(0, rs0, al0);
+            rescale_acc(1, rs1, al1);
+            pv2(nt - 1, p0, p1);
         }
     } else {
         // the rebalanced schedule (see the kernel's comment)

@@ -630,12 +630,14 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture(params=[(0, 1), (1, 1), (0, 2), (0, 3)], ids=["staged", "inkernel_deq", "staged_pf4", "staged_pf4s1"])
+@pytest.fixture(params=[(0, 1), (1, 1), (0, 2), (0, 3), (0, 4)],
+                ids=["staged", "inkernel_deq", "staged_pf4", "staged_pf4s1", "staged_pf4p"])
 def pf_force(request):
     """The prefill kernels on every eligible problem: Q8_0 / Q4_0 K/V staged
     to f16 first (the default) or dequantised inside the kernel
     (FATTN_OPT_PF_STAGE = 1); the f16 body in its 8-wave form (fattn_pf.h)
-    or one wave per SIMD (fattn_pf4.h, D = 128; FATTN_OPT_PF_FORM = 2)."""
+    or one wave per SIMD (fattn_pf4.h, D = 128; FATTN_OPT_PF_FORM = 2, 3 and
+    the pipelined 4)."""
     stage, form = request.param
     fattn.set_option(fattn.OPT_PF, 2)
     fattn.set_option(fattn.OPT_PF_STAGE, stage)
@@ -665,12 +667,13 @@ def test_pf4_bit_identical_to_pf(dev, case):
     outs = {}
     fattn.set_option(fattn.OPT_PF, 2)
     try:
-        for form in (1, 2, 3):
+        for form in (1, 2, 3, 4):
             fattn.set_option(fattn.OPT_PF_FORM, form)
             t = upload(p)
             att = fattn.Attention(*views(p, t), t["dst"], p.scale)
             assert ("fattn_pf4_kernel" in att.describe()) == (form >= 2), att.describe()
             assert ("(sched1)" in att.describe()) == (form == 3), att.describe()
+            assert ("(pipelined)" in att.describe()) == (form == 4), att.describe()
             att()
             outs[form] = t["dst"].cpu().numpy()
     finally:
@@ -678,7 +681,8 @@ def test_pf4_bit_identical_to_pf(dev, case):
         fattn.set_option(fattn.OPT_PF_FORM, 0)
     assert np.array_equal(outs[1], outs[2], equal_nan=True)
     assert np.array_equal(outs[1], outs[3], equal_nan=True)
-    assert attn_rel_err(outs[3], p.oracle()) <= RTOL
+    assert np.array_equal(outs[1], outs[4], equal_nan=True)
+    assert attn_rel_err(outs[4], p.oracle()) <= RTOL
 
 
 @pytest.mark.parametrize("case", [
