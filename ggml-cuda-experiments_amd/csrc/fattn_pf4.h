@@ -592,27 +592,48 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         // B_{j-1}'s issues in flight: K_{j+1}, V_{j-1} and mask j have landed
         // (this wave's pieces; B_j's barrier then covers everyone's).
         static_assert(C::NKI == 4 && C::NMI == 8, "the wait counts below are multiples of 4");
-        auto wait_dyn = [&](int n) {  // s_waitcnt vmcnt(n), n a multiple of 4 in [0, 28] (wave-uniform)
-            switch (__builtin_amdgcn_readfirstlane(n)) {
-                case 28: wait_vmcnt_c<28>(); break;
-                case 24: wait_vmcnt_c<24>(); break;
-                case 20: wait_vmcnt_c<20>(); break;
-                case 16: wait_vmcnt_c<16>(); break;
-                case 12: wait_vmcnt_c<12>(); break;
-                case 8: wait_vmcnt_c<8>(); break;
-                case 4: wait_vmcnt_c<4>(); break;
-                default: wait_vmcnt_c<0>(); break;
+        constexpr int MI = HM ? C::NMI : 0;
+        // Every tile issues the same DMA instructions (K_{j+3}, V_{j+1}, mask
+        // j+2 at B_j), a tile past the end through an offset past its
+        // descriptor (no traffic; into a slot nothing reads again), so every
+        // counted wait is one constant and the issues sit inside B's steps
+        // without a branch.
+        auto k_piece = [&](int s, int i) {
+            const uint32_t nk = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.k_nb1;
+            const uint32_t dst = lds0 + C::kOff + (s % C::KS) * C::img + (wave + kPf4Waves * i) * 1024;
+            dma<16>(rs.k, dst, s < nt ? nk + koff0 + 64 * i : a.k_span);
+        };
+        auto v_piece = [&](int s, int i) {
+            const uint32_t nv = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.v_nb1;
+            const uint32_t dst = lds0 + C::vOff + (s % C::VS) * C::img + (wave + kPf4Waves * i) * 1024;
+            dma<16>(rs.v, dst, s < nt ? nv + voff0 + 64 * i : a.v_span);
+        };
+        // (skip: tile s past the end or a +-0 block, decided once per tile --
+        // inside B's steps a branch would split the phase)
+        auto m_skip = [&](int s) { return s >= nt || zero_of(s); };
+        auto m_piece = [&](int s, int k, bool skip) {
+            if constexpr (HM) {
+                const uint32_t n2 = (uint32_t)(t0 + s) * kPfKeys * 2;
+                const uint32_t dst = lds0 + C::mOff + (wave * C::MS + s % C::MS) * C::maskSlot + k * 1024;
+                dma<16>(rs.m, dst, (skip || moff[k] == a.m_span) ? a.m_span : moff[k] + n2);
             }
         };
-        constexpr int MI = HM ? C::NMI : 0;
         // prologue: K 0 | K 1, mask 0 | K 2, V 0, mask 1 (the last two groups as
         // the steady state's B_{-2} and B_{-1})
-        if (nt > 0) k_issue(0);
-        if (nt > 1) k_issue(1);
-        if (nt > 0) m_issue(0);
-        if (nt > 2) k_issue(2);
-        if (nt > 0) v_issue(0);
-        if (nt > 1) m_issue(1);
+        if (nt > 0) {
+#pragma unroll
+            for (int i = 0; i < C::NKI; i++) k_piece(0, i);
+#pragma unroll
+            for (int i = 0; i < C::NKI; i++) k_piece(1, i);
+#pragma unroll
+            for (int k = 0; k < C::NMI; k++) m_piece(0, k, m_skip(0));
+#pragma unroll
+            for (int i = 0; i < C::NKI; i++) k_piece(2, i);
+#pragma unroll
+            for (int i = 0; i < C::NKI; i++) v_piece(0, i);
+#pragma unroll
+            for (int k = 0; k < C::NMI; k++) m_piece(1, k, m_skip(1));
+        }
         // O_rb^T += V_s^T . P_rb^T for both row blocks, each V^T operand read
         // once; per accumulator the 8-wave body's order (t, q)
         auto pv2 = [&](int s, const f16x8 (&pa)[2][2], const f16x8 (&pb)[2][2]) {
@@ -665,7 +686,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         };
         if (nt > 0) {
             // K 0 landed: everything issued after it may fly
-            wait_dyn((nt > 1 ? C::NKI : 0) + MI + (nt > 2 ? C::NKI : 0) + C::NKI + (nt > 1 ? MI : 0));
+            wait_vmcnt_c<3 * C::NKI + 2 * MI>();
             __syncthreads();
         }
         float us0[2][16], us1[2][16];
@@ -706,6 +727,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 us[t][k] = x;
                 tmax = fmaxf(tmax, x);
             }
+            // (the piece's results through a volatile asm: volatile asm statements
+            // keep their order, so the piece is computed in its step -- the
+            // instruction selector otherwise places side-effect-free VALU next to
+            // its last use, past every step)
+            asm volatile("" : "+v"(tmax), "+v"(us[t][k0]), "+v"(us[t][k0 + 1]));
         };
         auto smax_final = [&](int rb, float tmax, float& alpha, bool& resc) {
             tmax = PF4_XOR32(tmax, true) * cexp;
@@ -723,13 +749,14 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             lb = add_f32(lb, pq);
             pb[t][k >> 3][k & 7] = (f16)pa;
             pb[t][k >> 3][(k & 7) + 1] = (f16)pq;
+            asm volatile("" : "+v"(la), "+v"(lb));  // (see smax_piece)
         };
         auto iter = [&](int j, auto first) {
             constexpr bool F = decltype(first)::value;
             // ---- A_j: S_j for rb 1 (steps 0-15) and rb 0 (16-31); rb 1's
             // exponentials of tile j-1 beside steps 0-15, its scores and max of
             // tile j beside 16-31 (its S chains done by then)
-            wait_dyn((j + 2 < nt ? C::NKI : 0) + C::NKI + (j + 1 < nt ? MI : 0));
+            wait_vmcnt_c<2 * C::NKI + MI>();  // B_{j-1}'s issues may fly
             pr1 = rs1;  // rb 1's decision of tile j-1, applied at B_j
             pa1 = al1;
             u32x2 mk1[2][4], mk0[2][4];
@@ -766,8 +793,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             // once); rb 0's scores and max of tile j beside steps 0-15, its
             // exponentials beside 16-31
             __syncthreads();
-            if (j + 3 < nt) k_issue(j + 3);
-            if (j + 1 < nt) v_issue(j + 1);
             rescale_acc(0, rs0, al0);  // decisions of tile j-1
             rescale_acc(1, pr1, pa1);
             f16x8 va[2][2][NDB];
@@ -794,6 +819,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             }
             float tmax0 = kNegInf, nm0 = 0.0f, la0 = 0.0f, lb0 = 0.0f;
             f16x8 p0n[2][2];
+            const bool mskip = HM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 32; i++) {
@@ -809,6 +835,15 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     lb0 = l2[0].y;
                 }
                 if (i >= 16) sexp_piece(us0, p0n, nm0, la0, lb0, i - 16);
+                // this tile's DMA: K_{j+3} and V_{j+1} pieces in steps 1, 3, ..., 15
+                // (into slots every wave finished before the barrier), mask j+2
+                // in steps 17, 19, ..., 31 (this wave's reads of mask j are
+                // consumed by then)
+                if (i < 16 && (i & 1)) {
+                    if (i & 2) v_piece(j + 1, i >> 2);
+                    else k_piece(j + 3, i >> 2);
+                }
+                if (i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
                 __builtin_amdgcn_sched_barrier(0);
             }
             l2[0] = f32x2{la0, lb0};
@@ -817,10 +852,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             for (int t = 0; t < 2; t++) {
 #pragma unroll
                 for (int q = 0; q < 2; q++) p0[t][q] = p0n[t][q];
-            }
-            if (HM && j + 2 < nt) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's mask j has been read
-                m_issue(j + 2);
             }
         };
         if (nt > 0) iter(0, std::true_type());
