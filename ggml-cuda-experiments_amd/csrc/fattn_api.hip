@@ -62,7 +62,7 @@ std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge 
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
 std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto, 1 off, 2 on
-std::atomic<int> g_opt_pf_form{0};          // prefill body: 0 auto, 1 the 8-wave form, 2 one wave per SIMD (fattn_pf4.h)
+std::atomic<int> g_opt_pf_form{0};          // prefill body at D = 128 over f16 rows: 0 auto (4), 1 the 8-wave form, 2-4 one wave per SIMD (fattn_pf4.h)
 std::atomic<int> g_opt_pf_stage{0};         // prefill over Q8_0 / Q4_0: 0 auto (staged to f16), 1 in-kernel dequantisation, 2 staged
 std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
@@ -597,8 +597,11 @@ int make_plan(const fattn_params* p, Plan& pl) {
                  : D == 96 ? pf_lds(std::integral_constant<int, 96>())
                            : pf_lds(std::integral_constant<int, 128>());
         // f16 rows (native or staged) at D = 128: the one-wave-per-SIMD body
-        pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && g_opt_pf_form >= 2;
-        pl.pf4_sched = g_opt_pf_form >= 3 ? g_opt_pf_form - 2 : 0;
+        // (auto: the pipelined schedule, 3-10 % faster than the 8-wave body on
+        // the prefill shape, profiles/r05_h; form 1 keeps the 8-wave body)
+        const int form = g_opt_pf_form == 0 ? 4 : (int)g_opt_pf_form;
+        pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && form >= 2;
+        pl.pf4_sched = form >= 3 ? form - 2 : 0;
         if (pl.pf4) pl.lds = Pf4Cfg<128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
