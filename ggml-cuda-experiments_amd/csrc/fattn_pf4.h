@@ -673,16 +673,18 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         };
         // K_j's operands, read once per tile at the start of A_j for both row blocks
         f16x8 kr[2][NK];
-        auto k_read = [&](int s) {
+        // (the streamed forms: operand reads placed inside the steps, a few
+        // ahead of their MFMA -- with all of a phase's reads at its head the
+        // 4-bit lgkmcnt cannot name the first one, and the first MFMA waited
+        // for half of them)
+        auto k_base = [&](int s) {
             uint32_t kb = (uint32_t)(C::kOff + (s % C::KS) * C::img) + kbase;
             PF4_OPAQUE_V(kb);
-            const lds_u8* img = (const lds_u8*)smem + kb;
-#pragma unroll
-            for (int t = 0; t < 2; t++) {
-#pragma unroll
-                for (int kk = 0; kk < NK; kk++)
-                    kr[t][kk] = *(const __attribute__((address_space(3))) f16x8*)(img + kk * (kPfKeys * 32) + t * 1024);
-            }
+            return kb;
+        };
+        auto k_read1 = [&](uint32_t kb, int t, int kk) {
+            kr[t][kk] = *(const __attribute__((address_space(3))) f16x8*)((const lds_u8*)smem + kb + kk * (kPfKeys * 32) +
+                                                                       t * 1024);
         };
         if (nt > 0) {
             // K 0 landed: everything issued after it may fly
@@ -751,24 +753,45 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             pb[t][k >> 3][(k & 7) + 1] = (f16)pq;
             asm volatile("" : "+v"(la), "+v"(lb));  // (see smax_piece)
         };
+#ifdef FATTN_STAMPS
+        // diagnostic build only (tools/pf_stamps.py): shader-clock cycles per
+        // phase part, summed over tiles (0 A's wait, 1 A's steps, 2 A's tail,
+        // 3 B's barrier, 4 B's head -- rescale, V^T reads --, 5 B's steps, 6 B's
+        // tail, 7 between tiles)
+        uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint64_t t_prev = __builtin_amdgcn_s_memtime();
+#define PF4_T(k)                                              \
+    do {                                                      \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+        ph[k] += t_ - t_prev;                                 \
+        t_prev = t_;                                          \
+    } while (0)
+#else
+#define PF4_T(k) do { } while (0)
+#endif
         auto iter = [&](int j, auto first) {
             constexpr bool F = decltype(first)::value;
+            PF4_T(7);
             // ---- A_j: S_j for rb 1 (steps 0-15) and rb 0 (16-31); rb 1's
             // exponentials of tile j-1 beside steps 0-15, its scores and max of
             // tile j beside 16-31 (its S chains done by then)
             wait_vmcnt_c<2 * C::NKI + MI>();  // B_{j-1}'s issues may fly
+            PF4_T(0);
             pr1 = rs1;  // rb 1's decision of tile j-1, applied at B_j
             pa1 = al1;
             u32x2 mk1[2][4], mk0[2][4];
-            k_read(j);
-            mask_reads(j, 1, mk1);
-            mask_reads(j, 0, mk0);  // (rb 0's, for B_j: this wave's slot, no barrier needed)
+            const uint32_t kb = k_base(j);
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) k_read1(kb, 0, kk);  // the rest: 4 steps ahead, in the steps
             const float nm1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];
             float la1 = l2[1].x, lb1 = l2[1].y, tmax1 = kNegInf;
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 32; i++) {
                 const int t = (i >> 3) & 1, kk = i & 7;
+                if (i < 12) k_read1(kb, (i + 4) >> 3, (i + 4) & 7);
+                if (i == 12) mask_reads(j, 1, mk1);  // (for rb 1's scores, steps 18+)
+                if (i == 14) mask_reads(j, 0, mk0);  // (for B_j: this wave's slot, no barrier needed)
                 if (i < 16) {
                     if (kk == 0) s1[t] = f32x16{};
                     s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
@@ -780,6 +803,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
+            PF4_T(1);
             smax_piece(s1, mk1, us1, tmax1, 14);
             smax_piece(s1, mk1, us1, tmax1, 15);
             if constexpr (!F) l2[1] = f32x2{la1, lb1};
@@ -789,41 +813,41 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             if constexpr (!F) pin_p(p1);
             pin16(us1[0]);
             pin16(us1[1]);
+            PF4_T(2);
             // ---- B_j: P_{j-1}.V for both row blocks (each V^T operand read
             // once); rb 0's scores and max of tile j beside steps 0-15, its
             // exponentials beside 16-31
             __syncthreads();
+            PF4_T(3);
             rescale_acc(0, rs0, al0);  // decisions of tile j-1
             rescale_acc(1, pr1, pa1);
+            // V^T operands streamed: operand v (= the MFMAs of steps 2v, 2v+1)
+            // read 4 operands (8 steps) ahead
             f16x8 va[2][2][NDB];
+            uint32_t vb0 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[0];
+            uint32_t vb1 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[1];
+            PF4_OPAQUE_V2(vb0, vb1);
+            auto v_read1 = [&](int v) {
+                const int t = v >> 3, q = (v >> 2) & 1, db = v & 3;
+                const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb0 + off));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb1 + off));
+                const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
+            };
             if constexpr (!F) {
-                uint32_t b0 = (uint32_t)(C::vOff + ((j - 1) % C::VS) * C::img) + vbase[0];
-                uint32_t b1 = (uint32_t)(C::vOff + ((j - 1) % C::VS) * C::img) + vbase[1];
-                PF4_OPAQUE_V2(b0, b1);
-                lds_u8* const img0 = lsm + b0;
-                lds_u8* const img1 = lsm + b1;
 #pragma unroll
-                for (int t = 0; t < 2; t++) {
-#pragma unroll
-                    for (int q = 0; q < 2; q++) {
-#pragma unroll
-                        for (int db = 0; db < NDB; db++) {
-                            const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
-                            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
-                            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img1 + off));
-                            const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
-                            va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
-                        }
-                    }
-                }
+                for (int v = 0; v < 4; v++) v_read1(v);
             }
             float tmax0 = kNegInf, nm0 = 0.0f, la0 = 0.0f, lb0 = 0.0f;
             f16x8 p0n[2][2];
             const bool mskip = HM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
+            PF4_T(4);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 32; i++) {
                 if constexpr (!F) {
+                    if (!(i & 1) && i < 24) v_read1((i >> 1) + 4);
                     const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
                     o[rb][db] = mfma32(va[t][q][db], rb ? p1[t][q] : p0[t][q], o[rb][db]);
                 }
@@ -846,6 +870,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 if (i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
                 __builtin_amdgcn_sched_barrier(0);
             }
+            PF4_T(5);
             l2[0] = f32x2{la0, lb0};
             pin_p(p0n);
 #pragma unroll
@@ -853,6 +878,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
 #pragma unroll
                 for (int q = 0; q < 2; q++) p0[t][q] = p0n[t][q];
             }
+            PF4_T(6);
         };
         if (nt > 0) iter(0, std::true_type());
         for (int j = 1; j < nt; j++) iter(j, std::false_type());
@@ -866,6 +892,14 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             rescale_acc(1, rs1, al1);
             pv2(nt - 1, p0, p1);
         }
+#ifdef FATTN_STAMPS
+        if (lane == 0 && g_stamps) {
+            const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+            for (int k = 0; k < 8; k++) g_stamps[(blk * kPfWaves + wave) * 16 + k] = ph[k];
+            g_stamps[(blk * kPfWaves + wave) * 16 + 8] = (unsigned long long)nt;
+        }
+#endif
+#undef PF4_T
     } else {
         // the rebalanced schedule (see the kernel's comment)
         float us0[2][16], us1[2][16];

@@ -20,8 +20,10 @@ ap.add_argument("--n-q", type=int, default=4096)
 ap.add_argument("--kv-len", type=int, default=4096)
 ap.add_argument("--heads", type=int, default=32)
 ap.add_argument("--kv-type", default="q8_0")
+ap.add_argument("--form", type=int, default=0, help="FATTN_OPT_PF_FORM (0: the planner's body)")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
+fattn.set_option(fattn.OPT_PF_FORM, args.form)
 D, H, N, NQ = 128, args.heads, args.kv_len, args.n_q
 typ = fattn.TYPE_NAMES[args.kv_type]
 if args.kv_type == "f16":
@@ -52,9 +54,12 @@ s = st.cpu().numpy().reshape(-1, 8, 16)
 s = s[s[:, 0, 8] > 0]
 nt = s[:, :, 8].astype(np.float64)
 names = ["wait+barrier", "dma issue", "dequant", "S^T mfma", "softmax", "O^T mfma", "-", "loop tail"]
+pf4 = "fattn_pf4_kernel" in att.describe()
+if pf4:  # the pipelined one-wave-per-SIMD body (fattn_pf4.h SCHED 2): 4 waves
+    names = ["A wait", "A steps", "A tail", "B barrier", "B head", "B steps", "B tail", "between tiles"]
 print(att.describe())
 print(f"workgroups {len(s)}  event {e0.elapsed_time(e1) * 1e3:.1f} us  (cycles per tile, mean)")
-for half, sl in (("waves 0-3", slice(0, 4)), ("waves 4-7", slice(4, 8))):
+for half, sl in (("waves 0-3", slice(0, 4)),) + ((("waves 4-7", slice(4, 8)),) if not pf4 else ()):
     per = s[:, sl, :8].astype(np.float64) / nt[:, sl, None]
     tot = per.sum(axis=2).mean()
     print(f"{half}: total {tot:8.0f}  " + "  ".join(f"{n} {per[..., i].mean():6.0f}" for i, n in enumerate(names) if n != "-"))
