@@ -735,6 +735,14 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             // its last use, past every step)
             asm volatile("" : "+v"(tmax), "+v"(us[t][k0]), "+v"(us[t][k0 + 1]));
         };
+        // (the rescale decision from the lane pair's max, log2 units)
+        auto smax_decide = [&](int rb, float tmax, float& alpha, bool& resc) {
+            resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
+            const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
+            alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
+            m_run[rb] = m_new;
+            l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
+        };
         auto smax_final = [&](int rb, float tmax, float& alpha, bool& resc) {
             tmax = PF4_XOR32(tmax, true) * cexp;
             resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
@@ -787,25 +795,27 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             float la1 = l2[1].x, lb1 = l2[1].y, tmax1 = kNegInf;
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
+            // (each step: its vector piece first -- issued while the previous
+            // step's MFMA runs, and at the phase's head while the first operand
+            // reads land -- then its MFMA)
             for (int i = 0; i < 32; i++) {
                 const int t = (i >> 3) & 1, kk = i & 7;
                 if (i < 12) k_read1(kb, (i + 4) >> 3, (i + 4) & 7);
-                if (i == 12) mask_reads(j, 1, mk1);  // (for rb 1's scores, steps 18+)
+                if (i == 8) mask_reads(j, 1, mk1);   // (for rb 1's scores, steps 16+)
                 if (i == 14) mask_reads(j, 0, mk0);  // (for B_j: this wave's slot, no barrier needed)
                 if (i < 16) {
+                    if constexpr (!F) sexp_piece(us1, p1, nm1, la1, lb1, i);
                     if (kk == 0) s1[t] = f32x16{};
                     s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
-                    if constexpr (!F) sexp_piece(us1, p1, nm1, la1, lb1, i);
                 } else {
+                    // (S1's subtile-0 chain ended at step 7, subtile 1's at 15)
+                    smax_piece(s1, mk1, us1, tmax1, i - 16);
                     if (kk == 0) s0[t] = f32x16{};
                     s0[t] = mfma32(kr[t][kk], qop[0][kk], s0[t]);
-                    if (i >= 18) smax_piece(s1, mk1, us1, tmax1, i - 18);  // (S1's last chain lands ~2 steps late)
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
             PF4_T(1);
-            smax_piece(s1, mk1, us1, tmax1, 14);
-            smax_piece(s1, mk1, us1, tmax1, 15);
             if constexpr (!F) l2[1] = f32x2{la1, lb1};
             smax_final(1, tmax1, al1, rs1);
             // (the phase's results pinned here: hipcc's machine sinking would
@@ -844,21 +854,34 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             const bool mskip = HM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
             PF4_T(4);
             __builtin_amdgcn_sched_barrier(0);
+            float tred0 = 0.0f;
 #pragma unroll
             for (int i = 0; i < 32; i++) {
+                // vector piece: rb 0's scores and max (steps 0-13, two pieces in
+                // steps 0 and 1), the max across the lane pair (14), the rescale
+                // decision (15: a dependent chain, split over two steps), its
+                // exponentials (16-31)
+                if (i < 14) {
+                    if (i < 2) smax_piece(s0, mk0, us0, tmax0, 2 * i);
+                    smax_piece(s0, mk0, us0, tmax0, i < 2 ? 2 * i + 1 : i + 2);
+                }
+                if (i == 14) {
+                    tred0 = PF4_XOR32(tmax0, true) * cexp;
+                    asm volatile("" : "+v"(tred0));
+                }
+                if (i == 15) {
+                    smax_decide(0, tred0, al0, rs0);
+                    nm0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
+                    la0 = l2[0].x;
+                    lb0 = l2[0].y;
+                    asm volatile("" : "+v"(nm0), "+v"(la0), "+v"(lb0));
+                }
+                if (i >= 16) sexp_piece(us0, p0n, nm0, la0, lb0, i - 16);
                 if constexpr (!F) {
                     if (!(i & 1) && i < 24) v_read1((i >> 1) + 4);
                     const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
                     o[rb][db] = mfma32(va[t][q][db], rb ? p1[t][q] : p0[t][q], o[rb][db]);
                 }
-                if (i < 16) smax_piece(s0, mk0, us0, tmax0, i);
-                if (i == 16) {
-                    smax_final(0, tmax0, al0, rs0);
-                    nm0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
-                    la0 = l2[0].x;
-                    lb0 = l2[0].y;
-                }
-                if (i >= 16) sexp_piece(us0, p0n, nm0, la0, lb0, i - 16);
                 // this tile's DMA: K_{j+3} and V_{j+1} pieces in steps 1, 3, ..., 15
                 // (into slots every wave finished before the barrier), mask j+2
                 // in steps 17, 19, ..., 31 (this wave's reads of mask j are
