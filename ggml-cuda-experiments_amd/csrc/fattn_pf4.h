@@ -575,354 +575,383 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             if (s + 1 < nt) qk(s + 1, 0, s0);
         }
     } else if constexpr (SCHED == 2) {
-        // the pipelined schedule (cdna_hip_programming.md 'Fused attention
-        // prefill', 4-wave structure): per tile two phases of 32 MFMAs,
-        //   A_j: S_j = K_j . Q^T for both row blocks  ||  rb 1's exponentials
-        //        of tile j-1, rb 1's scores / max / rescale decision of tile j;
-        //   B_j: O += V_{j-1}^T . P_{j-1}^T for both row blocks (each V^T
-        //        operand read once, used twice)  ||  rb 0's scores / max /
-        //        decision and exponentials of tile j;
-        // so both phases carry one row block's exponentials (one v_exp per
-        // MFMA gap).  The O rescale a decision of tile j-1 asks for is applied
-        // at the start of A_j: after P_{j-2}.V (B_{j-1}), before P_{j-1}.V --
-        // the 8-wave body's order of operations on O and l, so the same bits.
-        // Rings: K_{j+3} and V_{j+1} are issued at B_j (after its barrier)
-        // into the slots of K_j (read in A_j) and V_{j-2} (B_{j-1}); the
-        // wave's mask j+2 after its reads of mask j.  A_j's counted wait leaves
-        // B_{j-1}'s issues in flight: K_{j+1}, V_{j-1} and mask j have landed
-        // (this wave's pieces; B_j's barrier then covers everyone's).
-        static_assert(C::NKI == 4 && C::NMI == 8, "the wait counts below are multiples of 4");
-        constexpr int MI = HM ? C::NMI : 0;
-        // Every tile issues the same DMA instructions (K_{j+3}, V_{j+1}, mask
-        // j+2 at B_j), a tile past the end through an offset past its
-        // descriptor (no traffic; into a slot nothing reads again), so every
-        // counted wait is one constant and the issues sit inside B's steps
-        // without a branch.
-        auto k_piece = [&](int s, int i) {
-            const uint32_t nk = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.k_nb1;
-            const uint32_t dst = lds0 + C::kOff + (s % C::KS) * C::img + (wave + kPf4Waves * i) * 1024;
-            dma<16>(rs.k, dst, s < nt ? nk + koff0 + 64 * i : a.k_span);
-        };
-        auto v_piece = [&](int s, int i) {
-            const uint32_t nv = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.v_nb1;
-            const uint32_t dst = lds0 + C::vOff + (s % C::VS) * C::img + (wave + kPf4Waves * i) * 1024;
-            dma<16>(rs.v, dst, s < nt ? nv + voff0 + 64 * i : a.v_span);
-        };
-        // (skip: tile s past the end or a +-0 block, decided once per tile --
-        // inside B's steps a branch would split the phase)
-        auto m_skip = [&](int s) { return s >= nt || zero_of(s); };
-        auto m_piece = [&](int s, int k, bool skip) {
-            if constexpr (HM) {
-                const uint32_t n2 = (uint32_t)(t0 + s) * kPfKeys * 2;
-                const uint32_t dst = lds0 + C::mOff + (wave * C::MS + s % C::MS) * C::maskSlot + k * 1024;
-                dma<16>(rs.m, dst, (skip || moff[k] == a.m_span) ? a.m_span : moff[k] + n2);
+        // A workgroup whose live tiles all hold +-0 masks (the flags pass's 2,
+        // SURVEY's zero-mask prefill) runs the body without mask values in
+        // LDS (ZM): no mask DMA, reads or waits, scores fma(s, scale, 0) --
+        // the masked path's arithmetic on a zero mask, so the same bits.
+        bool all_zero = false;
+        if constexpr (HM) {
+            int nz = 0;
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const int lo = 64 * w;
+                const uint64_t in = nt >= lo + 64 ? ~0ull : (nt > lo ? (1ull << (nt - lo)) - 1 : 0ull);
+                nz += __builtin_popcountll(zb[w] & in);
             }
-        };
-        // prologue: K 0 | K 1, mask 0 | K 2, V 0, mask 1 (the last two groups as
-        // the steady state's B_{-2} and B_{-1})
-        if (nt > 0) {
-#pragma unroll
-            for (int i = 0; i < C::NKI; i++) k_piece(0, i);
-#pragma unroll
-            for (int i = 0; i < C::NKI; i++) k_piece(1, i);
-#pragma unroll
-            for (int k = 0; k < C::NMI; k++) m_piece(0, k, m_skip(0));
-#pragma unroll
-            for (int i = 0; i < C::NKI; i++) k_piece(2, i);
-#pragma unroll
-            for (int i = 0; i < C::NKI; i++) v_piece(0, i);
-#pragma unroll
-            for (int k = 0; k < C::NMI; k++) m_piece(1, k, m_skip(1));
+            all_zero = nt > 0 && nz == nt;
         }
-        // O_rb^T += V_s^T . P_rb^T for both row blocks, each V^T operand read
-        // once; per accumulator the 8-wave body's order (t, q)
-        auto pv2 = [&](int s, const f16x8 (&pa)[2][2], const f16x8 (&pb)[2][2]) {
-            uint32_t b0 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[0];
-            uint32_t b1 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[1];
-            PF4_OPAQUE_V2(b0, b1);
-            lds_u8* const img0 = lsm + b0;
-            lds_u8* const img1 = lsm + b1;
-            // every V^T operand of the tile first (64 VGPRs), so that no MFMA
-            // of the phase waits for its own read
-            f16x8 va[2][2][NDB];
-#pragma unroll
-            for (int t = 0; t < 2; t++) {
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-#pragma unroll
-                    for (int db = 0; db < NDB; db++) {
-                        const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
-                        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
-                        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img1 + off));
-                        const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
-                        va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
-                    }
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < 2; t++) {
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-#pragma unroll
-                    for (int db = 0; db < NDB; db++) {
-                        o[0][db] = mfma32(va[t][q][db], pa[t][q], o[0][db]);
-                        o[1][db] = mfma32(va[t][q][db], pb[t][q], o[1][db]);
-                    }
-                }
-            }
-        };
-        // K_j's operands, read once per tile at the start of A_j for both row blocks
-        f16x8 kr[2][NK];
-        // (the streamed forms: operand reads placed inside the steps, a few
-        // ahead of their MFMA -- with all of a phase's reads at its head the
-        // 4-bit lgkmcnt cannot name the first one, and the first MFMA waited
-        // for half of them)
-        auto k_base = [&](int s) {
-            uint32_t kb = (uint32_t)(C::kOff + (s % C::KS) * C::img) + kbase;
-            PF4_OPAQUE_V(kb);
-            return kb;
-        };
-        auto k_read1 = [&](uint32_t kb, int t, int kk) {
-            kr[t][kk] = *(const __attribute__((address_space(3))) f16x8*)((const lds_u8*)smem + kb + kk * (kPfKeys * 32) +
-                                                                       t * 1024);
-        };
-        if (nt > 0) {
-            // K 0 landed: everything issued after it may fly
-            wait_vmcnt_c<3 * C::NKI + 2 * MI>();
-            __syncthreads();
-        }
-        float us0[2][16], us1[2][16];
-        float al0 = 1.0f, al1 = 1.0f;
-        bool rs0 = false, rs1 = false;
-        f16x8 p0[2][2], p1[2][2];
-        // (the first tile without rb 1's previous exponentials and without a
-        // P.V: a compile-time flag, so that no branch splits a phase -- a
-        // phase must stay one basic block for its VALU to sit between its MFMAs)
-        // O rescale (a decision of tile j-1: rb 0's made in B_{j-1}, rb 1's in
-        // A_{j-1}, kept as pending through A_j) at the start of B_j, after its
-        // barrier: after P_{j-2}.V, before P_{j-1}.V; in AGPRs (scale_acc16)
-        bool pr1 = false;
-        float pa1 = 1.0f;
-        auto rescale_acc = [&](int rb, bool resc, float alpha) {
-            if (__builtin_expect(resc, 0)) {
-#pragma unroll
-                for (int db = 0; db < NDB; db++) scale_acc16(o[rb][db], alpha);
-            }
-        };
-        // The phases are written as 32 explicit (MFMA, vector piece) steps, each
-        // its own scheduling region (sched_barrier): hipcc's scheduling groups
-        // left the exponentials behind the MFMA runs (in-order issue then
-        // serialises them).  A vector piece = two elements of one row block:
-        // scores + running max (smax_piece) or exponentials + row sums + f16
-        // pair (sexp_piece) -- the same operations in the same order per row
-        // as smax / sexp, so the same bits.
-        auto smax_piece = [&](const f32x16 (&st)[2], const u32x2 (&mk)[2][4], float (&us)[2][16], float& tmax, int pc) {
-            const int t = pc >> 3, k0 = 2 * (pc & 7);
-#pragma unroll
-            for (int k = k0; k < k0 + 2; k++) {
-                float x = st[t][k];
-                if constexpr (HM) {
-                    const int u = k >> 2, e = k & 3;
-                    const f16x2 mm = as_h2(e < 2 ? mk[t][u].x : mk[t][u].y);
-                    x = fmaf(x, scale, (float)(e & 1 ? mm.y : mm.x));
-                }
-                us[t][k] = x;
-                tmax = fmaxf(tmax, x);
-            }
-            // (the piece's results through a volatile asm: volatile asm statements
-            // keep their order, so the piece is computed in its step -- the
-            // instruction selector otherwise places side-effect-free VALU next to
-            // its last use, past every step)
-            asm volatile("" : "+v"(tmax), "+v"(us[t][k0]), "+v"(us[t][k0 + 1]));
-        };
-        // (the rescale decision from the lane pair's max, log2 units)
-        auto smax_decide = [&](int rb, float tmax, float& alpha, bool& resc) {
-            resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
-            const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
-            alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
-            m_run[rb] = m_new;
-            l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
-        };
-        auto smax_final = [&](int rb, float tmax, float& alpha, bool& resc) {
-            tmax = PF4_XOR32(tmax, true) * cexp;
-            resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
-            const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
-            alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
-            m_run[rb] = m_new;
-            l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
-        };
-        auto sexp_piece = [&](const float (&us)[2][16], f16x8 (&pb)[2][2], float nm, float& la, float& lb, int pc) {
-            const int t = pc >> 3, k = 2 * (pc & 7);
-            const float pa = __builtin_amdgcn_exp2f(fmaf(us[t][k], cexp, nm));
-            const float pq = __builtin_amdgcn_exp2f(fmaf(us[t][k + 1], cexp, nm));
-            la = add_f32(la, pa);
-            lb = add_f32(lb, pq);
-            pb[t][k >> 3][k & 7] = (f16)pa;
-            pb[t][k >> 3][(k & 7) + 1] = (f16)pq;
-            asm volatile("" : "+v"(la), "+v"(lb));  // (see smax_piece)
-        };
-#ifdef FATTN_STAMPS
-        // diagnostic build only (tools/pf_stamps.py): shader-clock cycles per
-        // phase part, summed over tiles (0 A's wait, 1 A's steps, 2 A's tail,
-        // 3 B's barrier, 4 B's head -- rescale, V^T reads --, 5 B's steps, 6 B's
-        // tail, 7 between tiles)
-        uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        uint64_t t_prev = __builtin_amdgcn_s_memtime();
-#define PF4_T(k)                                              \
-    do {                                                      \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
-        ph[k] += t_ - t_prev;                                 \
-        t_prev = t_;                                          \
-    } while (0)
-#else
-#define PF4_T(k) do { } while (0)
-#endif
-        auto iter = [&](int j, auto first) {
-            constexpr bool F = decltype(first)::value;
-            PF4_T(7);
-            // ---- A_j: S_j for rb 1 (steps 0-15) and rb 0 (16-31); rb 1's
-            // exponentials of tile j-1 beside steps 0-15, its scores and max of
-            // tile j beside 16-31 (its S chains done by then)
-            wait_vmcnt_c<2 * C::NKI + MI>();  // B_{j-1}'s issues may fly
-            PF4_T(0);
-            pr1 = rs1;  // rb 1's decision of tile j-1, applied at B_j
-            pa1 = al1;
-            u32x2 mk1[2][4], mk0[2][4];
-            const uint32_t kb = k_base(j);
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++) k_read1(kb, 0, kk);  // the rest: 4 steps ahead, in the steps
-            const float nm1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];
-            float la1 = l2[1].x, lb1 = l2[1].y, tmax1 = kNegInf;
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            // (each step: its vector piece first -- issued while the previous
-            // step's MFMA runs, and at the phase's head while the first operand
-            // reads land -- then its MFMA)
-            for (int i = 0; i < 32; i++) {
-                const int t = (i >> 3) & 1, kk = i & 7;
-                if (i < 12) k_read1(kb, (i + 4) >> 3, (i + 4) & 7);
-                if (i == 8) mask_reads(j, 1, mk1);   // (for rb 1's scores, steps 16+)
-                if (i == 14) mask_reads(j, 0, mk0);  // (for B_j: this wave's slot, no barrier needed)
-                if (i < 16) {
-                    if constexpr (!F) sexp_piece(us1, p1, nm1, la1, lb1, i);
-                    if (kk == 0) s1[t] = f32x16{};
-                    s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
-                } else {
-                    // (S1's subtile-0 chain ended at step 7, subtile 1's at 15)
-                    smax_piece(s1, mk1, us1, tmax1, i - 16);
-                    if (kk == 0) s0[t] = f32x16{};
-                    s0[t] = mfma32(kr[t][kk], qop[0][kk], s0[t]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            PF4_T(1);
-            if constexpr (!F) l2[1] = f32x2{la1, lb1};
-            smax_final(1, tmax1, al1, rs1);
-            // (the phase's results pinned here: hipcc's machine sinking would
-            // otherwise move their exponentials next to their uses in B)
-            if constexpr (!F) pin_p(p1);
-            pin16(us1[0]);
-            pin16(us1[1]);
-            PF4_T(2);
-            // ---- B_j: P_{j-1}.V for both row blocks (each V^T operand read
-            // once); rb 0's scores and max of tile j beside steps 0-15, its
-            // exponentials beside 16-31
-            __syncthreads();
-            PF4_T(3);
-            rescale_acc(0, rs0, al0);  // decisions of tile j-1
-            rescale_acc(1, pr1, pa1);
-            // V^T operands streamed: operand v (= the MFMAs of steps 2v, 2v+1)
-            // read 4 operands (8 steps) ahead
-            f16x8 va[2][2][NDB];
-            uint32_t vb0 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[0];
-            uint32_t vb1 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[1];
-            PF4_OPAQUE_V2(vb0, vb1);
-            auto v_read1 = [&](int v) {
-                const int t = v >> 3, q = (v >> 2) & 1, db = v & 3;
-                const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
-                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb0 + off));
-                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb1 + off));
-                const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
-                va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
+        auto body2 = [&](auto zm_tag) {
+            constexpr bool ZM = decltype(zm_tag)::value;
+            constexpr bool MM = HM && !ZM;  // mask values through LDS
+            // the pipelined schedule (cdna_hip_programming.md 'Fused attention
+            // prefill', 4-wave structure): per tile two phases of 32 MFMAs,
+            //   A_j: S_j = K_j . Q^T for both row blocks  ||  rb 1's exponentials
+            //        of tile j-1, rb 1's scores / max / rescale decision of tile j;
+            //   B_j: O += V_{j-1}^T . P_{j-1}^T for both row blocks (each V^T
+            //        operand read once, used twice)  ||  rb 0's scores / max /
+            //        decision and exponentials of tile j;
+            // so both phases carry one row block's exponentials (one v_exp per
+            // MFMA gap).  The O rescale a decision of tile j-1 asks for is applied
+            // at the start of A_j: after P_{j-2}.V (B_{j-1}), before P_{j-1}.V --
+            // the 8-wave body's order of operations on O and l, so the same bits.
+            // Rings: K_{j+3} and V_{j+1} are issued at B_j (after its barrier)
+            // into the slots of K_j (read in A_j) and V_{j-2} (B_{j-1}); the
+            // wave's mask j+2 after its reads of mask j.  A_j's counted wait leaves
+            // B_{j-1}'s issues in flight: K_{j+1}, V_{j-1} and mask j have landed
+            // (this wave's pieces; B_j's barrier then covers everyone's).
+            static_assert(C::NKI == 4 && C::NMI == 8, "the wait counts below are multiples of 4");
+            constexpr int MI = MM ? C::NMI : 0;
+            // Every tile issues the same DMA instructions (K_{j+3}, V_{j+1}, mask
+            // j+2 at B_j), a tile past the end through an offset past its
+            // descriptor (no traffic; into a slot nothing reads again), so every
+            // counted wait is one constant and the issues sit inside B's steps
+            // without a branch.
+            auto k_piece = [&](int s, int i) {
+                const uint32_t nk = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.k_nb1;
+                const uint32_t dst = lds0 + C::kOff + (s % C::KS) * C::img + (wave + kPf4Waves * i) * 1024;
+                dma<16>(rs.k, dst, s < nt ? nk + koff0 + 64 * i : a.k_span);
             };
-            if constexpr (!F) {
-#pragma unroll
-                for (int v = 0; v < 4; v++) v_read1(v);
+            auto v_piece = [&](int s, int i) {
+                const uint32_t nv = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.v_nb1;
+                const uint32_t dst = lds0 + C::vOff + (s % C::VS) * C::img + (wave + kPf4Waves * i) * 1024;
+                dma<16>(rs.v, dst, s < nt ? nv + voff0 + 64 * i : a.v_span);
+            };
+            // (skip: tile s past the end or a +-0 block, decided once per tile --
+            // inside B's steps a branch would split the phase)
+            auto m_skip = [&](int s) { return s >= nt || zero_of(s); };
+            auto m_piece = [&](int s, int k, bool skip) {
+                if constexpr (MM) {
+                    const uint32_t n2 = (uint32_t)(t0 + s) * kPfKeys * 2;
+                    const uint32_t dst = lds0 + C::mOff + (wave * C::MS + s % C::MS) * C::maskSlot + k * 1024;
+                    dma<16>(rs.m, dst, (skip || moff[k] == a.m_span) ? a.m_span : moff[k] + n2);
+                }
+            };
+            // prologue: K 0 | K 1, mask 0 | K 2, V 0, mask 1 (the last two groups as
+            // the steady state's B_{-2} and B_{-1})
+            if (nt > 0) {
+    #pragma unroll
+                for (int i = 0; i < C::NKI; i++) k_piece(0, i);
+    #pragma unroll
+                for (int i = 0; i < C::NKI; i++) k_piece(1, i);
+    #pragma unroll
+                for (int k = 0; k < C::NMI; k++) m_piece(0, k, m_skip(0));
+    #pragma unroll
+                for (int i = 0; i < C::NKI; i++) k_piece(2, i);
+    #pragma unroll
+                for (int i = 0; i < C::NKI; i++) v_piece(0, i);
+    #pragma unroll
+                for (int k = 0; k < C::NMI; k++) m_piece(1, k, m_skip(1));
             }
-            float tmax0 = kNegInf, nm0 = 0.0f, la0 = 0.0f, lb0 = 0.0f;
-            f16x8 p0n[2][2];
-            const bool mskip = HM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
-            PF4_T(4);
-            __builtin_amdgcn_sched_barrier(0);
-            float tred0 = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 32; i++) {
-                // vector piece: rb 0's scores and max (steps 0-13, two pieces in
-                // steps 0 and 1), the max across the lane pair (14), the rescale
-                // decision (15: a dependent chain, split over two steps), its
-                // exponentials (16-31)
-                if (i < 14) {
-                    if (i < 2) smax_piece(s0, mk0, us0, tmax0, 2 * i);
-                    smax_piece(s0, mk0, us0, tmax0, i < 2 ? 2 * i + 1 : i + 2);
+            // O_rb^T += V_s^T . P_rb^T for both row blocks, each V^T operand read
+            // once; per accumulator the 8-wave body's order (t, q)
+            auto pv2 = [&](int s, const f16x8 (&pa)[2][2], const f16x8 (&pb)[2][2]) {
+                uint32_t b0 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[0];
+                uint32_t b1 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[1];
+                PF4_OPAQUE_V2(b0, b1);
+                lds_u8* const img0 = lsm + b0;
+                lds_u8* const img1 = lsm + b1;
+                // every V^T operand of the tile first (64 VGPRs), so that no MFMA
+                // of the phase waits for its own read
+                f16x8 va[2][2][NDB];
+    #pragma unroll
+                for (int t = 0; t < 2; t++) {
+    #pragma unroll
+                    for (int q = 0; q < 2; q++) {
+    #pragma unroll
+                        for (int db = 0; db < NDB; db++) {
+                            const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
+                            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img1 + off));
+                            const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                            va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
+                        }
+                    }
                 }
-                if (i == 14) {
-                    tred0 = PF4_XOR32(tmax0, true) * cexp;
-                    asm volatile("" : "+v"(tred0));
+    #pragma unroll
+                for (int t = 0; t < 2; t++) {
+    #pragma unroll
+                    for (int q = 0; q < 2; q++) {
+    #pragma unroll
+                        for (int db = 0; db < NDB; db++) {
+                            o[0][db] = mfma32(va[t][q][db], pa[t][q], o[0][db]);
+                            o[1][db] = mfma32(va[t][q][db], pb[t][q], o[1][db]);
+                        }
+                    }
                 }
-                if (i == 15) {
-                    smax_decide(0, tred0, al0, rs0);
-                    nm0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
-                    la0 = l2[0].x;
-                    lb0 = l2[0].y;
-                    asm volatile("" : "+v"(nm0), "+v"(la0), "+v"(lb0));
+            };
+            // K_j's operands, read once per tile at the start of A_j for both row blocks
+            f16x8 kr[2][NK];
+            // (the streamed forms: operand reads placed inside the steps, a few
+            // ahead of their MFMA -- with all of a phase's reads at its head the
+            // 4-bit lgkmcnt cannot name the first one, and the first MFMA waited
+            // for half of them)
+            auto k_base = [&](int s) {
+                uint32_t kb = (uint32_t)(C::kOff + (s % C::KS) * C::img) + kbase;
+                PF4_OPAQUE_V(kb);
+                return kb;
+            };
+            auto k_read1 = [&](uint32_t kb, int t, int kk) {
+                kr[t][kk] = *(const __attribute__((address_space(3))) f16x8*)((const lds_u8*)smem + kb + kk * (kPfKeys * 32) +
+                                                                           t * 1024);
+            };
+            if (nt > 0) {
+                // K 0 landed: everything issued after it may fly
+                wait_vmcnt_c<3 * C::NKI + 2 * MI>();
+                __syncthreads();
+            }
+            float us0[2][16], us1[2][16];
+            float al0 = 1.0f, al1 = 1.0f;
+            bool rs0 = false, rs1 = false;
+            f16x8 p0[2][2], p1[2][2];
+            // (the first tile without rb 1's previous exponentials and without a
+            // P.V: a compile-time flag, so that no branch splits a phase -- a
+            // phase must stay one basic block for its VALU to sit between its MFMAs)
+            // O rescale (a decision of tile j-1: rb 0's made in B_{j-1}, rb 1's in
+            // A_{j-1}, kept as pending through A_j) at the start of B_j, after its
+            // barrier: after P_{j-2}.V, before P_{j-1}.V; in AGPRs (scale_acc16)
+            bool pr1 = false;
+            float pa1 = 1.0f;
+            auto rescale_acc = [&](int rb, bool resc, float alpha) {
+                if (__builtin_expect(resc, 0)) {
+    #pragma unroll
+                    for (int db = 0; db < NDB; db++) scale_acc16(o[rb][db], alpha);
                 }
-                if (i >= 16) sexp_piece(us0, p0n, nm0, la0, lb0, i - 16);
-                if constexpr (!F) {
-                    if (!(i & 1) && i < 24) v_read1((i >> 1) + 4);
-                    const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
-                    o[rb][db] = mfma32(va[t][q][db], rb ? p1[t][q] : p0[t][q], o[rb][db]);
+            };
+            // The phases are written as 32 explicit (MFMA, vector piece) steps, each
+            // its own scheduling region (sched_barrier): hipcc's scheduling groups
+            // left the exponentials behind the MFMA runs (in-order issue then
+            // serialises them).  A vector piece = two elements of one row block:
+            // scores + running max (smax_piece) or exponentials + row sums + f16
+            // pair (sexp_piece) -- the same operations in the same order per row
+            // as smax / sexp, so the same bits.
+            auto smax_piece = [&](const f32x16 (&st)[2], const u32x2 (&mk)[2][4], float (&us)[2][16], float& tmax, int pc) {
+                const int t = pc >> 3, k0 = 2 * (pc & 7);
+    #pragma unroll
+                for (int k = k0; k < k0 + 2; k++) {
+                    float x = st[t][k];
+                    if constexpr (MM) {
+                        const int u = k >> 2, e = k & 3;
+                        const f16x2 mm = as_h2(e < 2 ? mk[t][u].x : mk[t][u].y);
+                        x = fmaf(x, scale, (float)(e & 1 ? mm.y : mm.x));
+                    } else if constexpr (HM) {
+                        x = fmaf(x, scale, 0.0f);  // (a +-0 mask: the masked path's arithmetic, no mask values)
+                    }
+                    us[t][k] = x;
+                    tmax = fmaxf(tmax, x);
                 }
-                // this tile's DMA: K_{j+3} and V_{j+1} pieces in steps 1, 3, ..., 15
-                // (into slots every wave finished before the barrier), mask j+2
-                // in steps 17, 19, ..., 31 (this wave's reads of mask j are
-                // consumed by then)
-                if (i < 16 && (i & 1)) {
-                    if (i & 2) v_piece(j + 1, i >> 2);
-                    else k_piece(j + 3, i >> 2);
-                }
-                if (i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
+                // (the piece's results through a volatile asm: volatile asm statements
+                // keep their order, so the piece is computed in its step -- the
+                // instruction selector otherwise places side-effect-free VALU next to
+                // its last use, past every step)
+                asm volatile("" : "+v"(tmax), "+v"(us[t][k0]), "+v"(us[t][k0 + 1]));
+            };
+            // (the rescale decision from the lane pair's max, log2 units)
+            auto smax_decide = [&](int rb, float tmax, float& alpha, bool& resc) {
+                resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
+                const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
+                alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
+                m_run[rb] = m_new;
+                l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
+            };
+            auto smax_final = [&](int rb, float tmax, float& alpha, bool& resc) {
+                tmax = PF4_XOR32(tmax, true) * cexp;
+                resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
+                const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
+                alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
+                m_run[rb] = m_new;
+                l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
+            };
+            auto sexp_piece = [&](const float (&us)[2][16], f16x8 (&pb)[2][2], float nm, float& la, float& lb, int pc) {
+                const int t = pc >> 3, k = 2 * (pc & 7);
+                const float pa = __builtin_amdgcn_exp2f(fmaf(us[t][k], cexp, nm));
+                const float pq = __builtin_amdgcn_exp2f(fmaf(us[t][k + 1], cexp, nm));
+                la = add_f32(la, pa);
+                lb = add_f32(lb, pq);
+                pb[t][k >> 3][k & 7] = (f16)pa;
+                pb[t][k >> 3][(k & 7) + 1] = (f16)pq;
+                asm volatile("" : "+v"(la), "+v"(lb));  // (see smax_piece)
+            };
+    #ifdef FATTN_STAMPS
+            // diagnostic build only (tools/pf_stamps.py): shader-clock cycles per
+            // phase part, summed over tiles (0 A's wait, 1 A's steps, 2 A's tail,
+            // 3 B's barrier, 4 B's head -- rescale, V^T reads --, 5 B's steps, 6 B's
+            // tail, 7 between tiles)
+            uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            uint64_t t_prev = __builtin_amdgcn_s_memtime();
+    #define PF4_T(k)                                              \
+        do {                                                      \
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+            ph[k] += t_ - t_prev;                                 \
+            t_prev = t_;                                          \
+        } while (0)
+    #else
+    #define PF4_T(k) do { } while (0)
+    #endif
+            auto iter = [&](int j, auto first) {
+                constexpr bool F = decltype(first)::value;
+                PF4_T(7);
+                // ---- A_j: S_j for rb 1 (steps 0-15) and rb 0 (16-31); rb 1's
+                // exponentials of tile j-1 beside steps 0-15, its scores and max of
+                // tile j beside 16-31 (its S chains done by then)
+                wait_vmcnt_c<2 * C::NKI + MI>();  // B_{j-1}'s issues may fly
+                PF4_T(0);
+                pr1 = rs1;  // rb 1's decision of tile j-1, applied at B_j
+                pa1 = al1;
+                u32x2 mk1[2][4], mk0[2][4];
+                const uint32_t kb = k_base(j);
+    #pragma unroll
+                for (int kk = 0; kk < 4; kk++) k_read1(kb, 0, kk);  // the rest: 4 steps ahead, in the steps
+                const float nm1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];
+                float la1 = l2[1].x, lb1 = l2[1].y, tmax1 = kNegInf;
                 __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+                // (each step: its vector piece first -- issued while the previous
+                // step's MFMA runs, and at the phase's head while the first operand
+                // reads land -- then its MFMA)
+                for (int i = 0; i < 32; i++) {
+                    const int t = (i >> 3) & 1, kk = i & 7;
+                    if (i < 12) k_read1(kb, (i + 4) >> 3, (i + 4) & 7);
+                    if constexpr (MM) {
+                        if (i == 8) mask_reads(j, 1, mk1);   // (for rb 1's scores, steps 16+)
+                        if (i == 14) mask_reads(j, 0, mk0);  // (for B_j: this wave's slot, no barrier needed)
+                    }
+                    if (i < 16) {
+                        if constexpr (!F) sexp_piece(us1, p1, nm1, la1, lb1, i);
+                        if (kk == 0) s1[t] = f32x16{};
+                        s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
+                    } else {
+                        // (S1's subtile-0 chain ended at step 7, subtile 1's at 15)
+                        smax_piece(s1, mk1, us1, tmax1, i - 16);
+                        if (kk == 0) s0[t] = f32x16{};
+                        s0[t] = mfma32(kr[t][kk], qop[0][kk], s0[t]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                PF4_T(1);
+                if constexpr (!F) l2[1] = f32x2{la1, lb1};
+                smax_final(1, tmax1, al1, rs1);
+                // (the phase's results pinned here: hipcc's machine sinking would
+                // otherwise move their exponentials next to their uses in B)
+                if constexpr (!F) pin_p(p1);
+                pin16(us1[0]);
+                pin16(us1[1]);
+                PF4_T(2);
+                // ---- B_j: P_{j-1}.V for both row blocks (each V^T operand read
+                // once); rb 0's scores and max of tile j beside steps 0-15, its
+                // exponentials beside 16-31
+                __syncthreads();
+                PF4_T(3);
+                rescale_acc(0, rs0, al0);  // decisions of tile j-1
+                rescale_acc(1, pr1, pa1);
+                // V^T operands streamed: operand v (= the MFMAs of steps 2v, 2v+1)
+                // read 4 operands (8 steps) ahead
+                f16x8 va[2][2][NDB];
+                uint32_t vb0 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[0];
+                uint32_t vb1 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[1];
+                PF4_OPAQUE_V2(vb0, vb1);
+                auto v_read1 = [&](int v) {
+                    const int t = v >> 3, q = (v >> 2) & 1, db = v & 3;
+                    const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb0 + off));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb1 + off));
+                    const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                    va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
+                };
+                if constexpr (!F) {
+    #pragma unroll
+                    for (int v = 0; v < 4; v++) v_read1(v);
+                }
+                float tmax0 = kNegInf, nm0 = 0.0f, la0 = 0.0f, lb0 = 0.0f;
+                f16x8 p0n[2][2];
+                const bool mskip = MM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
+                PF4_T(4);
+                __builtin_amdgcn_sched_barrier(0);
+                float tred0 = 0.0f;
+    #pragma unroll
+                for (int i = 0; i < 32; i++) {
+                    // vector piece: rb 0's scores and max (steps 0-13, two pieces in
+                    // steps 0 and 1), the max across the lane pair (14), the rescale
+                    // decision (15: a dependent chain, split over two steps), its
+                    // exponentials (16-31)
+                    if (i < 14) {
+                        if (i < 2) smax_piece(s0, mk0, us0, tmax0, 2 * i);
+                        smax_piece(s0, mk0, us0, tmax0, i < 2 ? 2 * i + 1 : i + 2);
+                    }
+                    if (i == 14) {
+                        tred0 = PF4_XOR32(tmax0, true) * cexp;
+                        asm volatile("" : "+v"(tred0));
+                    }
+                    if (i == 15) {
+                        smax_decide(0, tred0, al0, rs0);
+                        nm0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
+                        la0 = l2[0].x;
+                        lb0 = l2[0].y;
+                        asm volatile("" : "+v"(nm0), "+v"(la0), "+v"(lb0));
+                    }
+                    if (i >= 16) sexp_piece(us0, p0n, nm0, la0, lb0, i - 16);
+                    if constexpr (!F) {
+                        if (!(i & 1) && i < 24) v_read1((i >> 1) + 4);
+                        const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
+                        o[rb][db] = mfma32(va[t][q][db], rb ? p1[t][q] : p0[t][q], o[rb][db]);
+                    }
+                    // this tile's DMA: K_{j+3} and V_{j+1} pieces in steps 1, 3, ..., 15
+                    // (into slots every wave finished before the barrier), mask j+2
+                    // in steps 17, 19, ..., 31 (this wave's reads of mask j are
+                    // consumed by then)
+                    if (i < 16 && (i & 1)) {
+                        if (i & 2) v_piece(j + 1, i >> 2);
+                        else k_piece(j + 3, i >> 2);
+                    }
+                    if (i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                PF4_T(5);
+                l2[0] = f32x2{la0, lb0};
+                pin_p(p0n);
+    #pragma unroll
+                for (int t = 0; t < 2; t++) {
+    #pragma unroll
+                    for (int q = 0; q < 2; q++) p0[t][q] = p0n[t][q];
+                }
+                PF4_T(6);
+            };
+            if (nt > 0) iter(0, std::true_type());
+            for (int j = 1; j < nt; j++) iter(j, std::false_type());
+            if (nt > 0) {
+                // ---- A_nt, B_nt: rb 1's exponentials of the last tile, its P.V
+                wait_vmcnt_c<0>();
+                sexp(1, 0, us1, p1);
+                sexp(1, 1, us1, p1);
+                __syncthreads();  // every wave's pieces of V nt-1 landed
+                rescale_acc(0, rs0, al0);
+                rescale_acc(1, rs1, al1);
+                pv2(nt - 1, p0, p1);
             }
-            PF4_T(5);
-            l2[0] = f32x2{la0, lb0};
-            pin_p(p0n);
-#pragma unroll
-            for (int t = 0; t < 2; t++) {
-#pragma unroll
-                for (int q = 0; q < 2; q++) p0[t][q] = p0n[t][q];
+    #ifdef FATTN_STAMPS
+            if (lane == 0 && g_stamps) {
+                const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+                for (int k = 0; k < 8; k++) g_stamps[(blk * kPfWaves + wave) * 16 + k] = ph[k];
+                g_stamps[(blk * kPfWaves + wave) * 16 + 8] = (unsigned long long)nt;
             }
-            PF4_T(6);
+    #endif
+    #undef PF4_T
         };
-        if (nt > 0) iter(0, std::true_type());
-        for (int j = 1; j < nt; j++) iter(j, std::false_type());
-        if (nt > 0) {
-            // ---- A_nt, B_nt: rb 1's exponentials of the last tile, its P.V
-            wait_vmcnt_c<0>();
-            sexp(1, 0, us1, p1);
-            sexp(1, 1, us1, p1);
-            __syncthreads();  // every wave's pieces of V nt-1 landed
-            rescale_acc(0, rs0, al0);
-            rescale_acc(1, rs1, al1);
-            pv2(nt - 1, p0, p1);
+        if constexpr (HM) {
+            if (__builtin_amdgcn_readfirstlane(all_zero ? 1 : 0)) body2(std::true_type());
+            else body2(std::false_type());
+        } else {
+            body2(std::false_type());
         }
-#ifdef FATTN_STAMPS
-        if (lane == 0 && g_stamps) {
-            const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-            for (int k = 0; k < 8; k++) g_stamps[(blk * kPfWaves + wave) * 16 + k] = ph[k];
-            g_stamps[(blk * kPfWaves + wave) * 16 + 8] = (unsigned long long)nt;
-        }
-#endif
-#undef PF4_T
     } else {
         // the rebalanced schedule (see the kernel's comment)
         float us0[2][16], us1[2][16];

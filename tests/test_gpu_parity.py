@@ -656,7 +656,8 @@ def pf_force(request):
     dict(kv_type="q8_0", NQ=256, H=2, Hkv=2, N=1024, mask="random", extreme=True),     # rescales
     dict(kv_type="f16", NQ=256, H=2, Hkv=2, N=128, mask="random"),            # two tiles (prologue paths)
     dict(kv_type="f16", NQ=256, H=2, Hkv=2, N=64, mask="random"),             # one tile
-], ids=["f16", "q8_causal_gqa", "q4_nomask_ragged", "f16_seq2_pos", "q8_extreme", "two_tiles", "one_tile"])
+    dict(kv_type="q8_0", NQ=300, H=2, Hkv=2, N=512, mask="zero"),             # +-0 mask: the ZM body
+], ids=["f16", "q8_causal_gqa", "q4_nomask_ragged", "f16_seq2_pos", "q8_extreme", "two_tiles", "one_tile", "q8_zero_mask"])
 def test_pf4_bit_identical_to_pf(dev, case):
     """The one-wave-per-SIMD prefill body (fattn_pf4_kernel) runs the 8-wave
     body's arithmetic in the same order -- per 64-key tile the same S^T
