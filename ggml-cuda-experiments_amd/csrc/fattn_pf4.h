@@ -639,17 +639,17 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             // prologue: K 0 | K 1, mask 0 | K 2, V 0, mask 1 (the last two groups as
             // the steady state's B_{-2} and B_{-1})
             if (nt > 0) {
-    #pragma unroll
+#pragma unroll
                 for (int i = 0; i < C::NKI; i++) k_piece(0, i);
-    #pragma unroll
+#pragma unroll
                 for (int i = 0; i < C::NKI; i++) k_piece(1, i);
-    #pragma unroll
+#pragma unroll
                 for (int k = 0; k < C::NMI; k++) m_piece(0, k, m_skip(0));
-    #pragma unroll
+#pragma unroll
                 for (int i = 0; i < C::NKI; i++) k_piece(2, i);
-    #pragma unroll
+#pragma unroll
                 for (int i = 0; i < C::NKI; i++) v_piece(0, i);
-    #pragma unroll
+#pragma unroll
                 for (int k = 0; k < C::NMI; k++) m_piece(1, k, m_skip(1));
             }
             // O_rb^T += V_s^T . P_rb^T for both row blocks, each V^T operand read
@@ -663,11 +663,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 // every V^T operand of the tile first (64 VGPRs), so that no MFMA
                 // of the phase waits for its own read
                 f16x8 va[2][2][NDB];
-    #pragma unroll
+#pragma unroll
                 for (int t = 0; t < 2; t++) {
-    #pragma unroll
+#pragma unroll
                     for (int q = 0; q < 2; q++) {
-    #pragma unroll
+#pragma unroll
                         for (int db = 0; db < NDB; db++) {
                             const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
                             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
@@ -677,11 +677,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                         }
                     }
                 }
-    #pragma unroll
+#pragma unroll
                 for (int t = 0; t < 2; t++) {
-    #pragma unroll
+#pragma unroll
                     for (int q = 0; q < 2; q++) {
-    #pragma unroll
+#pragma unroll
                         for (int db = 0; db < NDB; db++) {
                             o[0][db] = mfma32(va[t][q][db], pa[t][q], o[0][db]);
                             o[1][db] = mfma32(va[t][q][db], pb[t][q], o[1][db]);
@@ -723,7 +723,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             float pa1 = 1.0f;
             auto rescale_acc = [&](int rb, bool resc, float alpha) {
                 if (__builtin_expect(resc, 0)) {
-    #pragma unroll
+#pragma unroll
                     for (int db = 0; db < NDB; db++) scale_acc16(o[rb][db], alpha);
                 }
             };
@@ -734,27 +734,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             // scores + running max (smax_piece) or exponentials + row sums + f16
             // pair (sexp_piece) -- the same operations in the same order per row
             // as smax / sexp, so the same bits.
-            auto smax_piece = [&](const f32x16 (&st)[2], const u32x2 (&mk)[2][4], float (&us)[2][16], float& tmax, int pc) {
-                const int t = pc >> 3, k0 = 2 * (pc & 7);
-    #pragma unroll
-                for (int k = k0; k < k0 + 2; k++) {
-                    float x = st[t][k];
-                    if constexpr (MM) {
-                        const int u = k >> 2, e = k & 3;
-                        const f16x2 mm = as_h2(e < 2 ? mk[t][u].x : mk[t][u].y);
-                        x = fmaf(x, scale, (float)(e & 1 ? mm.y : mm.x));
-                    } else if constexpr (HM) {
-                        x = fmaf(x, scale, 0.0f);  // (a +-0 mask: the masked path's arithmetic, no mask values)
-                    }
-                    us[t][k] = x;
-                    tmax = fmaxf(tmax, x);
-                }
-                // (the piece's results through a volatile asm: volatile asm statements
-                // keep their order, so the piece is computed in its step -- the
-                // instruction selector otherwise places side-effect-free VALU next to
-                // its last use, past every step)
-                asm volatile("" : "+v"(tmax), "+v"(us[t][k0]), "+v"(us[t][k0 + 1]));
-            };
             // (the rescale decision from the lane pair's max, log2 units)
             auto smax_decide = [&](int rb, float tmax, float& alpha, bool& resc) {
                 resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
@@ -771,15 +750,58 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 m_run[rb] = m_new;
                 l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
             };
-            auto sexp_piece = [&](const float (&us)[2][16], f16x8 (&pb)[2][2], float nm, float& la, float& lb, int pc) {
+            // Staged forms of the pieces: a piece's three dependent instruction
+            // groups in three consecutive steps (its exponent arguments, its
+            // exponentials, its sums and f16 pair; its accumulator reads, its
+            // scores, its max), so that no step waits on its own results --
+            // each stage's results pinned into its step like the pieces'.
+            float sA[16][2], sE[16][2], mX[16][2];
+            auto e1 = [&](const float (&us)[2][16], float nm, int pc) {
                 const int t = pc >> 3, k = 2 * (pc & 7);
-                const float pa = __builtin_amdgcn_exp2f(fmaf(us[t][k], cexp, nm));
-                const float pq = __builtin_amdgcn_exp2f(fmaf(us[t][k + 1], cexp, nm));
-                la = add_f32(la, pa);
-                lb = add_f32(lb, pq);
-                pb[t][k >> 3][k & 7] = (f16)pa;
-                pb[t][k >> 3][(k & 7) + 1] = (f16)pq;
-                asm volatile("" : "+v"(la), "+v"(lb));  // (see smax_piece)
+                sA[pc][0] = fmaf(us[t][k], cexp, nm);
+                sA[pc][1] = fmaf(us[t][k + 1], cexp, nm);
+                asm volatile("" : "+v"(sA[pc][0]), "+v"(sA[pc][1]));
+            };
+            auto e2 = [&](int pc) {
+                sE[pc][0] = __builtin_amdgcn_exp2f(sA[pc][0]);
+                sE[pc][1] = __builtin_amdgcn_exp2f(sA[pc][1]);
+                asm volatile("" : "+v"(sE[pc][0]), "+v"(sE[pc][1]));
+            };
+            auto e3 = [&](f16x8 (&pb)[2][2], float& la, float& lb, int pc) {
+                const int t = pc >> 3, k = 2 * (pc & 7);
+                la = add_f32(la, sE[pc][0]);
+                lb = add_f32(lb, sE[pc][1]);
+                pb[t][k >> 3][k & 7] = (f16)sE[pc][0];
+                pb[t][k >> 3][(k & 7) + 1] = (f16)sE[pc][1];
+                asm volatile("" : "+v"(la), "+v"(lb));
+            };
+            auto m1 = [&](const f32x16 (&st)[2], int pc) {
+                const int t = pc >> 3, k = 2 * (pc & 7);
+                mX[pc][0] = st[t][k];
+                mX[pc][1] = st[t][k + 1];
+                asm volatile("" : "+v"(mX[pc][0]), "+v"(mX[pc][1]));
+            };
+            auto m2 = [&](const u32x2 (&mk)[2][4], float (&us)[2][16], int pc) {
+                const int t = pc >> 3, k0 = 2 * (pc & 7);
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const int k = k0 + e;
+                    float x = mX[pc][e];
+                    if constexpr (MM) {
+                        const int u = k >> 2, ee = k & 3;
+                        const f16x2 mm = as_h2(ee < 2 ? mk[t][u].x : mk[t][u].y);
+                        x = fmaf(x, scale, (float)(ee & 1 ? mm.y : mm.x));
+                    } else if constexpr (HM) {
+                        x = fmaf(x, scale, 0.0f);
+                    }
+                    us[t][k] = x;
+                }
+                asm volatile("" : "+v"(us[t][k0]), "+v"(us[t][k0 + 1]));
+            };
+            auto m3 = [&](const float (&us)[2][16], float& tmax, int pc) {
+                const int t = pc >> 3, k = 2 * (pc & 7);
+                tmax = fmaxf(fmaxf(tmax, us[t][k]), us[t][k + 1]);
+                asm volatile("" : "+v"(tmax));
             };
     #ifdef FATTN_STAMPS
             // diagnostic build only (tools/pf_stamps.py): shader-clock cycles per
@@ -809,15 +831,17 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 pa1 = al1;
                 u32x2 mk1[2][4], mk0[2][4];
                 const uint32_t kb = k_base(j);
-    #pragma unroll
+#pragma unroll
                 for (int kk = 0; kk < 4; kk++) k_read1(kb, 0, kk);  // the rest: 4 steps ahead, in the steps
                 const float nm1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];
                 float la1 = l2[1].x, lb1 = l2[1].y, tmax1 = kNegInf;
+                if constexpr (!F) e1(us1, nm1, 0);
                 __builtin_amdgcn_sched_barrier(0);
-    #pragma unroll
-                // (each step: its vector piece first -- issued while the previous
-                // step's MFMA runs, and at the phase's head while the first operand
-                // reads land -- then its MFMA)
+                // steps: rb 1's exponentials of tile j-1 (piece p: stages at steps
+                // p-1, p, p+1), its scores and max of tile j (piece p: 15+p, 16+p,
+                // 17+p -- S1's subtile-0 chain ended at step 7, subtile 1's at 15);
+                // then the step's MFMA
+#pragma unroll
                 for (int i = 0; i < 32; i++) {
                     const int t = (i >> 3) & 1, kk = i & 7;
                     if (i < 12) k_read1(kb, (i + 4) >> 3, (i + 4) & 7);
@@ -825,18 +849,24 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                         if (i == 8) mask_reads(j, 1, mk1);   // (for rb 1's scores, steps 16+)
                         if (i == 14) mask_reads(j, 0, mk0);  // (for B_j: this wave's slot, no barrier needed)
                     }
+                    if constexpr (!F) {
+                        if (i >= 1 && i <= 16) e3(p1, la1, lb1, i - 1);
+                        if (i <= 15) e2(i);
+                        if (i <= 14) e1(us1, nm1, i + 1);
+                    }
+                    if (i >= 17) m3(us1, tmax1, i - 17);
+                    if (i >= 16) m2(mk1, us1, i - 16);
+                    if (i >= 15 && i <= 30) m1(s1, i - 15);
                     if (i < 16) {
-                        if constexpr (!F) sexp_piece(us1, p1, nm1, la1, lb1, i);
                         if (kk == 0) s1[t] = f32x16{};
                         s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
                     } else {
-                        // (S1's subtile-0 chain ended at step 7, subtile 1's at 15)
-                        smax_piece(s1, mk1, us1, tmax1, i - 16);
                         if (kk == 0) s0[t] = f32x16{};
                         s0[t] = mfma32(kr[t][kk], qop[0][kk], s0[t]);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
+                m3(us1, tmax1, 15);
                 PF4_T(1);
                 if constexpr (!F) l2[1] = f32x2{la1, lb1};
                 smax_final(1, tmax1, al1, rs1);
@@ -868,7 +898,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
                 };
                 if constexpr (!F) {
-    #pragma unroll
+#pragma unroll
                     for (int v = 0; v < 4; v++) v_read1(v);
                 }
                 float tmax0 = kNegInf, nm0 = 0.0f, la0 = 0.0f, lb0 = 0.0f;
@@ -877,28 +907,37 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 PF4_T(4);
                 __builtin_amdgcn_sched_barrier(0);
                 float tred0 = 0.0f;
-    #pragma unroll
+                // steps: rb 0's scores and max (piece p at slot s(p) = p / 2 for
+                // p < 8, p - 4 after: stages at s-1, s, s+1), the max across the
+                // lane pair (13), the rescale decision (14), the exponentials
+                // (piece p: 15+p, 16+p, 17+p; the last ones after the loop); then
+                // the step's MFMA, operand reads and DMA
+                auto slot0 = [](int p) { return p < 8 ? p >> 1 : p - 4; };
+                m1(s0, 0);
+                m1(s0, 1);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
                 for (int i = 0; i < 32; i++) {
-                    // vector piece: rb 0's scores and max (steps 0-13, two pieces in
-                    // steps 0 and 1), the max across the lane pair (14), the rescale
-                    // decision (15: a dependent chain, split over two steps), its
-                    // exponentials (16-31)
-                    if (i < 14) {
-                        if (i < 2) smax_piece(s0, mk0, us0, tmax0, 2 * i);
-                        smax_piece(s0, mk0, us0, tmax0, i < 2 ? 2 * i + 1 : i + 2);
+#pragma unroll
+                    for (int p = 0; p < 16; p++) {
+                        if (slot0(p) + 1 == i) m3(us0, tmax0, p);
+                        if (slot0(p) == i) m2(mk0, us0, p);
+                        if (slot0(p) - 1 == i) m1(s0, p);
                     }
-                    if (i == 14) {
+                    if (i == 13) {
                         tred0 = PF4_XOR32(tmax0, true) * cexp;
                         asm volatile("" : "+v"(tred0));
                     }
-                    if (i == 15) {
+                    if (i == 14) {
                         smax_decide(0, tred0, al0, rs0);
                         nm0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
                         la0 = l2[0].x;
                         lb0 = l2[0].y;
                         asm volatile("" : "+v"(nm0), "+v"(la0), "+v"(lb0));
                     }
-                    if (i >= 16) sexp_piece(us0, p0n, nm0, la0, lb0, i - 16);
+                    if (i >= 17) e3(p0n, la0, lb0, i - 17);
+                    if (i >= 16) e2(i - 16);
+                    if (i >= 15 && i <= 30) e1(us0, nm0, i - 15);
                     if constexpr (!F) {
                         if (!(i & 1) && i < 24) v_read1((i >> 1) + 4);
                         const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
@@ -915,12 +954,13 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     if (i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
                     __builtin_amdgcn_sched_barrier(0);
                 }
+                e3(p0n, la0, lb0, 15);  // (piece 15's last stage, after the loop)
                 PF4_T(5);
                 l2[0] = f32x2{la0, lb0};
                 pin_p(p0n);
-    #pragma unroll
+#pragma unroll
                 for (int t = 0; t < 2; t++) {
-    #pragma unroll
+#pragma unroll
                     for (int q = 0; q < 2; q++) p0[t][q] = p0n[t][q];
                 }
                 PF4_T(6);
