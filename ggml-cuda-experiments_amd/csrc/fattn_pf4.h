@@ -604,11 +604,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             // MFMA gap).  The O rescale a decision of tile j-1 asks for is applied
             // at the start of A_j: after P_{j-2}.V (B_{j-1}), before P_{j-1}.V --
             // the 8-wave body's order of operations on O and l, so the same bits.
-            // Rings: K_{j+3} and V_{j+1} are issued at B_j (after its barrier)
-            // into the slots of K_j (read in A_j) and V_{j-2} (B_{j-1}); the
-            // wave's mask j+2 after its reads of mask j.  A_j's counted wait leaves
-            // B_{j-1}'s issues in flight: K_{j+1}, V_{j-1} and mask j have landed
-            // (this wave's pieces; B_j's barrier then covers everyone's).
+            // Rings: V_j is issued in A_j (into V_{j-3}'s slot), K_{j+3} in B_j
+            // (after its barrier, into K_j's slot), the wave's mask j+2 in B_j
+            // after its reads of mask j.  A_j's counted wait leaves B_{j-1}'s
+            // issues in flight: K_{j+1}, V_{j-1} and mask j have landed (this
+            // wave's pieces; B_j's barrier then covers everyone's).
             static_assert(C::NKI == 4 && C::NMI == 8, "the wait counts below are multiples of 4");
             constexpr int MI = MM ? C::NMI : 0;
             // Every tile issues the same DMA instructions (K_{j+3}, V_{j+1}, mask
@@ -636,8 +636,8 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     dma<16>(rs.m, dst, (skip || moff[k] == a.m_span) ? a.m_span : moff[k] + n2);
                 }
             };
-            // prologue: K 0 | K 1, mask 0 | K 2, V 0, mask 1 (the last two groups as
-            // the steady state's B_{-2} and B_{-1})
+            // prologue: K 0 | K 1, mask 0 | K 2, mask 1 (the last two groups as
+            // the steady state's B_{-2} and B_{-1}; V 0 comes in A_0)
             if (nt > 0) {
 #pragma unroll
                 for (int i = 0; i < C::NKI; i++) k_piece(0, i);
@@ -647,8 +647,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 for (int k = 0; k < C::NMI; k++) m_piece(0, k, m_skip(0));
 #pragma unroll
                 for (int i = 0; i < C::NKI; i++) k_piece(2, i);
-#pragma unroll
-                for (int i = 0; i < C::NKI; i++) v_piece(0, i);
 #pragma unroll
                 for (int k = 0; k < C::NMI; k++) m_piece(1, k, m_skip(1));
             }
@@ -706,7 +704,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             };
             if (nt > 0) {
                 // K 0 landed: everything issued after it may fly
-                wait_vmcnt_c<3 * C::NKI + 2 * MI>();
+                wait_vmcnt_c<2 * C::NKI + 2 * MI>();
                 __syncthreads();
             }
             float us0[2][16], us1[2][16];
@@ -825,7 +823,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 // ---- A_j: S_j for rb 1 (steps 0-15) and rb 0 (16-31); rb 1's
                 // exponentials of tile j-1 beside steps 0-15, its scores and max of
                 // tile j beside 16-31 (its S chains done by then)
-                wait_vmcnt_c<2 * C::NKI + MI>();  // B_{j-1}'s issues may fly
+                wait_vmcnt_c<C::NKI + MI>();  // B_{j-1}'s issues (K_{j+2}, mask j+1) may fly
                 PF4_T(0);
                 pr1 = rs1;  // rb 1's decision of tile j-1, applied at B_j
                 pa1 = al1;
@@ -845,6 +843,9 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 for (int i = 0; i < 32; i++) {
                     const int t = (i >> 3) & 1, kk = i & 7;
                     if (i < 12) k_read1(kb, (i + 4) >> 3, (i + 4) & 7);
+                    // V_j's DMA (into V_{j-3}'s slot, read in B_{j-2}; needed at B_{j+1}):
+                    // the other half of the tile's issue cost beside A's MFMAs
+                    if (i < 16 && (i & 3) == 1) v_piece(j, i >> 2);
                     if constexpr (MM) {
                         if (i == 8) mask_reads(j, 1, mk1);   // (for rb 1's scores, steps 16+)
                         if (i == 14) mask_reads(j, 0, mk0);  // (for B_j: this wave's slot, no barrier needed)
@@ -947,10 +948,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     // (into slots every wave finished before the barrier), mask j+2
                     // in steps 17, 19, ..., 31 (this wave's reads of mask j are
                     // consumed by then)
-                    if (i < 16 && (i & 1)) {
-                        if (i & 2) v_piece(j + 1, i >> 2);
-                        else k_piece(j + 3, i >> 2);
-                    }
+                    if (i < 16 && (i & 3) == 1) k_piece(j + 3, i >> 2);  // (K_{j+3} into K_j's slot; V_j went in A_j)
                     if (i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
                     __builtin_amdgcn_sched_barrier(0);
                 }
