@@ -10,6 +10,10 @@
       tagged with the workload, the plan (describe string) and the kernel
       source hash of the bench.py JSON line of the same command (bench.py
       reads a traffic file back only when all three match)
+  --kernel a,b,c --sum-kernels
+      several kernels of one launch (the staged prefill: kv_stage_f16,
+      pf_mask_flags_kernel, the prefill body): per counter the sum over the
+      kernels of each one's mean per dispatch
   --mfma
       MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMDs x CUs x cycles),
       cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums it over the 8 XCDs)
@@ -22,16 +26,19 @@ import sys
 from collections import defaultdict
 
 
-def load(paths, kernel):
-    vals = defaultdict(list)  # counter -> per-dispatch values
+def load(paths, kernel, per_kernel=False):
+    """counter -> per-dispatch values (per_kernel: (kernel name, counter) -> values)"""
+    vals = defaultdict(list)
     names = set()
+    pats = kernel.split(",")
     for p in paths:
         with open(p, newline="") as f:
             for row in csv.DictReader(f):
-                if kernel not in row["Kernel_Name"]:
+                if not any(k in row["Kernel_Name"] for k in pats):
                     continue
                 names.add(row["Kernel_Name"])
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+                key = (row["Kernel_Name"], row["Counter_Name"]) if per_kernel else row["Counter_Name"]
+                vals[key].append(float(row["Counter_Value"]))
     return vals, sorted(names)
 
 
@@ -44,14 +51,26 @@ def main():
     ap.add_argument("--bench-line", default="", help="log holding the bench.py JSON line of the profiled command")
     ap.add_argument("--command", default="")
     ap.add_argument("--mfma", action="store_true")
+    ap.add_argument("--sum-kernels", action="store_true", help="sum the per-kernel means (several kernels per launch)")
     ap.add_argument("--cus", type=int, default=256)
     ap.add_argument("csv", nargs="+")
     a = ap.parse_args()
-    vals, names = load(a.csv, a.kernel)
+    vals, names = load(a.csv, a.kernel, per_kernel=a.sum_kernels)
     if not vals:
         sys.exit(f"no dispatch of a kernel matching {a.kernel!r}")
-    summ = {c: {"dispatches": len(v), "mean": statistics.fmean(v), "min": min(v), "max": max(v)}
-            for c, v in sorted(vals.items())}
+    if a.sum_kernels:
+        per = {}
+        for (kn, c), v in sorted(vals.items()):
+            print(f"  {kn[:70]:70s} {c:16s} n={len(v):4d} mean={statistics.fmean(v):.6g}")
+            d = per.setdefault(c, {"dispatches": 0, "mean": 0.0, "min": 0.0, "max": 0.0})
+            d["dispatches"] += len(v)
+            d["mean"] += statistics.fmean(v)
+            d["min"] += min(v)
+            d["max"] += max(v)
+        summ = per
+    else:
+        summ = {c: {"dispatches": len(v), "mean": statistics.fmean(v), "min": min(v), "max": max(v)}
+                for c, v in sorted(vals.items())}
     print("kernels:", "; ".join(names))
     for c, s in summ.items():
         print(f"{c:32s} n={s['dispatches']:5d} mean={s['mean']:.6g} min={s['min']:.6g} max={s['max']:.6g}")
