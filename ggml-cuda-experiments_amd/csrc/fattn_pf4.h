@@ -827,6 +827,20 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 PF4_T(0);
                 pr1 = rs1;  // rb 1's decision of tile j-1, applied at B_j
                 pa1 = al1;
+                // V_{j-1}^T operands for B_j, streamed: operand v (= B's MFMAs of
+                // steps 2v, 2v+1); the first four read in A_j after its barrier
+                f16x8 va[2][2][NDB];
+                uint32_t vb0 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[0];
+                uint32_t vb1 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[1];
+                PF4_OPAQUE_V2(vb0, vb1);
+                auto v_read1 = [&](int v) {
+                    const int t = v >> 3, q = (v >> 2) & 1, db = v & 3;
+                    const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb0 + off));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb1 + off));
+                    const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                    va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
+                };
                 u32x2 mk1[2][4], mk0[2][4];
                 const uint32_t kb = k_base(j);
 #pragma unroll
@@ -843,6 +857,14 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 for (int i = 0; i < 32; i++) {
                     const int t = (i >> 3) & 1, kk = i & 7;
                     if (i < 12) k_read1(kb, (i + 4) >> 3, (i + 4) & 7);
+                    // the tile's one barrier, mid-A (this wave's K_j reads were
+                    // all issued by step 11 and are consumed by step 12's MFMA):
+                    // every wave is then past its A_j wait -- V_{j-1}, K_{j+1} and
+                    // mask j complete for all -- and done with K_j and V_{j-2}
+                    if (i == 12) __syncthreads();
+                    if constexpr (!F) {
+                        if (i >= 24 && !(i & 1)) v_read1((i - 24) >> 1);  // (after the barrier)
+                    }
                     // V_j's DMA (into V_{j-3}'s slot, read in B_{j-2}; needed at B_{j+1}):
                     // the other half of the tile's issue cost beside A's MFMAs
                     if (i < 16 && (i & 3) == 1) v_piece(j, i >> 2);
@@ -880,28 +902,9 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 // ---- B_j: P_{j-1}.V for both row blocks (each V^T operand read
                 // once); rb 0's scores and max of tile j beside steps 0-15, its
                 // exponentials beside 16-31
-                __syncthreads();
                 PF4_T(3);
                 rescale_acc(0, rs0, al0);  // decisions of tile j-1
                 rescale_acc(1, pr1, pa1);
-                // V^T operands streamed: operand v (= the MFMAs of steps 2v, 2v+1)
-                // read 4 operands (8 steps) ahead
-                f16x8 va[2][2][NDB];
-                uint32_t vb0 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[0];
-                uint32_t vb1 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[1];
-                PF4_OPAQUE_V2(vb0, vb1);
-                auto v_read1 = [&](int v) {
-                    const int t = v >> 3, q = (v >> 2) & 1, db = v & 3;
-                    const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
-                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb0 + off));
-                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb1 + off));
-                    const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
-                    va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
-                };
-                if constexpr (!F) {
-#pragma unroll
-                    for (int v = 0; v < 4; v++) v_read1(v);
-                }
                 float tmax0 = kNegInf, nm0 = 0.0f, la0 = 0.0f, lb0 = 0.0f;
                 f16x8 p0n[2][2];
                 const bool mskip = MM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
