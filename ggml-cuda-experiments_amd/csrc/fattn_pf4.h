@@ -714,13 +714,16 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             // (the first tile without rb 1's previous exponentials and without a
             // P.V: a compile-time flag, so that no branch splits a phase -- a
             // phase must stay one basic block for its VALU to sit between its MFMAs)
-            // O rescale (a decision of tile j-1: rb 0's made in B_{j-1}, rb 1's in
-            // A_{j-1}, kept as pending through A_j) at the start of B_j, after its
-            // barrier: after P_{j-2}.V, before P_{j-1}.V; in AGPRs (scale_acc16)
-            bool pr1 = false;
-            float pa1 = 1.0f;
+            // O rescale (the decisions of tile j, both made in B_j) at the end of
+            // B_j: after P_{j-1}.V, before P_j.V (B_{j+1}); in AGPRs (scale_acc16).
+            // There only O is live in AGPRs -- at B_j's start (the old place) S0
+            // was, and the branch made hipcc copy all of it to VGPRs in one block
+            // behind its last MFMA.  The pad: B_j's last P.V MFMAs may still be
+            // writing the O registers the asm reads (wait states hipcc cannot see
+            // inside the asm; a rare branch, so the pad is free).
             auto rescale_acc = [&](int rb, bool resc, float alpha) {
                 if (__builtin_expect(resc, 0)) {
+                    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
                     for (int db = 0; db < NDB; db++) scale_acc16(o[rb][db], alpha);
                 }
@@ -737,16 +740,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
                 const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
                 alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
-                m_run[rb] = m_new;
-                l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
-            };
-            auto smax_final = [&](int rb, float tmax, float& alpha, bool& resc) {
-                tmax = PF4_XOR32(tmax, true) * cexp;
-                resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
-                const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
-                alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
-                m_run[rb] = m_new;
-                l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
+                float mn = m_new, lx = l2[rb].x * alpha, ly = l2[rb].y * alpha;
+                // (pinned into its step: rb 1's results are next used past B's
+                // loop, and hipcc sank the whole chain there)
+                asm volatile("" : "+v"(alpha), "+v"(mn), "+v"(lx), "+v"(ly));
+                m_run[rb] = mn;
+                l2[rb] = f32x2{lx, ly};
             };
             // Staged forms of the pieces: a piece's three dependent instruction
             // groups in three consecutive steps (its exponent arguments, its
@@ -825,8 +824,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 // tile j beside 16-31 (its S chains done by then)
                 wait_vmcnt_c<C::NKI + MI>();  // B_{j-1}'s issues (K_{j+2}, mask j+1) may fly
                 PF4_T(0);
-                pr1 = rs1;  // rb 1's decision of tile j-1, applied at B_j
-                pa1 = al1;
                 // V_{j-1}^T operands for B_j, streamed: operand v (= B's MFMAs of
                 // steps 2v, 2v+1); the first four read in A_j after its barrier
                 f16x8 va[2][2][NDB];
@@ -843,8 +840,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 };
                 u32x2 mk1[2][4], mk0[2][4];
                 const uint32_t kb = k_base(j);
+                // the first four operands: read in B_{j-1}'s last steps (here for
+                // tile 0); the rest 4 steps ahead, in the steps
+                if constexpr (F) {
 #pragma unroll
-                for (int kk = 0; kk < 4; kk++) k_read1(kb, 0, kk);  // the rest: 4 steps ahead, in the steps
+                    for (int kk = 0; kk < 4; kk++) k_read1(kb, 0, kk);
+                }
                 const float nm1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];
                 float la1 = l2[1].x, lb1 = l2[1].y, tmax1 = kNegInf;
                 if constexpr (!F) e1(us1, nm1, 0);
@@ -867,7 +868,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     }
                     // V_j's DMA (into V_{j-3}'s slot, read in B_{j-2}; needed at B_{j+1}):
                     // the other half of the tile's issue cost beside A's MFMAs
+#ifdef FATTN_PF4_VDMA_LATE
+                    if (i >= 16 && (i & 3) == 1) v_piece(j, (i - 16) >> 2);
+#else
                     if (i < 16 && (i & 3) == 1) v_piece(j, i >> 2);
+#endif
                     if constexpr (MM) {
                         if (i == 8) mask_reads(j, 1, mk1);   // (for rb 1's scores, steps 16+)
                         if (i == 14) mask_reads(j, 0, mk0);  // (for B_j: this wave's slot, no barrier needed)
@@ -892,7 +897,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 m3(us1, tmax1, 15);
                 PF4_T(1);
                 if constexpr (!F) l2[1] = f32x2{la1, lb1};
-                smax_final(1, tmax1, al1, rs1);
+                // (rb 1's decision of tile j: in B_j's steps 12-13)
                 // (the phase's results pinned here: hipcc's machine sinking would
                 // otherwise move their exponentials next to their uses in B)
                 if constexpr (!F) pin_p(p1);
@@ -903,19 +908,19 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 // once); rb 0's scores and max of tile j beside steps 0-15, its
                 // exponentials beside 16-31
                 PF4_T(3);
-                rescale_acc(0, rs0, al0);  // decisions of tile j-1
-                rescale_acc(1, pr1, pa1);
                 float tmax0 = kNegInf, nm0 = 0.0f, la0 = 0.0f, lb0 = 0.0f;
                 f16x8 p0n[2][2];
                 const bool mskip = MM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
                 PF4_T(4);
                 __builtin_amdgcn_sched_barrier(0);
-                float tred0 = 0.0f;
+                float tred0 = 0.0f, tred1 = 0.0f;
+                const uint32_t kbn = k_base(j + 1);
                 // steps: rb 0's scores and max (piece p at slot s(p) = p / 2 for
-                // p < 8, p - 4 after: stages at s-1, s, s+1), the max across the
-                // lane pair (13), the rescale decision (14), the exponentials
-                // (piece p: 15+p, 16+p, 17+p; the last ones after the loop); then
-                // the step's MFMA, operand reads and DMA
+                // p < 8, p - 4 after: stages at s-1, s, s+1), rb 1's max across the
+                // lane pair (12) and rescale decision (13), rb 0's (13, 14), rb 0's
+                // exponentials (piece p: 15+p, 16+p, 17+p; the last ones after the
+                // loop); then the step's MFMA, operand reads (V^T; K_{j+1}'s first
+                // four in 28-31 -- past the end a slot nothing uses) and DMA
                 auto slot0 = [](int p) { return p < 8 ? p >> 1 : p - 4; };
                 m1(s0, 0);
                 m1(s0, 1);
@@ -928,7 +933,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                         if (slot0(p) == i) m2(mk0, us0, p);
                         if (slot0(p) - 1 == i) m1(s0, p);
                     }
+                    if (i == 12) {
+                        tred1 = PF4_XOR32(tmax1, true) * cexp;
+                        asm volatile("" : "+v"(tred1));
+                    }
                     if (i == 13) {
+                        smax_decide(1, tred1, al1, rs1);
                         tred0 = PF4_XOR32(tmax0, true) * cexp;
                         asm volatile("" : "+v"(tred0));
                     }
@@ -953,12 +963,19 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     // consumed by then)
                     if (i < 16 && (i & 3) == 1) k_piece(j + 3, i >> 2);  // (K_{j+3} into K_j's slot; V_j went in A_j)
                     if (i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
+#ifdef FATTN_PF4_KREAD_EARLY
+                    if (i >= 5 && i < 9) k_read1(kbn, 0, i - 5);
+#else
+                    if (i >= 28) k_read1(kbn, 0, i - 28);
+#endif
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 e3(p0n, la0, lb0, 15);  // (piece 15's last stage, after the loop)
                 PF4_T(5);
                 l2[0] = f32x2{la0, lb0};
                 pin_p(p0n);
+                rescale_acc(0, rs0, al0);  // the decisions of tile j
+                rescale_acc(1, rs1, al1);
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
 #pragma unroll
@@ -974,9 +991,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 sexp(1, 0, us1, p1);
                 sexp(1, 1, us1, p1);
                 __syncthreads();  // every wave's pieces of V nt-1 landed
-                rescale_acc(0, rs0, al0);
-                rescale_acc(1, rs1, al1);
-                pv2(nt - 1, p0, p1);
+                pv2(nt - 1, p0, p1);  // (tile nt-1's rescale: at the end of B_{nt-1})
             }
     #ifdef FATTN_STAMPS
             if (lane == 0 && g_stamps) {
