@@ -126,8 +126,10 @@ bool combine_ok(int64_t nch, int rv, int D) {
 // at least 6 steps per CU take 8 waves per workgroup, one step in flight each
 // (config 3: 8 waves x 2 steps, 11.3 us against 11.8 with 16 waves x 1 step
 // all requested at once, 12.4 with both steps of the 8 waves in flight, 12.6
-// for the 4-wave form; config 2: 8 x 1); multi-row tiles keep 4 waves (config
-// 4: 10.8 vs 11.3 us, config 5 shard 14.6 vs 15.7).  The grid is sized so that
+// for the 4-wave form; config 2: 8 x 1); multi-row tiles keep 4 waves up to 8
+// steps per CU (config 4: 10.8 vs 11.3 us; config 5's 8-rank shard, 4 heads:
+// 11.7 vs 12.0) and take 8 from 16 (round 5, same box: 4-rank shard 14.0 vs
+// 15.2 us, 2-rank shard 19.6 vs 19.9; profiles/r05_l).  The grid is sized so that
 // all (Y x S x chunks) workgroups are co-resident, limited by LDS (steps in
 // flight) and registers.
 int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t NQ) {
@@ -143,7 +145,7 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
             nwv = g_opt_split_waves;
         } else if (kv_chunk <= 0) {
             const int64_t per_cu = total / pl.cus;
-            nwv = (rv_max == 1 && per_cu >= 6) ? 8 : 4;
+            nwv = ((rv_max == 1 && per_cu >= 6) || (rv_max > 1 && per_cu >= 16)) ? 8 : 4;
         }
         nwv = std::min(nwv, 4 * wps);
         while (nwv > 4 && G.lds_bytes(1, nwv) > kLdsPerCU) nwv /= 2;

@@ -151,7 +151,34 @@ pass_k() {
   grep -h "median" gpurun_out/ab_f16_*.log gpurun_out/ab_q8_*.log
 }
 
+# config-5 shards (4 / 8 heads per rank): kernel families and chunk sizes
+pass_l() {
+  V="--variant base: --variant bdp:BD=3 --variant bd:BD=2 --variant mq:MQ_MIN_ROWS=64 --variant c128:kv_chunk=128 --variant w8:SPLIT_WAVES=8"
+  run ab_s8_fam 300 python -u tools/ab_decode.py --workload config5_s8 --rounds 3 $V
+  run ab_s4_fam 300 python -u tools/ab_decode.py --workload config5_s4 --rounds 3 $V
+}
+
+# config-5 shards: split-kernel waves / chunk / steps, and where the time goes
+pass_m() {
+  V="--variant base: --variant w8:SPLIT_WAVES=8 --variant w8c256:SPLIT_WAVES=8,kv_chunk=256 --variant w8c1024:SPLIT_WAVES=8,kv_chunk=1024 --variant w16:SPLIT_WAVES=16 --variant w8i2:SPLIT_WAVES=8,SPLIT_INFLIGHT=2"
+  for w in config5_s8 config5_s4 config5_s2; do
+    run ab_${w}_w 300 python -u tools/ab_decode.py --workload $w --rounds 3 $V
+  done
+  run kt_s8 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5m_kt8 -o kt -- python3 tools/ab_decode.py --workload config5_s8 --rounds 1 --variant base:
+  python tools/kstats.py $(find gpurun_out/r5m_kt8 -name "*kernel_stats.csv") > gpurun_out/kt_s8_summary.txt 2>&1 || true
+  cat gpurun_out/kt_s8_summary.txt
+}
+
+# the planner's 8-wave rule for multi-row split tiles from 16 steps per CU:
+# parity of the split paths, then auto vs forced 4 waves
+pass_n() {
+  run t_split 600 python -u -m pytest tests -x -q --timeout 200 --timeout-method thread -m gpu -k "split or shard or sweep or config4 or config2"
+  for w in config5_s8 config5_s4 config5_s2 config4 config2; do
+    run ab_${w}_n 300 python -u tools/ab_decode.py --workload $w --rounds 3 --variant auto: --variant w4:SPLIT_WAVES=4
+  done
+}
+
 case "$1" in
-  a|b|c|d|e|f|g|h|i|j|k) pass_$1 ;;
-  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k}"; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|j|k|l|m|n) pass_$1 ;;
+  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n}"; exit 2 ;;
 esac
