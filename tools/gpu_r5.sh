@@ -178,7 +178,13 @@ pass_n() {
   done
 }
 
+# config 3 (the headline decode) re-swept on the round-5 kernel: chunk, waves, in flight
+pass_o() {
+  V="--variant auto: --variant c256:kv_chunk=256 --variant c1024:kv_chunk=1024 --variant w4:SPLIT_WAVES=4 --variant w16:SPLIT_WAVES=16 --variant i2:SPLIT_INFLIGHT=2 --variant plain:SPLIT_XCD=1 --variant wm1:SPLIT_WAVE_MERGE=1"
+  run ab_config3_o 300 python -u tools/ab_decode.py --workload config3 --rounds 5 $V
+}
+
 case "$1" in
-  a|b|c|d|e|f|g|h|i|j|k|l|m|n) pass_$1 ;;
-  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n}"; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o) pass_$1 ;;
+  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o}"; exit 2 ;;
 esac
