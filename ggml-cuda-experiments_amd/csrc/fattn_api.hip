@@ -62,7 +62,7 @@ std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge 
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
 std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto, 1 off, 2 on
-std::atomic<int> g_opt_pf_form{0};          // prefill body at D = 128 over f16 rows: 0 auto (4), 1 the 8-wave form, 2-4 one wave per SIMD (fattn_pf4.h)
+std::atomic<int> g_opt_pf_form{0};          // prefill body at D = 128 over f16 rows: 0 auto (5), 1 the 8-wave form, 2-5 one wave per SIMD (fattn_pf4.h)
 std::atomic<int> g_opt_pf_stage{0};         // prefill over Q8_0 / Q4_0: 0 auto (staged to f16), 1 in-kernel dequantisation, 2 staged
 std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
@@ -599,9 +599,11 @@ int make_plan(const fattn_params* p, Plan& pl) {
                  : D == 96 ? pf_lds(std::integral_constant<int, 96>())
                            : pf_lds(std::integral_constant<int, 128>());
         // f16 rows (native or staged) at D = 128: the one-wave-per-SIMD body
-        // (auto: the pipelined schedule, 3-10 % faster than the 8-wave body on
-        // the prefill shape, profiles/r05_h; form 1 keeps the 8-wave body)
-        const int form = g_opt_pf_form == 0 ? 4 : (int)g_opt_pf_form;
+        // (auto: the balanced pipelined schedule -- 0-4 % faster than the 8-wave
+        // body on f16 rows, 12-21 % on staged Q8_0 with the zero mask, and 1-3 %
+        // faster than the pipelined form 4, profiles/r05_h, r05_p; form 1 keeps
+        // the 8-wave body)
+        const int form = g_opt_pf_form == 0 ? 5 : (int)g_opt_pf_form;
         pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && form >= 2;
         pl.pf4_sched = form >= 3 ? form - 2 : 0;
         if (pl.pf4) pl.lds = Pf4Cfg<128>::ldsBytes;
@@ -717,7 +719,7 @@ int fattn_set_option(int option, int value) {
             g_opt_split_xcd = value;
             return FATTN_OK;
         case FATTN_OPT_PF_FORM:
-            if (value < 0 || value > 4) return FATTN_ERR_INVALID_ARG;
+            if (value < 0 || value > 5) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_form = value;
             return FATTN_OK;
         case FATTN_OPT_PF_STAGE:
@@ -785,7 +787,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
                       pl.pf_stage ? (pl.stage_kt == FATTN_TYPE_Q8_0 ? "kv_stage_f16<q8_0> + " : "kv_stage_f16<q4_0> + ")
                                   : "",
                       pl.pf_flags ? "pf_mask_flags_kernel + " : "",
-                      pl.pf4 ? (pl.pf4_sched == 2 ? "fattn_pf4_kernel(pipelined)" : pl.pf4_sched ? "fattn_pf4_kernel(sched1)" : "fattn_pf4_kernel") : "fattn_pf_kernel",
+                      pl.pf4 ? (pl.pf4_sched == 3 ? "fattn_pf4_kernel(balanced)" : pl.pf4_sched == 2 ? "fattn_pf4_kernel(pipelined)" : pl.pf4_sched ? "fattn_pf4_kernel(sched1)" : "fattn_pf4_kernel") : "fattn_pf_kernel",
                       tn(pl.kt), pl.D, hm);
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,

@@ -187,8 +187,9 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     const void* main_kern = (const void*)kern;
     if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
         if (pl.pf4)
-            main_kern = pl.pf4_sched == 2 ? (const void*)fattn_pf4_kernel<D, HM, 2>
-                        : pl.pf4_sched    ? (const void*)fattn_pf4_kernel<D, HM, 1>
+            main_kern = pl.pf4_sched == 3   ? (const void*)fattn_pf4_kernel<D, HM, 3>
+                        : pl.pf4_sched == 2 ? (const void*)fattn_pf4_kernel<D, HM, 2>
+                        : pl.pf4_sched      ? (const void*)fattn_pf4_kernel<D, HM, 1>
                                           : (const void*)fattn_pf4_kernel<D, HM, 0>;
     }
     return launch_kernel(main_kern, pl, st, ev, [&] {
@@ -209,7 +210,9 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
                                pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
         if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
             if (pl.pf4) {
-                if (pl.pf4_sched == 2)
+                if (pl.pf4_sched == 3)
+                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 3>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
+                else if (pl.pf4_sched == 2)
                     hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 2>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
                 else if (pl.pf4_sched)
                     hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 1>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);

@@ -155,6 +155,19 @@ __device__ __forceinline__ void pin_p(f16x8 (&p)[2][2]) {
 #define PF4_OPAQUE_V2(x, y) asm volatile("" : "+v"(x), "+v"(y))
 #endif
 
+// the piece q in [0, 16) whose stage of schedule s(q) = C + (A q) / B falls on
+// step i, or -1 (s strictly increasing: A >= B)
+template <int A, int B, int C>
+__device__ __forceinline__ constexpr int sched_inv(int i) {
+    static_assert(A >= B, "the schedule must be strictly increasing");
+    const int d = i - C;
+    if (d < 0) return -1;
+    const int q0 = (d * B) / A;
+    if (q0 < 16 && (A * q0) / B == d) return q0;
+    if (q0 + 1 < 16 && (A * (q0 + 1)) / B == d) return q0 + 1;
+    return -1;
+}
+
 // SCHED 0: per tile A (QK rb1 || softmax rb0), B (PV rb0 || softmax rb1),
 // C (PV rb1, QK rb0 of the next tile).  SCHED 1 (rebalanced): the softmax in
 // two parts -- smax (scores, max, rescale decision) and sexp (exponentials,
@@ -574,7 +587,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             pv(s, 1, p1);
             if (s + 1 < nt) qk(s + 1, 0, s0);
         }
-    } else if constexpr (SCHED == 2) {
+    } else if constexpr (SCHED >= 2) {
         // A workgroup whose live tiles all hold +-0 masks (the flags pass's 2,
         // SURVEY's zero-mask prefill) runs the body without mask values in
         // LDS (ZM): no mask DMA, reads or waits, scores fma(s, scale, 0) --
@@ -983,6 +996,198 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 }
                 PF4_T(6);
             };
+            // The balanced form (SCHED 3): each phase carries one row block's
+            // exponentials and the OTHER row block's scores and max, interleaved
+            // over all 32 steps (no dependency between them inside the phase):
+            //   A_j: S_j (both)  ||  rb 0's exponentials of tile j-1, rb 1's
+            //        scores / max of tile j;
+            //   B_j: P_{j-1}.V (both)  ||  rb 1's decision and exponentials of
+            //        tile j, rb 0's scores / max / decision of tile j.
+            // Per row block the same operations in the same order as the other
+            // forms (decision, then the tile's exponentials and sums), so the
+            // same bits.  P_{j-1} of rb 0 comes from A_j, of rb 1 from B_{j-1}.
+            // Stage steps: A's max pieces from step 9 (S1's subtile-0 chain ends
+            // at 7), spread to 31; A's exponential pieces one per two steps; B's
+            // rb 1 decision in steps 0-1, its exponentials from 2, rb 0's max
+            // pieces over 0-28 and its decision in 29-30.
+            // (each schedule s(q) = C + (A q) / B is strictly increasing, so a step
+            // holds at most one piece's stage: sched_inv finds it without a loop --
+            // a loop over the pieces in every step kept hipcc from unrolling)
+            // (diagnostic builds only, outputs wrong: the phases without their
+            // vector pieces / without their in-loop DMA -- what the skeleton costs)
+#ifdef FATTN_PF4_DIAG_NO_VALU
+            constexpr bool kDiagNoValu = true;
+#else
+            constexpr bool kDiagNoValu = false;
+#endif
+#ifdef FATTN_PF4_DIAG_NO_DMA
+            constexpr bool kDiagNoDma = true;
+#else
+            constexpr bool kDiagNoDma = false;
+#endif
+            auto iter_bal = [&](int j, auto first) {
+                constexpr bool F = decltype(first)::value;
+                PF4_T(7);
+                wait_vmcnt_c<C::NKI + MI>();  // B_{j-1}'s issues (K_{j+2}, mask j+1) may fly
+                PF4_T(0);
+                f16x8 va[2][2][NDB];
+                uint32_t vb0 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[0];
+                uint32_t vb1 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[1];
+                PF4_OPAQUE_V2(vb0, vb1);
+                auto v_read1 = [&](int v) {
+                    const int t = v >> 3, q = (v >> 2) & 1, db = v & 3;
+                    const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb0 + off));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lsm + vb1 + off));
+                    const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
+                    va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
+                };
+                u32x2 mk1[2][4], mk0[2][4];
+                const uint32_t kb = k_base(j);
+                if constexpr (F) {
+#pragma unroll
+                    for (int kk = 0; kk < 4; kk++) k_read1(kb, 0, kk);
+                }
+                // ---- A_j
+                const float nm0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
+                float la0 = l2[0].x, lb0 = l2[0].y, tmax1 = kNegInf;
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 32; i++) {
+                    const int t = (i >> 3) & 1, kk = i & 7;
+                    if (i < 12) k_read1(kb, (i + 4) >> 3, (i + 4) & 7);
+                    if (i == 12) __syncthreads();
+                    if constexpr (!F) {
+                        if (i >= 24 && !(i & 1)) v_read1((i - 24) >> 1);
+                    }
+                    if (!kDiagNoDma && i < 16 && (i & 3) == 1) v_piece(j, i >> 2);
+                    if constexpr (MM) {
+                        if (i == 8) mask_reads(j, 1, mk1);
+                        if (i == 14) mask_reads(j, 0, mk0);
+                    }
+                    if constexpr (!F && !kDiagNoValu) {
+                        // rb 0's exponentials of tile j-1: piece p at 2p, 2p+1, 2p+2
+                        if (i >= 2 && !(i & 1)) e3(p0, la0, lb0, (i - 2) >> 1);
+                        if (i & 1) e2(i >> 1);
+                        if (!(i & 1)) e1(us0, nm0, i >> 1);
+                    }
+                    if constexpr (!kDiagNoValu) {
+                        const int q3 = sched_inv<22, 15, 9>(i - 2), q2 = sched_inv<22, 15, 9>(i - 1),
+                                  q1 = sched_inv<22, 15, 9>(i);
+                        if (q3 >= 0) m3(us1, tmax1, q3);
+                        if (q2 >= 0) m2(mk1, us1, q2);
+                        if (q1 >= 0) m1(s1, q1);
+                    }
+                    if (i < 16) {
+                        if (kk == 0) s1[t] = f32x16{};
+                        s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
+                    } else {
+                        if (kk == 0) s0[t] = f32x16{};
+                        s0[t] = mfma32(kr[t][kk], qop[0][kk], s0[t]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if constexpr (!F) e3(p0, la0, lb0, 15);
+                {
+                    // (the stages of the last pieces past step 31)
+                    const int q2 = sched_inv<22, 15, 9>(31), q3a = sched_inv<22, 15, 9>(30),
+                              q3b = sched_inv<22, 15, 9>(31);
+                    if (q2 >= 0) m2(mk1, us1, q2);
+                    if (q3a >= 0) m3(us1, tmax1, q3a);
+                    if (q3b >= 0) m3(us1, tmax1, q3b);
+                }
+                if constexpr (kDiagNoValu) asm volatile("" ::"v"(s1[0][0]), "v"(s1[1][0]), "v"(s0[0][0]), "v"(s0[1][0]));
+                PF4_T(1);
+                if constexpr (!F) {
+                    l2[0] = f32x2{la0, lb0};
+                    pin_p(p0);
+                }
+                pin16(us1[0]);
+                pin16(us1[1]);
+                PF4_T(2);
+                // ---- B_j
+                PF4_T(3);
+                float tmax0 = kNegInf, nm1 = 0.0f, la1 = 0.0f, lb1 = 0.0f;
+                f16x8 p1n[2][2];
+                const bool mskip = MM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
+                PF4_T(4);
+                __builtin_amdgcn_sched_barrier(0);
+                float tred0 = 0.0f, tred1 = 0.0f;
+                const uint32_t kbn = k_base(j + 1);
+#pragma unroll
+                for (int i = 0; i < 32; i++) {
+                    if (i == 0) {
+                        tred1 = PF4_XOR32(tmax1, true) * cexp;
+                        asm volatile("" : "+v"(tred1));
+                    }
+                    if (i == 1) {
+                        smax_decide(1, tred1, al1, rs1);
+                        nm1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];
+                        la1 = l2[1].x;
+                        lb1 = l2[1].y;
+                        asm volatile("" : "+v"(nm1), "+v"(la1), "+v"(lb1));
+                    }
+                    if constexpr (!kDiagNoValu) {
+                        const int e3p = sched_inv<28, 15, 2>(i - 2), e2p = sched_inv<28, 15, 2>(i - 1),
+                                  e1p = sched_inv<28, 15, 2>(i);
+                        const int m3p = sched_inv<26, 15, 0>(i - 2), m2p = sched_inv<26, 15, 0>(i - 1),
+                                  m1p = sched_inv<26, 15, 0>(i);
+                        if (e3p >= 0) e3(p1n, la1, lb1, e3p);
+                        if (e2p >= 0) e2(e2p);
+                        if (e1p >= 0) e1(us1, nm1, e1p);
+                        if (m3p >= 0) m3(us0, tmax0, m3p);
+                        if (m2p >= 0) m2(mk0, us0, m2p);
+                        if (m1p >= 0) m1(s0, m1p);
+                    }
+                    if (i == 29) {
+                        tred0 = PF4_XOR32(tmax0, true) * cexp;
+                        asm volatile("" : "+v"(tred0));
+                    }
+                    if (i == 30) smax_decide(0, tred0, al0, rs0);
+                    if constexpr (!F) {
+                        if (!(i & 1) && i < 24) v_read1((i >> 1) + 4);
+                        const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
+                        o[rb][db] = mfma32(va[t][q][db], rb ? p1[t][q] : p0[t][q], o[rb][db]);
+                    }
+                    if (!kDiagNoDma && i < 16 && (i & 3) == 1) k_piece(j + 3, i >> 2);
+                    if (!kDiagNoDma && i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
+                    if (i >= 28) k_read1(kbn, 0, i - 28);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                {
+                    // (the stages of the last pieces past step 31)
+                    const int e2p = sched_inv<28, 15, 2>(31), e3a = sched_inv<28, 15, 2>(30),
+                              e3b = sched_inv<28, 15, 2>(31);
+                    if (e2p >= 0) e2(e2p);
+                    if (e3a >= 0) e3(p1n, la1, lb1, e3a);
+                    if (e3b >= 0) e3(p1n, la1, lb1, e3b);
+                }
+                PF4_T(5);
+                l2[1] = f32x2{la1, lb1};
+                pin_p(p1n);
+                pin16(us0[0]);
+                pin16(us0[1]);
+                rescale_acc(0, rs0, al0);  // the decisions of tile j
+                rescale_acc(1, rs1, al1);
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+#pragma unroll
+                    for (int q = 0; q < 2; q++) p1[t][q] = p1n[t][q];
+                }
+                PF4_T(6);
+            };
+            if constexpr (SCHED == 3) {
+                if (nt > 0) iter_bal(0, std::true_type());
+                for (int j = 1; j < nt; j++) iter_bal(j, std::false_type());
+                if (nt > 0) {
+                    // ---- A_nt, B_nt: rb 0's exponentials of the last tile, its P.V
+                    wait_vmcnt_c<0>();
+                    sexp(0, 0, us0, p0);
+                    sexp(0, 1, us0, p0);
+                    __syncthreads();  // every wave's pieces of V nt-1 landed
+                    pv2(nt - 1, p0, p1);
+                }
+            } else {
             if (nt > 0) iter(0, std::true_type());
             for (int j = 1; j < nt; j++) iter(j, std::false_type());
             if (nt > 0) {
@@ -992,6 +1197,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 sexp(1, 1, us1, p1);
                 __syncthreads();  // every wave's pieces of V nt-1 landed
                 pv2(nt - 1, p0, p1);  // (tile nt-1's rescale: at the end of B_{nt-1})
+            }
             }
     #ifdef FATTN_STAMPS
             if (lane == 0 && g_stamps) {

@@ -198,10 +198,12 @@ enum {
                                        the kernel, tile by tile, once per 256-row query tile; 2 = staged: the rows
                                        converted once to f16 in the workspace (kv_stage_f16, + 2 * Skv * Hkv * N *
                                        D * 2 bytes of fattn_workspace_size), then the f16 prefill kernel */,
-    FATTN_OPT_PF_FORM = 29          /* prefill body over f16 rows (native or staged) at D = 128: 0 = auto (4), 1 =
+    FATTN_OPT_PF_FORM = 29          /* prefill body over f16 rows (native or staged) at D = 128: 0 = auto (5), 1 =
                                        the 8-wave form (fattn_pf_kernel), 2 = one wave per SIMD (fattn_pf4_kernel),
                                        3 = the same with the rebalanced phase schedule, 4 = the same pipelined
-                                       (two 32-MFMA phases per tile, P.V one tile behind S) */
+                                       (two 32-MFMA phases per tile, P.V one tile behind S), 5 = pipelined and
+                                       balanced (each phase carries one row block's exponentials and the other's
+                                       scores / max, interleaved over its 32 steps) */
 };
 int fattn_set_option(int option, int value);
 

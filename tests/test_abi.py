@@ -222,20 +222,20 @@ def test_mq_min_rows_explicit_default_lifts_the_wide_gate():
 
 
 def test_pf_form_option():
-    """The prefill body over f16 rows at D = 128: the pipelined one-wave-per-
-    SIMD body by default, the 8-wave body with FATTN_OPT_PF_FORM = 1, the
-    other one-wave-per-SIMD schedules with 2 / 3; other head dims keep the
-    8-wave body."""
+    """The prefill body over f16 rows at D = 128: the balanced pipelined
+    one-wave-per-SIMD body by default, the 8-wave body with FATTN_OPT_PF_FORM = 1, the
+    other one-wave-per-SIMD schedules with 2 / 3 / 5 (5: the balanced
+    pipeline); other head dims keep the 8-wave body."""
     p = _params(NQ=4096, kt=fattn.TYPE_F16)
-    assert "fattn_pf4_kernel(pipelined)<f16,D128" in fattn.describe(p)
+    assert "fattn_pf4_kernel(balanced)<f16,D128" in fattn.describe(p)
     want = {1: "fattn_pf_kernel<f16,D128", 2: "fattn_pf4_kernel<f16,D128", 3: "fattn_pf4_kernel(sched1)<f16,D128",
-            4: "fattn_pf4_kernel(pipelined)<f16,D128"}
+            4: "fattn_pf4_kernel(pipelined)<f16,D128", 5: "fattn_pf4_kernel(balanced)<f16,D128"}
     for form, name in want.items():
         with fattn.options({fattn.OPT_PF_FORM: form}):
             assert name in fattn.describe(p), (form, fattn.describe(p))
     assert "fattn_pf_kernel<f16,D64" in fattn.describe(_params(NQ=4096, D=64, kt=fattn.TYPE_F16))
     with pytest.raises(Exception):
-        with fattn.options({fattn.OPT_PF_FORM: 5}):
+        with fattn.options({fattn.OPT_PF_FORM: 6}):
             pass
 
 
@@ -245,7 +245,7 @@ def test_pf_stage_option_and_workspace():
     FATTN_OPT_PF_STAGE = 1; f16 caches are never staged."""
     p = _params(NQ=4096)
     d = fattn.describe(p)
-    assert d.startswith("kv_stage_f16<q8_0> + pf_mask_flags_kernel + fattn_pf4_kernel(pipelined)<f16,D128"), d
+    assert d.startswith("kv_stage_f16<q8_0> + pf_mask_flags_kernel + fattn_pf4_kernel(balanced)<f16,D128"), d
     ws = fattn.workspace_size(p)
     with fattn.options({fattn.OPT_PF_STAGE: 1}):
         d1 = fattn.describe(p)

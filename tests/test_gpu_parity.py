@@ -630,14 +630,14 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture(params=[(0, 1), (1, 1), (0, 2), (0, 3), (0, 4)],
-                ids=["staged", "inkernel_deq", "staged_pf4", "staged_pf4s1", "staged_pf4p"])
+@pytest.fixture(params=[(0, 1), (1, 1), (0, 2), (0, 3), (0, 4), (0, 5)],
+                ids=["staged", "inkernel_deq", "staged_pf4", "staged_pf4s1", "staged_pf4p", "staged_pf4b"])
 def pf_force(request):
     """The prefill kernels on every eligible problem: Q8_0 / Q4_0 K/V staged
     to f16 first (the default) or dequantised inside the kernel
     (FATTN_OPT_PF_STAGE = 1); the f16 body in its 8-wave form (fattn_pf.h)
-    or one wave per SIMD (fattn_pf4.h, D = 128; FATTN_OPT_PF_FORM = 2, 3 and
-    the pipelined 4)."""
+    or one wave per SIMD (fattn_pf4.h, D = 128; FATTN_OPT_PF_FORM = 2, 3, the
+    pipelined 4 and the balanced 5)."""
     stage, form = request.param
     fattn.set_option(fattn.OPT_PF, 2)
     fattn.set_option(fattn.OPT_PF_STAGE, stage)
@@ -668,13 +668,14 @@ def test_pf4_bit_identical_to_pf(dev, case):
     outs = {}
     fattn.set_option(fattn.OPT_PF, 2)
     try:
-        for form in (1, 2, 3, 4):
+        for form in (1, 2, 3, 4, 5):
             fattn.set_option(fattn.OPT_PF_FORM, form)
             t = upload(p)
             att = fattn.Attention(*views(p, t), t["dst"], p.scale)
             assert ("fattn_pf4_kernel" in att.describe()) == (form >= 2), att.describe()
             assert ("(sched1)" in att.describe()) == (form == 3), att.describe()
             assert ("(pipelined)" in att.describe()) == (form == 4), att.describe()
+            assert ("(balanced)" in att.describe()) == (form == 5), att.describe()
             att()
             outs[form] = t["dst"].cpu().numpy()
     finally:
@@ -683,6 +684,7 @@ def test_pf4_bit_identical_to_pf(dev, case):
     assert np.array_equal(outs[1], outs[2], equal_nan=True)
     assert np.array_equal(outs[1], outs[3], equal_nan=True)
     assert np.array_equal(outs[1], outs[4], equal_nan=True)
+    assert np.array_equal(outs[1], outs[5], equal_nan=True)
     assert attn_rel_err(outs[4], p.oracle()) <= RTOL
 
 

@@ -25,7 +25,7 @@ def main():
         ref = p.oracle()[0, :, 0, :]
         outs = {}
         fattn.set_option(fattn.OPT_PF, 2)
-        for form in (1, 2, 3, 4):
+        for form in (1, 2, 3, 4, 5):
             fattn.set_option(fattn.OPT_PF_FORM, form)
             t = upload(p)
             att = fattn.Attention(*views(p, t), t["dst"], p.scale)
@@ -34,7 +34,7 @@ def main():
             outs[form] = t["dst"].cpu().numpy()[0, :, 0, :]
         fattn.reset_options()
         print("case", case)
-        for form in (1, 2, 3, 4):
+        for form in (1, 2, 3, 4, 5):
             o = outs[form]
             err = np.abs(o - ref).max(axis=1) / np.abs(ref).max(axis=1)
             bad = np.nonzero(err > 1e-3)[0]

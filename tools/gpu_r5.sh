@@ -184,7 +184,29 @@ pass_o() {
   run ab_config3_o 300 python -u tools/ab_decode.py --workload config3 --rounds 5 $V
 }
 
+# the balanced pipelined prefill (FATTN_OPT_PF_FORM = 5): row diagnostic,
+# parity, stamps, same-box A/B against the pipelined (4) and 8-wave (1) bodies
+pass_p() {
+  run dbg_bal 200 python -u tools/dbg_pf4.py
+  run t_bal 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -m gpu -k "pf4 or pf_sweep or pf_prefill or pf_staged"
+  run st_bal_f16 200 python -u tools/pf_stamps.py --no-mask --kv-type f16 --form 5
+  run st_bal_q8 200 python -u tools/pf_stamps.py --kv-type q8_0 --form 5
+  run ab_bal_f16 300 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 3 --variant pf8:PF_FORM=1 --variant pf4p:PF_FORM=4 --variant bal:PF_FORM=5
+  run ab_bal_q8 300 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 3 --variant pf8:PF_FORM=1 --variant pf4p:PF_FORM=4 --variant bal:PF_FORM=5
+}
+
+# where the balanced body's phase time goes: stamps of diagnostic builds
+# without the vector pieces (snv), without the in-loop DMA (snd), without both
+# (snb); outputs wrong, cycles only (make variant VAR=snv VFLAGS="-DFATTN_STAMPS
+# -DFATTN_PF4_DIAG_NO_VALU", ...)
+pass_q() {
+  run st_q_full 200 python -u tools/pf_stamps.py --no-mask --kv-type f16 --form 5
+  for v in snv snd snb; do
+    FATTN_LIB=libfattn_$v.so run st_q_$v 200 python -u tools/pf_stamps.py --no-mask --kv-type f16 --form 5
+  done
+}
+
 case "$1" in
-  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o) pass_$1 ;;
-  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o}"; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q) pass_$1 ;;
+  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q}"; exit 2 ;;
 esac
