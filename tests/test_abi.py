@@ -69,7 +69,8 @@ def test_workspace_size_config3():
     (dict(N=2048, kt=fattn.TYPE_F16), ["f16,f16", "8waves>", "grid(8,32,1)"]),              # config 2
     (dict(H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0), ["4waves> + fattn_merge_kernel", "grid(32,8,1)"]),  # config 4
     (dict(NQ=64), ["fattn_bdp_kernel<q8_0", "+ fattn_bd_merge_kernel", "grid(8,32,1)"]),   # config 5, one GPU
-    (dict(NQ=64, H=4, Hkv=4), ["fattn_split_kernel", "+ fattn_merge_kernel"]),             # config 5, 8-rank shard
+    (dict(NQ=64, H=4, Hkv=4), ["fattn_split_kernel", "4waves> + fattn_merge_kernel"]),     # config 5, 8-rank shard
+    (dict(NQ=64, H=8, Hkv=8), ["fattn_split_kernel", "8waves> + fattn_merge_kernel", "grid(8,32,1)"]),  # 4-rank shard
     (dict(NQ=64, H=16, Hkv=16), ["fattn_bdp_kernel", "+ fattn_bd_merge_kernel", "grid(16,16,1)"]),  # config 5, 2-rank shard
     (dict(NQ=256), ["fattn_bdp_kernel", "grid(2,128,1)"]),                                  # batched: 4 row tiles
     (dict(NQ=64, kt=fattn.TYPE_F16), ["fattn_bd_kernel<f16,D128", "+ fattn_bd_merge_kernel"]),  # config 5 shape, f16
@@ -83,13 +84,14 @@ def test_workspace_size_config3():
     (dict(D=96, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16), ["fattn_pf_kernel<f16,D96"]),
     (dict(D=80, NQ=4096, H=32, Hkv=32, kt=fattn.TYPE_F16), ["fattn_pf_kernel<f16,D80"]),      # D = 80 prefill (f16)
     (dict(D=256, NQ=4096, H=16, Hkv=16), ["fattn_mq_kernel<q8_0,D256,4waves"]),              # D = 256 prefill
-], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard2", "mq_nq256", "bd_f16", "bd_f16_d64", "bd_f16_d96",
+], ids=["config3", "config2", "config4", "config5", "config5_shard", "config5_shard4", "config5_shard2", "mq_nq256", "bd_f16", "bd_f16_d64", "bd_f16_d96",
         "bd_gqa6", "bd_f16_shard", "split_nq8_gqa", "pf_d64", "pf_d96", "pf_d96_f16", "pf_d80_f16", "mq_d256"])
 def test_planner_picks(kw, want):
     """The plans the round-2 measurements chose, at 256 CUs:
     one-row tiles take 8 waves with the fused row merge; multi-row split tiles
     with 4+ chunks and batched-decode tiles merge in a second launch; long
-    multi-row slices take twice the chunks."""
+    multi-row slices take twice the chunks; multi-row split tiles take 8 waves
+    from 16 steps per CU (round 5: the 4-rank config-5 shard)."""
     d = fattn.describe(_params(**kw))
     for w in want:
         assert w in d, d
