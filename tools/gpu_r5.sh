@@ -206,7 +206,18 @@ pass_q() {
   done
 }
 
+# a second box for the prefill body choice (forms 1 / 4 / 5, 5 rounds), and
+# where the 4-rank shard's step goes on the new plan (rocprofv3)
+pass_r() {
+  run ab_r_f16 300 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 5 --variant pf8:PF_FORM=1 --variant pf4p:PF_FORM=4 --variant bal:PF_FORM=5
+  run ab_r_q8 300 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 5 --variant pf8:PF_FORM=1 --variant pf4p:PF_FORM=4 --variant bal:PF_FORM=5
+  run ab_r_q8r 300 python -u tools/ab_prefill.py --kv q8_0 --mask random --rounds 3 --variant pf8:PF_FORM=1 --variant pf4p:PF_FORM=4 --variant bal:PF_FORM=5
+  run kt_s4 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5r_kt4 -o kt -- python3 tools/ab_decode.py --workload config5_s4 --rounds 1 --variant auto:
+  python tools/kstats.py $(find gpurun_out/r5r_kt4 -name "*kernel_stats.csv") > gpurun_out/kt_s4_summary.txt 2>&1 || true
+  cat gpurun_out/kt_s4_summary.txt
+}
+
 case "$1" in
-  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q) pass_$1 ;;
-  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q}"; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r) pass_$1 ;;
+  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r}"; exit 2 ;;
 esac
