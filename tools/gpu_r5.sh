@@ -217,7 +217,18 @@ pass_r() {
   cat gpurun_out/kt_s4_summary.txt
 }
 
+# would a pre-transposed V image pay?  a diagnostic build reading each V^T
+# operand with ONE ds_read_b128 (outputs wrong; lib/libfattn_vb128.so from
+# -DFATTN_PF4_DIAG_VB128, kept out of the tree) against the shipped body
+pass_s() {
+  for i in 1 2 3; do
+    run ab_s_base_$i 200 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 3 --variant bal:PF_FORM=5
+    FATTN_LIB=libfattn_vb128.so run ab_s_vb128_$i 200 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 3 --variant vb128:PF_FORM=5
+  done
+  grep -h median gpurun_out/ab_s_*.log
+}
+
 case "$1" in
-  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r) pass_$1 ;;
-  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r}"; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s) pass_$1 ;;
+  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s}"; exit 2 ;;
 esac
