@@ -228,7 +228,12 @@ pass_s() {
   grep -h median gpurun_out/ab_s_*.log
 }
 
+# config 3: wave priorities and the masked-step skip, re-measured on the round-5 kernel
+pass_t() {
+  run ab_config3_t 300 python -u tools/ab_decode.py --workload config3 --rounds 7 --variant auto: --variant prio_none:SPLIT_PRIO=1 --variant prio_issue:SPLIT_PRIO=2 --variant noskip:SPLIT_SKIP=1
+}
+
 case "$1" in
-  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s) pass_$1 ;;
-  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s}"; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t) pass_$1 ;;
+  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t}"; exit 2 ;;
 esac
