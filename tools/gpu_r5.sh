@@ -233,7 +233,12 @@ pass_t() {
   run ab_config3_t 300 python -u tools/ab_decode.py --workload config3 --rounds 7 --variant auto: --variant prio_none:SPLIT_PRIO=1 --variant prio_issue:SPLIT_PRIO=2 --variant noskip:SPLIT_SKIP=1
 }
 
+# config 4 (Q4_0, GQA 32/8, N 8192): chunk / waves around the auto plan, merge launch kept
+pass_u() {
+  run ab_config4_u 300 python -u tools/ab_decode.py --workload config4 --rounds 5 --variant auto: --variant c512:kv_chunk=512 --variant w8:SPLIT_WAVES=8 --variant w8c512:SPLIT_WAVES=8,kv_chunk=512 --variant c128:kv_chunk=128 --variant xcd:SPLIT_XCD=2
+}
+
 case "$1" in
-  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t) pass_$1 ;;
-  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t}"; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u) pass_$1 ;;
+  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u}"; exit 2 ;;
 esac
