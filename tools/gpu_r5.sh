@@ -238,7 +238,13 @@ pass_u() {
   run ab_config4_u 300 python -u tools/ab_decode.py --workload config4 --rounds 5 --variant auto: --variant c512:kv_chunk=512 --variant w8:SPLIT_WAVES=8 --variant w8c512:SPLIT_WAVES=8,kv_chunk=512 --variant c128:kv_chunk=128 --variant xcd:SPLIT_XCD=2
 }
 
+# D = 256 on the multi-query kernel: rows per wave and chunk around the auto plan
+pass_v() {
+  run ab_d256_pf_v 300 python -u tools/ab_prefill.py --kv q8_0 --mask zero --D 256 --H 16 --rounds 2 --variant auto: --variant r16:MQ_ROWS_PER_WAVE=16 --variant r32:MQ_ROWS_PER_WAVE=32
+  run ab_d256_dec_v 300 python -u tools/ab_decode.py --workload config5 --D 256 --rounds 3 --variant auto: --variant r16:MQ_ROWS_PER_WAVE=16 --variant r32:MQ_ROWS_PER_WAVE=32 --variant c256:kv_chunk=256 --variant c1024:kv_chunk=1024
+}
+
 case "$1" in
-  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u) pass_$1 ;;
-  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u}"; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v) pass_$1 ;;
+  *) echo "usage: bash tools/gpu_r5.sh {a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r|s|t|u|v}"; exit 2 ;;
 esac
