@@ -246,14 +246,15 @@ def test_workspace_not_zeroed(dev, case, fill):
 
 # ------------------------------------------------------------------ multi-GPU head shard, one GPU
 
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_config5_head_shard_slices(dev, world):
     """BASELINE config 5 (n_q = 64, 32 heads, N = 4096, Q8_0) cut into the
     per-rank slices bench.py --gpus N runs (fattn.shard.shard_heads +
     head_views: zero-copy q / k / v views, the GQA map kept inside a slice),
     each slice run through the HIP kernel on this GPU, the slices assembled
     into the ggml dst layout exactly as gather_heads does after the RCCL
-    all_gather -- against the oracle of the whole problem."""
+    all_gather -- against the oracle of the whole problem.  (World 4: the
+    multi-row split kernel's 8-wave plan.)"""
     import torch
     p = make_problem(D=128, NQ=64, H=32, N=4096, kv_type="q8_0", seed=55)
     t = upload(p, dev)
@@ -263,7 +264,10 @@ def test_config5_head_shard_slices(dev, world):
         sh = shard_heads(p.H, p.Hkv, world, rank)
         qs, ks, vs = head_views(qv, kv, vv, sh)
         dst = torch.full((1, p.NQ, sh.n_heads, p.D), float("nan"), dtype=torch.float32, device=dev)
-        fattn.Attention(qs, ks, vs, mv, dst, p.scale)()
+        att = fattn.Attention(qs, ks, vs, mv, dst, p.scale)
+        if world == 4:
+            assert "8waves> + fattn_merge_kernel" in att.describe(), att.describe()
+        att()
         parts.append(dst)
     torch.cuda.synchronize()
     full = assemble_heads(torch.stack(parts)).cpu().numpy()
