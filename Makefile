@@ -11,7 +11,7 @@ HARNESS := $(BINDIR)/kernel_test
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
             -munsafe-fp-atomics -Iinclude
 CSRC := $(wildcard $(PKG)/csrc/*.hip)
-CHDR := $(wildcard $(PKG)/csrc/*.h) include/fattn.h
+CHDR := $(wildcard $(PKG)/csrc/*.h) include/fattn.h include/fattn_debug.h
 
 .PHONY: all lib harness oracle clean asm stamps tests-hip probe isa variant
 

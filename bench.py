@@ -145,13 +145,46 @@ def measured_hbm_peaks():
     return {"copy_dwordx4": round(cp.value, 1), "read_dwordx4": round(rd.value, 1)}
 
 
+def oneshot_ceiling(shape):
+    """The one-shot read ceiling of THIS launch shape (tools/hbm_copy.hip
+    hbm_oneshot): the same 256 workgroups each reading its contiguous slice of
+    the K cache and of the V cache once -- nothing else in the launch -- over 16
+    rotated cache pairs, back-to-back launches, HIP events.  Two load forms (all
+    of a workgroup's share in flight): LDS-DMA from 8 waves, and
+    global_load_dwordx4 into registers from 8 and 16 waves; the fastest is the
+    ceiling.  Config-3-shaped workloads only (Hkv x 8 chunks = 256 workgroups
+    of whole KiB), else None."""
+    import fattn
+    path = os.path.join(ROOT, "ggml-cuda-experiments_amd", "lib", "libhbmcopy.so")
+    typ = fattn.TYPE_NAMES[shape["kv_type"]]
+    per = shape["kv_len"] * fattn.row_size(typ, shape["head_dim"]) // 8
+    if not os.path.exists(path) or shape["kv_heads"] * 8 != 256 or per % 1024 or per // 1024 > 160:
+        return None
+    L = C.CDLL(path)
+    if not hasattr(L, "hbm_oneshot"):
+        return None
+    L.hbm_oneshot.restype = C.c_float
+    L.hbm_oneshot.argtypes = [C.c_uint, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+    forms = {"ldsdma_8waves": (8, 0), "vgpr_8waves": (8, 2), "vgpr_16waves": (16, 2)}
+    us = {}
+    for name, (w, mode) in forms.items():
+        t = [L.hbm_oneshot(per, 256, w, mode, 16, 200) for _ in range(3)]
+        t = [x for x in t if x > 0]
+        if t:
+            us[name] = round(min(t), 3)
+    if not us:
+        return None
+    best = min(us, key=us.get)
+    return {"us_per_launch": us, "best": best, "kv_bytes": 2 * 256 * per}
+
+
 def source_hash():
     """Hash of the kernel sources + ABI header: tags the committed PMC traffic so
     a changed kernel never reports stale bytes."""
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "ggml-cuda-experiments_amd", "csrc")
-    for f in sorted(os.listdir(csrc)) + ["../../include/fattn.h"]:
+    for f in sorted(os.listdir(csrc)) + ["../../include/fattn.h", "../../include/fattn_debug.h"]:
         with open(os.path.join(csrc, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
     return h.hexdigest()[:16]
@@ -685,7 +718,14 @@ def roofline(res, args, traffic=None, peaks=None):
     r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": res["kernel"],
          "frac_median_kernel": round(res["rank_bytes"] / (res["kernel_ms_median"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    if peaks:
+    if peaks and peaks.get("oneshot"):
+        os_ = peaks["oneshot"]
+        best_us = os_["us_per_launch"][os_["best"]]
+        r["peak_measured_oneshot"] = round(res["rank_bytes"] / (best_us * 1e-6) / 1e9, 1)
+        r["frac_of_oneshot"] = round(ach / r["peak_measured_oneshot"], 4)
+        r["oneshot_probe"] = {**os_, "note": "tools/hbm_copy.hip hbm_oneshot: this launch's 256 workgroups reading "
+                                             "their K and V slices once, nothing else; min of 3 x 200 launches"}
+    if peaks and "copy_dwordx4" in peaks:
         r["peak_measured_copy"] = peaks["copy_dwordx4"]
         r["frac_of_measured_copy"] = round(ach / peaks["copy_dwordx4"], 4)
         r["peak_measured_read"] = peaks["read_dwordx4"]
@@ -767,6 +807,10 @@ def main():
     if rank == 0:
         traffic = committed_traffic(res["workload"], res["kernel"]) if not multi else None
         peaks = None if args.no_copy_peak or multi else measured_hbm_peaks()
+        if not args.no_copy_peak and not multi:
+            one = oneshot_ceiling(shape)
+            if one:
+                peaks = dict(peaks or {}, oneshot=one)
         sh = res["shard"]
         K = args.steps
         value = res["job_bytes"] * K / res["elapsed"] / 1e9

@@ -61,8 +61,9 @@ std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and compute
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
+std::atomic<int> g_opt_split_loaders{0};    // split kernel, one-row tiles: loader waves (FATTN_OPT_SPLIT_LOADERS): 0 auto, 1 off, 2 on
 std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto, 1 off, 2 on
-std::atomic<int> g_opt_pf_form{0};          // prefill body at D = 128 over f16 rows: 0 auto (5), 1 the 8-wave form, 2-5 one wave per SIMD (fattn_pf4.h)
+std::atomic<int> g_opt_pf_form{0};          // prefill body at D = 128 over f16 rows: 0 auto (5), 1 the 8-wave form, 4-5 one wave per SIMD (fattn_pf4.h)
 std::atomic<int> g_opt_pf_stage{0};         // prefill over Q8_0 / Q4_0: 0 auto (staged to f16), 1 in-kernel dequantisation, 2 staged
 std::atomic<int> g_opt_merge_in_kernel{0};  // 1: multi-row chunk partials merge in-kernel when co-resident (FATTN_OPT_MERGE_IN_KERNEL)
 // launch epochs for the arrival words (SplitArgs::arrival_stamp); 32 bits, 0 skipped
@@ -228,6 +229,18 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     // slower than the second launch (config 4 10.7-10.9 vs 10.0-10.3 us, the
     // config-5 8-rank shard 12.2 vs 11.6-11.7; profiles/r03_merge)
     pl.lds = G.lds_bytes(nbuf, nwv);
+    // loader waves (fattn_split_ld_kernel): one-row tiles on 8 waves whose
+    // whole chunk fits the LDS (every step resident), 16-B rows, D = 64 / 128,
+    // one K / V type; 4 loader waves issue it all up front
+    pl.nld = 0;
+    if (g_opt_split_loaders == 2 && pl.gran == 16 && a.wave_merge == 2 && nwv == 8 && spw <= 2 &&
+        (pl.D == 64 || pl.D == 128) && pl.kt == pl.vt && g_opt_split_nbuf == 0 &&
+        G.lds_bytes(spw, nwv) + kSplitLdFlagBytes <= kLdsPerCU) {
+        pl.nld = kSplitLoaders;
+        a.nbuf = nbuf = spw;
+        a.wave_bytes = G.wave_bytes(spw);
+        pl.lds = G.lds_bytes(spw, nwv) + kSplitLdFlagBytes;
+    }
     const int64_t wgs_cu = std::max(1, std::min(4 * wps / nwv, kLdsPerCU / pl.lds));
     const bool resident = (int64_t)a.n_chunks * Y * S <= (int64_t)pl.cus * wgs_cu;
     a.merge_launch = (a.n_chunks >= 4 && a.wave_merge == 0 && !g_opt_split_fused_merge)
@@ -604,8 +617,8 @@ int make_plan(const fattn_params* p, Plan& pl) {
         // faster than the pipelined form 4, profiles/r05_h, r05_p; form 1 keeps
         // the 8-wave body)
         const int form = g_opt_pf_form == 0 ? 5 : (int)g_opt_pf_form;
-        pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && form >= 2;
-        pl.pf4_sched = form >= 3 ? form - 2 : 0;
+        pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && form >= 4;
+        pl.pf4_sched = form - 2;  // 4: pipelined (SCHED 2), 5: balanced (SCHED 3)
         if (pl.pf4) pl.lds = Pf4Cfg<128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
@@ -714,12 +727,17 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_bd_xcd = value;
             return FATTN_OK;
+        case FATTN_OPT_SPLIT_LOADERS:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_split_loaders = value;
+            return FATTN_OK;
         case FATTN_OPT_SPLIT_XCD:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_split_xcd = value;
             return FATTN_OK;
         case FATTN_OPT_PF_FORM:
-            if (value < 0 || value > 5) return FATTN_ERR_INVALID_ARG;
+            // 2, 3: round 5's unpipelined one-wave-per-SIMD forms, removed (slower)
+            if (value < 0 || value > 5 || value == 2 || value == 3) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_form = value;
             return FATTN_OK;
         case FATTN_OPT_PF_STAGE:
@@ -787,7 +805,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
                       pl.pf_stage ? (pl.stage_kt == FATTN_TYPE_Q8_0 ? "kv_stage_f16<q8_0> + " : "kv_stage_f16<q4_0> + ")
                                   : "",
                       pl.pf_flags ? "pf_mask_flags_kernel + " : "",
-                      pl.pf4 ? (pl.pf4_sched == 3 ? "fattn_pf4_kernel(balanced)" : pl.pf4_sched == 2 ? "fattn_pf4_kernel(pipelined)" : pl.pf4_sched ? "fattn_pf4_kernel(sched1)" : "fattn_pf4_kernel") : "fattn_pf_kernel",
+                      pl.pf4 ? (pl.pf4_sched == 3 ? "fattn_pf4_kernel(balanced)" : "fattn_pf4_kernel(pipelined)") : "fattn_pf_kernel",
                       tn(pl.kt), pl.D, hm);
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,
@@ -797,8 +815,9 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,
                       pl.a.merge_launch ? " + fattn_mq_merge_kernel" : "");
     else
-        std::snprintf(kern, sizeof kern, "fattn_split_kernel<%s,%s,D%d,gran%d,%s,%dwaves>%s%s", tn(pl.kt), tn(pl.vt),
-                      pl.D, pl.gran, hm, pl.nwv, pl.a.xcd_group ? " (xcd order)" : "",
+        std::snprintf(kern, sizeof kern, "%s<%s,%s,D%d,gran%d,%s,%dwaves%s>%s%s",
+                      pl.nld ? "fattn_split_ld_kernel" : "fattn_split_kernel", tn(pl.kt), tn(pl.vt),
+                      pl.D, pl.gran, hm, pl.nwv, pl.nld ? "+4loaders" : "", pl.a.xcd_group ? " (xcd order)" : "",
                       pl.a.merge_launch == 1 ? " + fattn_merge_kernel" : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     const int n = std::snprintf(out, cap, "%s grid(%u,%u,%u) lds %d chunk %d steps/slots %d ws %zu", kern, pl.grid.x,
                                 pl.grid.y, pl.grid.z, pl.lds, pl.a.chunk_len, pl.a.nbuf, pl.ws_bytes);

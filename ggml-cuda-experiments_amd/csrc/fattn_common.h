@@ -8,7 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/fattn.h"
+#include "../../include/fattn_debug.h"
 
 namespace fattn {
 

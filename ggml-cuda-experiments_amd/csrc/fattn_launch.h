@@ -32,6 +32,7 @@ struct Plan {
     size_t ws_bytes, cnt_bytes, ml_bytes;
     int cus;  // compute units of the device the plan is for
     int nwv;  // split kernel: waves per workgroup (4, 8, 16)
+    int nld = 0;  // split kernel: loader waves beside the nwv compute waves (fattn_split_ld_kernel), 0 = none
     bool mq;  // multi-query kernel (fattn_mq.h)
     bool pf;  // prefill kernel (fattn_pf.h)
     bool bd;  // batched-decode kernel (fattn_bd.h)
@@ -91,6 +92,15 @@ int launch_kernel(const void* kern, const Plan& pl, hipStream_t st, const Events
 
 template <int KT, int VT, int D, int GRAN, bool HM, int NWV, int EPI>
 int launch_split_e(const Plan& pl, hipStream_t st, const Events& ev) {
+    if constexpr (GRAN == 16 && NWV == 8 && EPI == 2 && KT == VT && (D == 64 || D == 128)) {
+        if (pl.nld == kSplitLoaders) {
+            auto lk = fattn_split_ld_kernel<KT, VT, D, HM, NWV, kSplitLoaders>;
+            return launch_kernel((const void*)lk, pl, st, ev, [&] {
+                hipLaunchKernelGGL(lk, pl.grid, dim3((NWV + kSplitLoaders) * kWave), pl.lds, st, pl.a);
+            });
+        }
+    }
+    if (pl.nld) return FATTN_ERR_INVALID_ARG;
     auto kern = fattn_split_kernel<KT, VT, D, GRAN, HM, NWV, EPI>;
     return launch_kernel((const void*)kern, pl, st, ev, [&] {
         hipLaunchKernelGGL(kern, pl.grid, dim3(NWV * kWave), pl.lds, st, pl.a);
@@ -187,10 +197,8 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     const void* main_kern = (const void*)kern;
     if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
         if (pl.pf4)
-            main_kern = pl.pf4_sched == 3   ? (const void*)fattn_pf4_kernel<D, HM, 3>
-                        : pl.pf4_sched == 2 ? (const void*)fattn_pf4_kernel<D, HM, 2>
-                        : pl.pf4_sched      ? (const void*)fattn_pf4_kernel<D, HM, 1>
-                                          : (const void*)fattn_pf4_kernel<D, HM, 0>;
+            main_kern = pl.pf4_sched == 3 ? (const void*)fattn_pf4_kernel<D, HM, 3>
+                                          : (const void*)fattn_pf4_kernel<D, HM, 2>;
     }
     return launch_kernel(main_kern, pl, st, ev, [&] {
         if constexpr (KT == FATTN_TYPE_F16 && D % QK == 0) {
@@ -212,12 +220,8 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
             if (pl.pf4) {
                 if (pl.pf4_sched == 3)
                     hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 3>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
-                else if (pl.pf4_sched == 2)
-                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 2>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
-                else if (pl.pf4_sched)
-                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 1>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
                 else
-                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 0>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
+                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 2>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
                 return;
             }
         }

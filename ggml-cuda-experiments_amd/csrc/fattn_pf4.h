@@ -13,20 +13,22 @@
 //  * K and V operands are read from LDS ONCE per wave and tile and used for
 //    both row blocks (the 8-wave form reads them once per 32 rows: twice the
 //    LDS traffic, which bounded it);
-//  * per 64-key tile j, three phases, the vector work of one row block under
-//    the matrix work of the other (cdna_hip_programming.md 'Fused attention
-//    prefill', 4-wave structure):
-//      A_j: S1 = K_j . Q1^T (16 MFMA)       || softmax of rb 0 (scores, max, exp)
-//      B_j: O0 += V_j^T . P0^T (16 MFMA)    || softmax of rb 1
-//      C_j: O1 += V_j^T . P1^T, S0 = K_{j+1} . Q0^T (32 MFMA) || operand reads, DMA issue
-//    with S0 of tile j computed in C_{j-1}; one workgroup barrier per tile (at
-//    the start of C_j);
+//  * per 64-key tile j, two phases of 32 MFMAs, the vector work of one row
+//    block beside the matrix work (cdna_hip_programming.md 'Fused attention
+//    prefill', 4-wave structure), P.V one tile behind S:
+//      A_j: S_j = K_j . Q^T for both row blocks || rb 0's exponentials of
+//           tile j-1, rb 1's scores / max of tile j
+//      B_j: O += V_{j-1}^T . P_{j-1}^T for both  || rb 1's decision and
+//           exponentials of tile j, rb 0's scores / max / decision of tile j
+//    (SCHED 3, "balanced", the default; SCHED 2, "pipelined": each phase's
+//    exponentials in one half and its max pieces in the other); one
+//    workgroup barrier per tile, mid-A;
 //  * HBM -> LDS by LDS-DMA straight into the f16 images (the swizzles of
 //    fattn_pf.h, 16-B granular, so each lane's source offset carries them):
-//    K and V rings of 3 tiles, per-wave mask rings of 2: at C_j, K j+3 (two
-//    tiles of latency), V j+2 and mask j+2 (one tile) into the slots their
-//    tiles j, j-1 and j freed; K and V operands are re-read from LDS per
-//    phase (256 B/clk: LDS has the bandwidth, the register file not the room).
+//    K and V rings of 3 tiles, per-wave mask rings of 2: V j in A_j, K j+3
+//    and mask j+2 in B_j, into the slots their tiles freed; K and V operands
+//    are re-read from LDS per phase (256 B/clk: LDS has the bandwidth, the
+//    register file not the room).
 //
 // LDS (D = 128): K ring 3 x 16 KiB, V ring 3 x 16 KiB, mask [4 waves][2][64
 // rows][128 B] = 64 KiB: 160 KiB.  The epilogue parks each wave's 64
@@ -134,12 +136,7 @@ __device__ __forceinline__ void pin_p(f16x8 (&p)[2][2]) {
     p[1][1] = __builtin_bit_cast(f16x8, d);
 }
 
-// diagnostic builds only: without the scheduling groups / the opaque bases
-#ifdef FATTN_PF4_NO_SGB
-#define PF4_SGB(m, n, id) ((void)0)
-#else
-#define PF4_SGB(m, n, id) __builtin_amdgcn_sched_group_barrier(m, n, id)
-#endif
+// diagnostic builds only: without the opaque bases
 #ifdef FATTN_PF4_SHFL
 #define PF4_XOR32(x, mx) ((mx) ? fmaxf((x), __shfl_xor((x), 32)) : (x) + __shfl_xor((x), 32))
 #else
@@ -168,13 +165,10 @@ __device__ __forceinline__ constexpr int sched_inv(int i) {
     return -1;
 }
 
-// SCHED 0: per tile A (QK rb1 || softmax rb0), B (PV rb0 || softmax rb1),
-// C (PV rb1, QK rb0 of the next tile).  SCHED 1 (rebalanced): the softmax in
-// two parts -- smax (scores, max, rescale decision) and sexp (exponentials,
-// sums, f16 P) -- spread so that every 16-MFMA group carries some of it:
-//   A: QK rb1 || sexp rb0;  B: PV rb0 || smax rb1, sexp rb1 t0;
-//   C1: QK rb0 (next tile) || sexp rb1 t1;  C2: PV rb1 || smax rb0 (next tile).
-// Same arithmetic, same order per row block: both give the same bits.
+// SCHED 2: the pipelined schedule (FATTN_OPT_PF_FORM 4); SCHED 3: the balanced
+// one (FATTN_OPT_PF_FORM 5, the default).  Same arithmetic, same order per row
+// block: both give the same bits as fattn_pf_kernel.  (Round 5's unpipelined
+// three-phase forms, SCHED 0 / 1, measured 18-33 % slower and were removed.)
 template <int D, bool HM, int SCHED>
 __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const SplitArgs a) {
     using C = Pf4Cfg<D>;
@@ -297,28 +291,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             moff[k] = ok ? (uint32_t)q1 * (uint32_t)a.m_nb1 + 16 * pc : a.m_span;
         }
     }
-    auto k_issue = [&](int s) {  // tile s (relative to t0) into K slot s % KS
-        const uint32_t nk = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.k_nb1;
-        const uint32_t dst = lds0 + C::kOff + (s % C::KS) * C::img;
-#pragma unroll
-        for (int i = 0; i < C::NKI; i++) dma<16>(rs.k, dst + (wave + kPf4Waves * i) * 1024, nk + koff0 + 64 * i);
-    };
-    auto v_issue = [&](int s) {
-        const uint32_t nv = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.v_nb1;
-        const uint32_t dst = lds0 + C::vOff + (s % C::VS) * C::img;
-#pragma unroll
-        for (int i = 0; i < C::NKI; i++) dma<16>(rs.v, dst + (wave + kPf4Waves * i) * 1024, nv + voff0 + 64 * i);
-    };
-    auto m_issue = [&](int s) {  // (a +-0 block: through an offset past the descriptor -- no traffic, same count)
-        if constexpr (HM) {
-            const uint32_t n2 = (uint32_t)(t0 + s) * kPfKeys * 2;
-            const bool zero = zero_of(s);
-            const uint32_t dst = lds0 + C::mOff + (wave * C::MS + s % C::MS) * C::maskSlot;
-#pragma unroll
-            for (int k = 0; k < C::NMI; k++)
-                dma<16>(rs.m, dst + k * 1024, (moff[k] == a.m_span || zero) ? a.m_span : moff[k] + n2);
-        }
-    };
 
     // per-lane LDS read offsets within an image: K slice kk, row 32t + c32,
     // half h; V^T gather (ds_read_b64_tr_b16) as fattn_pf.h
@@ -341,18 +313,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         for (int u = 0; u < 4; u++) mrd[t][u] = c32 * 128 + (((4 * t + u) ^ ((c32 >> 1) & 7)) * 16) + 8 * h;
     }
 
-    // ---- prologue: mask 0, V 0, K 0, mask 1, V 1, K 1, K 2 (the steady
-    // state's issue order -- mask s+2, V s+2, K s+3 at C_s -- so that a
-    // counted wait can leave the youngest K in flight)
-    // (SCHED 2: its own order, below)
-    if constexpr (SCHED != 2) {
-        for (int s = 0; s < 2 && s < nt; s++) {
-            m_issue(s);
-            v_issue(s);
-            k_issue(s);
-        }
-        if (nt > 2) k_issue(2);
-    }
 
     const float log2e = 1.4426950408889634f;
     const float scale = a.scale_log2 / log2e;
@@ -368,30 +328,8 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             for (int j = 0; j < 16; j++) o[rb][db][j] = 0.0f;
         }
     }
-    f32x16 s0[2], s1[2];  // S^T of rb 0 (computed in C_{s-1}) and rb 1 (A_s), per subtile
+    f32x16 s0[2], s1[2];  // S^T of rb 0 and rb 1 (both computed in A_j), per subtile
 
-    // S^T of row block rb over tile s: per subtile one chain of NK MFMAs (one
-    // accumulator chain runs at full rate, MI355X_MICROARCH.md constants);
-    // the K operands are read here, per phase, not held across phases (the
-    // register file holds O, Q^T and one tile's V^T operands)
-    auto qk = [&](int s, int rb, f32x16 (&st)[2]) {
-        uint32_t kb = (uint32_t)(C::kOff + (s % C::KS) * C::img) + kbase;
-        PF4_OPAQUE_V(kb);  // (see pv: keeps the reads' offsets immediate)
-        const lds_u8* img = (const lds_u8*)smem + kb;
-        f16x8 ka[2][NK];
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-#pragma unroll
-            for (int kk = 0; kk < NK; kk++) ka[t][kk] = *(const __attribute__((address_space(3))) f16x8*)(img + kk * (kPfKeys * 32) + t * 1024);
-        }
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) st[t][j] = 0.0f;
-#pragma unroll
-            for (int kk = 0; kk < NK; kk++) st[t] = mfma32(ka[t][kk], qop[rb][kk], st[t]);
-        }
-    };
     // mask values of row block rb for tile s (a +-0 block's slot holds the
     // zeros its empty DMA wrote)
     auto mask_reads = [&](int s, int rb, u32x2 (&mk)[2][4]) {
@@ -406,45 +344,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             }
         }
     };
-    // softmax of one row block's tile: scores u = scale * s + mask (natural
-    // units), the tile max (in-lane + one permlane32 swap), the deferred-max
-    // rescale of that block's O and l, then p = exp2(u * c - m) to f16 P^T
-    // fragments in the accumulator's own key order (element j of subtile t is
-    // key 32t + 8(j/4) + 4h + (j%4)); row sums as scalar f32 adds
-    // Branch-free inside the phase (a branch would split the phase into
-    // basic blocks, and the exponentials could no longer sit between the
-    // MFMAs): the rescale decision and l's factor are selects; O's factor is
-    // applied at the next phase boundary (rescale_o), before that block's P.V.
-    // In two parts (the rebalanced schedule places them in different phases):
-    // smax -- scores, tile max, the rescale decision (wave-uniform), l's
-    // factor -- and sexp per subtile -- exponentials, row sums, f16 P^T.
-    auto smax = [&](int rb, const f32x16 (&st)[2], const u32x2 (&mk)[2][4], float (&us)[2][16], float& alpha,
-                    bool& resc) {
-        float tmax = kNegInf;
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    float x = st[t][4 * u + e];
-                    if constexpr (HM) {
-                        const f16x2 mm = as_h2(e < 2 ? mk[t][u].x : mk[t][u].y);
-                        x = fmaf(x, scale, (float)(e & 1 ? mm.y : mm.x));
-                    }
-                    us[t][4 * u + e] = x;
-                    tmax = fmaxf(tmax, x);
-                }
-            }
-        }
-        tmax = PF4_XOR32(tmax, true) * cexp;
-        // deferred max (T13; rare after the first tiles): wave-uniform decision
-        resc = __builtin_amdgcn_ballot_w64(tmax > m_run[rb] + kDeferLog2) != 0;
-        const float m_new = resc ? fmaxf(m_run[rb], tmax) : m_run[rb];
-        alpha = (!resc || m_new == kNegInf) ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
-        m_run[rb] = m_new;
-        l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
-    };
+    // exponentials of one row block's tile (subtile t): p = exp2(u * c - m) to
+    // f16 P^T fragments in the accumulator's own key order (element j of
+    // subtile t is key 32t + 8(j/4) + 4h + (j%4)); row sums as scalar f32 adds
+    // (the last tile's, after the loop; the loop stages the same operations
+    // over its steps, e1 / e2 / e3 below)
     auto sexp = [&](int rb, int t, const float (&us)[2][16], f16x8 (&pb)[2][2]) {
         const float nm = (m_run[rb] == kNegInf) ? 0.0f : -m_run[rb];
         float la = l2[rb].x, lb = l2[rb].y;
@@ -464,130 +368,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         }
         l2[rb] = f32x2{la, lb};
     };
-    auto softmax = [&](int rb, const f32x16 (&st)[2], const u32x2 (&mk)[2][4], f16x8 (&pb)[2][2], float& alpha,
-                       bool& resc) {
-        float us[2][16];
-        smax(rb, st, mk, us, alpha, resc);
-        sexp(rb, 0, us, pb);
-        sexp(rb, 1, us, pb);
-    };
-    // (the empty asm keeps hipcc from if-converting the rare branch into an
-    // unconditional multiply of O by alpha = 1: 128 VALU + AGPR moves a tile)
-    auto rescale_o = [&](int rb, bool resc, float alpha) {  // (at a phase boundary; resc: wave-uniform)
-        if (__builtin_expect(resc, 0)) {
-            asm volatile("; rescale O" ::: "memory");
-#pragma unroll
-            for (int db = 0; db < NDB; db++) o[rb][db] *= alpha;
-        }
-    };
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
     // (LDS-space arithmetic: the per-read offsets fold into the instructions'
     // immediate; through a generic pointer every read got its own v_add)
     lds_u8* const lsm = (lds_u8*)smem;
-    // O_rb^T += V_s^T . P_rb^T: per subtile t, its V^T operands (gathered by
-    // ds_read_b64_tr_b16 in the accumulator's key order) then 2 x NDB MFMAs;
-    // the V^T operands are read per phase (B for rb 0, C for rb 1), not held
-    auto pv_t = [&](int s, int rb, int t, const f16x8 (&pb)[2][2]) {
-        // (the per-tile base through an empty asm: otherwise hipcc hoists
-        // vbase + every read's offset out of the loop -- 32 loop-invariant
-        // addresses, spilled to AGPRs -- and no offset folds into a read)
-        uint32_t b0 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[0];
-        uint32_t b1 = (uint32_t)(C::vOff + (s % C::VS) * C::img) + vbase[1];
-        PF4_OPAQUE_V2(b0, b1);
-        lds_u8* const img0 = lsm + b0;
-        lds_u8* const img1 = lsm + b1;
-        u32x4 va[2][NDB];
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-#pragma unroll
-            for (int db = 0; db < NDB; db++) {
-                const uint32_t off = db * (kPfKeys * 64) + t * 2048 + q * 1024;
-                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img0 + off));
-                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img1 + off));
-                const u32x2 a2 = __builtin_bit_cast(u32x2, lo), b2 = __builtin_bit_cast(u32x2, hi);
-                va[q][db] = u32x4{a2.x, a2.y, b2.x, b2.y};
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-#pragma unroll
-            for (int db = 0; db < NDB; db++) o[rb][db] = mfma32(__builtin_bit_cast(f16x8, va[q][db]), pb[t][q], o[rb][db]);
-        }
-    };
-    auto pv = [&](int s, int rb, const f16x8 (&pb)[2][2]) {
-        pv_t(s, rb, 0, pb);
-        pv_t(s, rb, 1, pb);
-    };
 
-    // ---- S0 of tile 0 (the loop's C phase computes it for the next tile):
-    // K 0 landed (mask 0 and V 0 before it; mask 1, V 1, K 1, K 2 may fly)
-    if (SCHED != 2 && nt > 0) {
-        const int later = (HM && nt > 1 ? C::NMI : 0) + (nt > 1 ? 2 * C::NKI : 0) + (nt > 2 ? C::NKI : 0);
-        static_assert(C::NMI == 2 * C::NKI, "the prologue's wait counts: 0, 8, 12, 16, 20");
-        switch (__builtin_amdgcn_readfirstlane(later)) {  // (wave-uniform)
-            case 5 * C::NKI: wait_vmcnt_c<5 * C::NKI>(); break;
-            case 4 * C::NKI: wait_vmcnt_c<4 * C::NKI>(); break;
-            case 3 * C::NKI: wait_vmcnt_c<3 * C::NKI>(); break;
-            case 2 * C::NKI: wait_vmcnt_c<2 * C::NKI>(); break;
-            default: wait_vmcnt_c<0>(); break;
-        }
-        __syncthreads();
-        qk(0, 0, s0);
-    }
-
-    if constexpr (SCHED == 0) {
-        for (int s = 0; s < nt; s++) {
-            // ---- A: S1 = K_s . Q1^T  ||  softmax of rb 0
-            u32x2 mk0[2][4], mk1[2][4];
-            f16x8 p0[2][2], p1[2][2];
-            float al0, al1;
-            bool rs0, rs1;
-            mask_reads(s, 0, mk0);
-            qk(s, 1, s1);
-            softmax(0, s0, mk0, p0, al0, rs0);
-            PF4_SGB(0x100, NK + (HM ? 8 : 0), 0);  // subtile 0's K operands, the mask
-#pragma unroll
-            for (int i = 0; i < 2 * NK; i++) {
-                PF4_SGB(0x008, 1, 0);  // one MFMA
-                PF4_SGB(0x002, 5, 0);  // up to five VALU
-                if (i < NK) PF4_SGB(0x100, 1, 0);  // subtile 1's K operands
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            rescale_o(0, rs0, al0);
-            // ---- B: O0 += V_s^T . P0^T  ||  softmax of rb 1
-            mask_reads(s, 1, mk1);
-            pv(s, 0, p0);
-            softmax(1, s1, mk1, p1, al1, rs1);
-            // the mask and subtile 0's V^T reads, then per MFMA up to five VALU
-            // and one of subtile 1's V^T reads
-            PF4_SGB(0x100, 4 * NDB + (HM ? 8 : 0), 0);
-#pragma unroll
-            for (int i = 0; i < 4 * NDB; i++) {
-                PF4_SGB(0x008, 1, 0);
-                PF4_SGB(0x002, 5, 0);
-                if (i < 4 * NDB) PF4_SGB(0x100, 1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            // ---- C: barrier (every wave is done with tile s's K and mask and
-            // tile s-1's V; tile s+1's mask and V and K landed), refill, O1 +=
-            // V_s^T . P1^T, S0 = K_{s+1} . Q0^T
-            {
-                // issued at C_{s-1} (or in the prologue): mask s+1, V s+1, K s+2 --
-                // K s+2 may fly on
-                if (s + 2 < nt) wait_vmcnt_c<C::NKI>();
-                else wait_vmcnt_c<0>();
-            }
-            __syncthreads();
-            if (s + 2 < nt) {
-                m_issue(s + 2);
-                v_issue(s + 2);
-            }
-            if (s + 3 < nt) k_issue(s + 3);
-            rescale_o(1, rs1, al1);
-            pv(s, 1, p1);
-            if (s + 1 < nt) qk(s + 1, 0, s0);
-        }
-    } else if constexpr (SCHED >= 2) {
+    {
         // A workgroup whose live tiles all hold +-0 masks (the flags pass's 2,
         // SURVEY's zero-mask prefill) runs the body without mask values in
         // LDS (ZM): no mask DMA, reads or waits, scores fma(s, scale, 0) --
@@ -1214,86 +1000,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         } else {
             body2(std::false_type());
         }
-    } else {
-        // the rebalanced schedule (see the kernel's comment)
-        float us0[2][16], us1[2][16];
-        float al0 = 1.0f, al1 = 1.0f;
-        bool rs0 = false, rs1 = false;
-        if (nt > 0) {
-            u32x2 mk[2][4];
-            mask_reads(0, 0, mk);
-            smax(0, s0, mk, us0, al0, rs0);
-        }
-        auto iter = [&](int s, auto has_next) {
-            constexpr bool NX = decltype(has_next)::value;
-            f16x8 p0[2][2], p1[2][2];
-            u32x2 mk1[2][4], mk0[2][4];
-            rescale_o(0, rs0, al0);
-            // ---- A: S1 = K_s . Q1^T  ||  rb 0's exponentials
-            mask_reads(s, 1, mk1);
-            qk(s, 1, s1);
-            sexp(0, 0, us0, p0);
-            sexp(0, 1, us0, p0);
-            PF4_SGB(0x100, NK + (HM ? 8 : 0), 0);
-#pragma unroll
-            for (int i = 0; i < 2 * NK; i++) {
-                PF4_SGB(0x008, 1, 0);
-                PF4_SGB(0x002, 7, 0);
-                if (i < NK) PF4_SGB(0x100, 1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            // ---- B: O0 += V_s^T . P0^T  ||  rb 1's scores and max, its first subtile's exponentials
-            pv(s, 0, p0);
-            smax(1, s1, mk1, us1, al1, rs1);
-            sexp(1, 0, us1, p1);
-            PF4_SGB(0x100, 4 * NDB, 0);
-#pragma unroll
-            for (int i = 0; i < 4 * NDB; i++) {
-                PF4_SGB(0x008, 1, 0);
-                PF4_SGB(0x002, 9, 0);
-                PF4_SGB(0x100, 1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            // ---- C: barrier (as SCHED 0), refill
-            if (s + 2 < nt) wait_vmcnt_c<C::NKI>();
-            else wait_vmcnt_c<0>();
-            __syncthreads();
-            if (s + 2 < nt) {
-                m_issue(s + 2);
-                v_issue(s + 2);
-            }
-            if (s + 3 < nt) k_issue(s + 3);
-            rescale_o(1, rs1, al1);
-            // ---- C1: S0 = K_{s+1} . Q0^T  ||  rb 1's second subtile's exponentials
-            if constexpr (NX) {
-                mask_reads(s + 1, 0, mk0);
-                qk(s + 1, 0, s0);
-            }
-            sexp(1, 1, us1, p1);
-            if constexpr (NX) {
-                PF4_SGB(0x100, NK + (HM ? 8 : 0), 0);
-#pragma unroll
-                for (int i = 0; i < 2 * NK; i++) {
-                    PF4_SGB(0x008, 1, 0);
-                    PF4_SGB(0x002, 4, 0);
-                    if (i < NK) PF4_SGB(0x100, 1, 0);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            // ---- C2: O1 += V_s^T . P1^T  ||  rb 0's scores and max of the next tile
-            pv(s, 1, p1);
-            if constexpr (NX) smax(0, s0, mk0, us0, al0, rs0);
-            PF4_SGB(0x100, 4 * NDB, 0);
-#pragma unroll
-            for (int i = 0; i < 4 * NDB; i++) {
-                PF4_SGB(0x008, 1, 0);
-                PF4_SGB(0x002, 6, 0);
-                PF4_SGB(0x100, 1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        for (int s = 0; s + 1 < nt; s++) iter(s, std::true_type());
-        if (nt > 0) iter(nt - 1, std::false_type());
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 

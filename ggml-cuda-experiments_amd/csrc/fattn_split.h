@@ -620,9 +620,36 @@ static __device__ unsigned long long* g_stamps;  // one per translation unit (fa
             atomicMax(&g_stamps[blk_ * 16 * 16 + (k)], (unsigned long long)(v));      \
         }                                                                                       \
     } while (0)
+// The split kernel keeps its stamps in LDS (a static array) and each wave
+// stores its own at the kernel's end (FATTN_SSTAMP_FLUSH): a global store per
+// stamp would be counted by vmcnt and every counted wait would wait for it
+// too, stretching the very timeline it measures (round 3's stamps: a 17 us
+// span for an 11 us launch).
+__device__ __forceinline__ unsigned long long* split_stamp_slots() {
+    __shared__ unsigned long long s[16 * 16];
+    return s;
+}
+#define FATTN_SSTAMP(k)                                                                          \
+    do {                                                                                         \
+        if (lane == 0) split_stamp_slots()[wave * 16 + (k)] = __builtin_amdgcn_s_memrealtime();  \
+    } while (0)
+#define FATTN_SSTAMP_INIT()                                                                      \
+    do {                                                                                         \
+        if (lane < 16) split_stamp_slots()[wave * 16 + lane] = 0ull;                             \
+    } while (0)
+#define FATTN_SSTAMP_FLUSH()                                                                     \
+    do {                                                                                         \
+        if (lane < 16 && g_stamps) {                                                             \
+            const int64_t blk_ = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
+            g_stamps[(blk_ * 16 + wave) * 16 + lane] = split_stamp_slots()[wave * 16 + lane];    \
+        }                                                                                        \
+    } while (0)
 #else
 #define FATTN_STAMP(k) do { } while (0)
 #define FATTN_STAMP_MAX(k, v) do { } while (0)
+#define FATTN_SSTAMP(k) do { } while (0)
+#define FATTN_SSTAMP_INIT() do { } while (0)
+#define FATTN_SSTAMP_FLUSH() do { } while (0)
 #endif
 
 // ---------------------------------------------------------------- kernel
@@ -694,11 +721,11 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
         if (g == 0) st_sc1_x2(a.ws_ml + 2 * (tile * NP + part), u32x2{bits(m_run), bits(l_tot)});
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FATTN_STAMP(12);
+    FATTN_SSTAMP(12);
     int last = 0;
     if (lane == 0) last = arrive_last(a, tile, NP);
     last = __builtin_amdgcn_readfirstlane(last);
-    FATTN_STAMP(14);
+    FATTN_SSTAMP(14);
     if (!last) return;
     // ---- merge: lane half h = lane / 32 takes the parts of parity h, dims
     // 4 (lane % 32) .. +3, one 16-B load per part (parts past NP fall outside
@@ -717,7 +744,7 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     issue(0);
     const uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8));      // lane p: m of part p
     const uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * 8 + 4));  //          l of part p
-    FATTN_STAMP(15);
+    FATTN_SSTAMP(15);
     const float mp = lane < NP ? __builtin_bit_cast(float, mlm) : kNegInf;
     const float M = seg_reduce<true>(mp, 64);
     const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M);
@@ -745,7 +772,7 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
     float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D + d4;
     const float inv = L == 0.0f ? __builtin_nanf("") : 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
     *(f32x4*)out = acc * inv;
-    FATTN_STAMP(13);
+    FATTN_SSTAMP(13);
 }
 
 // Log-sum-exp merge of NP <= 64 one-row partials of a tile: O rows [NP][D]
@@ -849,7 +876,7 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
     }
     __syncthreads();
     if (wave != 0) return;
-    FATTN_STAMP(11);
+    FATTN_SSTAMP(11);
     // ---- wave 0: merge the NW states
     const int h = lane / LPP, d4 = 4 * (lane % LPP);
     const f32x2 ml = lane < NW ? *(const f32x2*)((const float*)(smem + lane * region) + D) : f32x2{kNegInf, 0.0f};
@@ -907,14 +934,14 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
     if (h == 0) st_sc1(po + d4, u32x4{bits(acc.x), bits(acc.y), bits(acc.z), bits(acc.w)});
     if (lane == 0) st_sc1_x2(a.ws_ml + 2 * (tile * a.n_chunks + chunk), u32x2{bits(M), bits(L)});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FATTN_STAMP(12);
+    FATTN_SSTAMP(12);
 #ifdef FATTN_DIAG_NOATOMIC
     return;  // diagnostic build only: stop after the published row drained
 #endif
     int last = 0;
     if (lane == 0) last = arrive_last(a, tile, a.n_chunks);
     last = __builtin_amdgcn_readfirstlane(last);
-    FATTN_STAMP(14);
+    FATTN_SSTAMP(14);
     if (!last) return;
     // as few load slots per lane as the chunk count needs (a slot past it is
     // still an issued instruction; config 3: 8 chunks = 4 slots)
@@ -924,7 +951,7 @@ __device__ __forceinline__ void wg_row_merge(const SplitArgs& a, const f32x4 (&o
     if (need <= 4) merge_row_parts<D, 4>(po_all, pml_all, a.n_chunks, out, lane);
     else if (need <= 8) merge_row_parts<D, 8>(po_all, pml_all, a.n_chunks, out, lane);
     else merge_row_parts<D>(po_all, pml_all, a.n_chunks, out, lane);
-    FATTN_STAMP(13);
+    FATTN_SSTAMP(13);
 }
 
 // Tail of a split-KV workgroup: the waves' (O, m, l) states merge.  EPI (the
@@ -997,7 +1024,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
         mml[2 * m + 1] = l_tot;
     }
     __syncthreads();
-    FATTN_STAMP(11);
+    FATTN_SSTAMP(11);
 
     constexpr int EPT = epi_ept<D>();  // outputs per thread: 16 rows x D over 256 threads
     const int tm = threadIdx.x / 16;
@@ -1047,7 +1074,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
                 *(f32x4*)(out + e) = v;
             }
         }
-        FATTN_STAMP(12);
+        FATTN_SSTAMP(12);
         return;
     }
 
@@ -1088,7 +1115,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
         if (threadIdx.x == 0) *flag = tile_arrive_wait(a, tile, a.n_chunks);
         __syncthreads();
         const bool ok = *flag != 0;
-        FATTN_STAMP(12);
+        FATTN_SSTAMP(12);
         for (int r = chunk * NW + wave; r < rv; r += NW * a.n_chunks) {  // wave-uniform
             const int64_t s0 = tile * a.n_chunks * kRows + r;  // chunk 0's row r
             float* out = dst_row(r);
@@ -1099,7 +1126,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
                                                   __builtin_nanf("")};
             }
         }
-        FATTN_STAMP(13);
+        FATTN_SSTAMP(13);
         return;
     }
     // every storing wave drains: the merging workgroup reads its own partial back too
@@ -1111,10 +1138,10 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
     int* last_flag = (int*)smem;
     if (threadIdx.x == 0) *last_flag = arrive_last(a, tile, a.n_chunks);
     __syncthreads();
-    FATTN_STAMP(12);
+    FATTN_SSTAMP(12);
     if (!*last_flag) return;
     combine_tile<D, (D == 128 && KT != FATTN_TYPE_F16) ? 8 : 2>(a, tile, qt, hs, ik2, iq3, rv, 0, smem);
-    FATTN_STAMP(13);
+    FATTN_SSTAMP(13);
 }
 
 // One 32-position step of one wave: S^T = K.Q^T for the step's two 16-row
@@ -1319,7 +1346,8 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4;
     const int i16 = lane & 15;
-    FATTN_STAMP(0);
+    FATTN_SSTAMP_INIT();
+    FATTN_SSTAMP(0);
 
     // ---- tile decode: y -> (kv head, head subgroup, query-row tile)
     int chunk, y, iq3;
@@ -1422,7 +1450,7 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     if (a.n_chunks > 1 && a.merge_launch != 1 && lane == 0 && (EPI == 1 || wave == 0))
         arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
 
-    FATTN_STAMP(1);
+    FATTN_SSTAMP(1);
     if (a.split_prio == 2) __builtin_amdgcn_s_setprio(0);
     wait_steps<NI>(pro);  // Q and the mask words landed (the steps issued after them may fly on)
     // every untracked result, on every path, passes its fence right behind
@@ -1471,7 +1499,7 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
         const int ahead = min(nbuf - 1, nsteps - 1 - s);  // steps issued after step s
         // K and mask of step s landed (its V and the later steps may fly on)
         wait_steps_plus<NI, P::NIV>(ahead);
-        if (s < 8) FATTN_STAMP(2 + s);
+        if (s < 8) FATTN_SSTAMP(2 + s);
 #ifdef FATTN_DIAG_NOCOMPUTE
         // diagnostic build only: memory-side ceiling of this access pattern
         wait_steps<NI>(ahead);
@@ -1486,6 +1514,7 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
         asm volatile("" : "+s"(s_opaque));
         split_step<KT, VT, D, HM>(a, wbuf + cur * C::stepBytes, qop, mq, g, i16, min(kStep, w_hi - n0), s_opaque == 0,
                                   m_run, l_run, o, corr, [&] { wait_steps<NI>(ahead); });
+        if (nsteps <= 4 && s < 2) FATTN_SSTAMP(6 + 2 * s);  // (stamps build: step s computed)
 
         // -- refill this buffer with step s + nbuf (K/V not fetched if -inf)
         if (s + nbuf < nsteps) {
@@ -1493,6 +1522,7 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
             const int sn = s + nbuf;
             issue_step<KT, VT, D, GRAN, HM>(a, rs, w_lo + sn * kStep, mrow0, wbuf + cur * C::stepBytes, lane,
                                             sn >= 64 || ((live >> sn) & 1));
+            if (nsteps <= 4 && s < 2) FATTN_SSTAMP(7 + 2 * s);  // (stamps build: step s + nbuf issued)
         }
         cur = (cur + 1 == nbuf) ? 0 : cur + 1;
     }
@@ -1507,9 +1537,156 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
     }
     return;
 #endif
-    FATTN_STAMP(10);
+    FATTN_SSTAMP(10);
     split_epilogue<KT, VT, D, NWV, EPI>(a, o, m_run, l_run, corr, wave, lane, qt, hs, ik2, iq3, y, chunk, smem, a.wave_bytes,
                                    true, false);
+    FATTN_SSTAMP_FLUSH();
+}
+
+// ---------------------------------------------------------------- loader waves
+// The split kernel with its DMA issue taken off the compute waves (one-row
+// tiles whose whole chunk fits the LDS; config 3).  In fattn_split_kernel each
+// wave issues its own steps: a wave that issues step s + 1 before computing
+// step s stalls on the CU's full memory queue before it can compute (both
+// steps in flight: 12.2 vs 11.3 us), and a wave that issues it after computing
+// step s leaves that queue idle for the whole of step s's compute (stamps,
+// round 6: step 0 lands at 3.9 us, is computed by 5.7, step 1 issued at 6.2).
+// Here NLD loader waves issue every step of the workgroup up front -- step 0
+// of every compute wave first, then step 1 -- and hand each (wave, step) over
+// by two LDS flags (K + mask landed, V landed), set behind counted vmcnt
+// waits; the NWV compute waves never issue a DMA, so step 1 streams in while
+// step 0 computes.  Same compute (split_step) and epilogue (wg_row_merge).
+// Every step of the chunk is resident: LDS = NWV x steps x stepBytes + flags.
+constexpr int kSplitLoaders = 4;
+constexpr int kSplitLdFlagBytes = 256;  // [8 waves][<= 2 steps][2] u32 flags, past the step buffers
+
+// (LDS flag of a (wave, step) hand-off: relaxed atomic load, polled with
+// s_sleep; the empty asm keeps every later LDS read below the poll -- LDS
+// instructions of one wave execute in order, and the loader set the flag only
+// after its counted wait saw the DMA data written)
+__device__ __forceinline__ void wait_lds_flag(const uint32_t* f) {
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0)
+        __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+template <int KT, int VT, int D, bool HM, int NWV, int NLD>
+__global__ __launch_bounds__((NWV + NLD) * kWave, 1) void fattn_split_ld_kernel(const SplitArgs a) {
+    using C = SplitCfg<KT, VT, D>;
+    using P = StepPlan<KT, VT, D, 16>;
+    constexpr int NI = P::NIKV + (HM ? P::NIM : 0);  // VMEM instructions per step
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NB = (D + QK - 1) / QK;
+    constexpr int NC = D / 16;
+    constexpr float kNegInf = -__builtin_inff();
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4;
+    const int i16 = lane & 15;
+    FATTN_SSTAMP_INIT();
+    FATTN_SSTAMP(0);
+
+    int chunk, y, iq3;
+    tile_coords(a, chunk, y, iq3);
+    int qt = 0, hs = 0, ik2 = y, ik3 = iq3;
+    if (a.n_qt != 1 || a.n_hsub != 1) {
+        qt = y % a.n_qt;
+        hs = (y / a.n_qt) % a.n_hsub;
+        ik2 = y / (a.n_qt * a.n_hsub);
+    }
+    if (a.rk3 != 1) ik3 = iq3 / a.rk3;
+    const int wl = a.chunk_len / NWV;    // positions per compute wave
+    const int spw = a.nbuf;              // steps per compute wave, all resident (planner: nbuf == steps)
+    const int mrow0 = qt * a.QPT;
+    const int c_hi = min(a.N, (chunk + 1) * a.chunk_len);
+    uint32_t* flags = (uint32_t*)(smem + NWV * a.wave_bytes);  // [NWV][spw][2]: K + mask, V
+    if (threadIdx.x < NWV * spw * 2) flags[threadIdx.x] = 0u;
+    __syncthreads();
+
+    if (wave >= NWV) {
+        // ---- loader: units u = s * NWV + w (every wave's step 0 first), dealt
+        // round-robin; U units per loader, issued back to back, then handed
+        // over oldest first (K + mask when all but the unit's V and the later
+        // units landed, V when all but the later units)
+        __builtin_amdgcn_s_setprio(3);
+        const int L = wave - NWV;
+        const int U = spw * NWV / NLD;  // (planner: <= 4, a whole number)
+        StepSrc rs;
+        rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
+        rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
+        rs.m = make_srd(a.mask, HM ? a.m_span : 0);
+        for (int k = 0; k < U; k++) {
+            const int u = L + NLD * k, w = u % NWV, s = u / NWV;
+            const int n0 = chunk * a.chunk_len + w * wl + s * kStep;
+            issue_step<KT, VT, D, 16, HM>(a, rs, n0, mrow0, smem + w * a.wave_bytes + s * C::stepBytes, lane);
+        }
+        FATTN_SSTAMP(1);
+        for (int k = 0; k < U; k++) {
+            const int u = L + NLD * k, w = u % NWV, s = u / NWV;
+            uint32_t* f = flags + (w * spw + s) * 2;
+            wait_steps_plus<NI, P::NIV>(U - 1 - k);
+            if (lane == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            wait_steps<NI>(U - 1 - k);
+            if (lane == 0) __hip_atomic_store(f + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();  // wg_row_merge's one barrier (the loaders then leave)
+        FATTN_SSTAMP_FLUSH();
+        return;
+    }
+
+    // ---- compute wave: the split kernel's, minus the DMA
+    const int m = i16;
+    const int mq = div_R(a, m);
+    const int mh = hs * a.R + (m - mq * a.R);
+    const int iq1 = qt * a.QPT + mq;
+    const int iq2 = ik2 * a.rk2 + mh;
+    const bool row_ok = (m < a.QPT * a.R) && (iq1 < a.NQ) && (mh < a.rk2);
+    const int w_lo = chunk * a.chunk_len + wave * wl;
+    const int w_hi = min(c_hi, w_lo + wl);
+    const int nsteps = w_hi > w_lo ? (w_hi - w_lo + kStep - 1) / kStep : 0;
+    f16x8 qop[NB];
+    {
+        const __amdgpu_buffer_rsrc_t qs = make_rsrc(a.q + (int64_t)iq3 * a.q_nb3, a.q_span);
+        const uint32_t qoff = row_ok ? (uint32_t)iq1 * (uint32_t)a.q_nb1 + (uint32_t)iq2 * (uint32_t)a.q_nb2 + 32 * g
+                                     : a.q_span;
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const uint32_t qb = (D % QK == 0 || 32 * b + 8 * g < D) ? qoff + 128 * b : a.q_span;
+            const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qb, 0, 0));
+            const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qb + 16, 0, 0));
+            f16x8 h;
+            h.s0 = (f16)x0.x; h.s1 = (f16)x0.y; h.s2 = (f16)x0.z; h.s3 = (f16)x0.w;
+            h.s4 = (f16)x1.x; h.s5 = (f16)x1.y; h.s6 = (f16)x1.z; h.s7 = (f16)x1.w;
+            qop[b] = h;
+        }
+    }
+    if (a.n_chunks > 1 && lane == 0 && wave == 0) arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
+
+    float m_run = kNegInf;
+    float l_run = 0.0f;
+    f32x4 o[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) o[c] = f32x4{0, 0, 0, 0};
+    float corr[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) corr[b] = 0.0f;
+    uint8_t* wbuf = smem + wave * a.wave_bytes;
+    for (int s = 0; s < nsteps; s++) {
+        const uint32_t* f = flags + (wave * spw + s) * 2;
+        wait_lds_flag(f);
+        if (s < 2) FATTN_SSTAMP(2 + s);
+        const int n0 = w_lo + s * kStep;
+        int s_opaque = s;
+        asm volatile("" : "+s"(s_opaque));
+        split_step<KT, VT, D, HM>(a, wbuf + s * C::stepBytes, qop, mq, g, i16, min(kStep, w_hi - n0), s_opaque == 0,
+                                  m_run, l_run, o, corr, [&] { wait_lds_flag(f + 1); });
+        if (s < 2) FATTN_SSTAMP(6 + 2 * s);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    FATTN_SSTAMP(10);
+    split_epilogue<KT, VT, D, NWV, 2>(a, o, m_run, l_run, corr, wave, lane, qt, hs, ik2, iq3, y, chunk, smem,
+                                      a.wave_bytes, true, false);
+    FATTN_SSTAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------- merge launch

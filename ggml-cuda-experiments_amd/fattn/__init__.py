@@ -30,7 +30,7 @@ ERRORS = {
     -4: "FATTN_ERR_BAD_STRIDE", -5: "FATTN_ERR_WORKSPACE", -6: "FATTN_ERR_LAUNCH", -7: "FATTN_ERR_ALIGNMENT",
 }
 
-# every symbol include/fattn.h declares
+# every symbol include/fattn.h and include/fattn_debug.h declare
 EXPORTS = (
     "fattn_workspace_size", "fattn_workspace_init", "fattn_ext", "fattn_ext_events", "fattn_ext_f16_launch", "fattn_row_workspace_size", "fattn_row",
     "fattn_dequantize", "fattn_quantize", "fattn_strerror", "fattn_row_size", "fattn_version", "fattn_set_option",
@@ -55,12 +55,13 @@ OPT_BD_XCD = 25
 OPT_SPLIT_XCD = 26
 OPT_PF_STAGE = 28
 OPT_PF_FORM = 29
-# every option's default (include/fattn.h): reset_options() restores them
+OPT_SPLIT_LOADERS = 30
+# every option's default (include/fattn_debug.h): reset_options() restores them
 OPTION_DEFAULTS = {
     OPT_MQ_ROWS_PER_WAVE: 0, OPT_MQ_DISABLE: 0, OPT_SPLIT_STEPS: 0, OPT_SPLIT_INFLIGHT: 0, OPT_PF: 0,
     OPT_PF_STAGGER: 2, OPT_SPLIT_WAVE_MERGE: 0, OPT_SPLIT_PRIO: 0, OPT_PF_SKIP: 0, OPT_MQ_MIN_ROWS: 0,
     OPT_SPLIT_WAVES: 0, OPT_SPLIT_SKIP: 0, OPT_SPLIT_MERGE: 0, OPT_BD: 0, OPT_MERGE_IN_KERNEL: 0, OPT_BD_XCD: 0, OPT_SPLIT_XCD: 0,
-    OPT_PF_STAGE: 0, OPT_PF_FORM: 0,
+    OPT_PF_STAGE: 0, OPT_PF_FORM: 0, OPT_SPLIT_LOADERS: 0,
 }
 
 
@@ -138,7 +139,7 @@ def _check(rc: int, what: str):
 
 
 def set_option(option: int, value: int):
-    """Planner override (include/fattn.h fattn_set_option): OPT_MQ_ROWS_PER_WAVE
+    """Planner override (include/fattn_debug.h fattn_set_option): OPT_MQ_ROWS_PER_WAVE
     (0 auto, 16, 32), OPT_MQ_DISABLE (1 = split-KV kernel only), OPT_SPLIT_STEPS
     (32-position steps per wave, 0 auto) or OPT_SPLIT_INFLIGHT (steps in flight, 0 auto)."""
     _check(lib().fattn_set_option(option, value), "fattn_set_option")

@@ -11,10 +11,25 @@ import fattn
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_symbols():
-    src = open(os.path.join(ROOT, "include", "fattn.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(fattn_\w+)\s*\(", src, flags=re.M)))
+def header_symbols(names=("fattn.h", "fattn_debug.h")):
+    """The functions include/fattn.h (the drop-in ABI) and include/fattn_debug.h
+    (its diagnostics) declare."""
+    syms = set()
+    for n in names:
+        src = open(os.path.join(ROOT, "include", n)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        syms |= set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(fattn_\w+)\s*\(", src, flags=re.M))
+    return sorted(syms)
+
+
+def test_drop_in_header_lists_no_diagnostics():
+    """include/fattn.h holds the drop-in entry points only: the planner
+    overrides, fattn_describe and fattn_ext_events live in fattn_debug.h."""
+    main = header_symbols(("fattn.h",))
+    assert "fattn_ext" in main and "fattn_row" in main and "fattn_cpy" in main
+    for s in ("fattn_set_option", "fattn_describe", "fattn_ext_events"):
+        assert s not in main and s in header_symbols(("fattn_debug.h",))
+    assert "FATTN_OPT_" not in open(os.path.join(ROOT, "include", "fattn.h")).read()
 
 
 def test_header_symbols_parsed():
@@ -225,20 +240,22 @@ def test_mq_min_rows_explicit_default_lifts_the_wide_gate():
 
 def test_pf_form_option():
     """The prefill body over f16 rows at D = 128: the balanced pipelined
-    one-wave-per-SIMD body by default, the 8-wave body with FATTN_OPT_PF_FORM = 1, the
-    other one-wave-per-SIMD schedules with 2 / 3 / 5 (5: the balanced
-    pipeline); other head dims keep the 8-wave body."""
+    one-wave-per-SIMD body by default, the 8-wave body with FATTN_OPT_PF_FORM = 1,
+    the pipelined one with 4, the balanced one with 5; 2 and 3 (round 5's
+    unpipelined one-wave-per-SIMD forms) were removed and are rejected; other
+    head dims keep the 8-wave body."""
     p = _params(NQ=4096, kt=fattn.TYPE_F16)
     assert "fattn_pf4_kernel(balanced)<f16,D128" in fattn.describe(p)
-    want = {1: "fattn_pf_kernel<f16,D128", 2: "fattn_pf4_kernel<f16,D128", 3: "fattn_pf4_kernel(sched1)<f16,D128",
-            4: "fattn_pf4_kernel(pipelined)<f16,D128", 5: "fattn_pf4_kernel(balanced)<f16,D128"}
+    want = {1: "fattn_pf_kernel<f16,D128", 4: "fattn_pf4_kernel(pipelined)<f16,D128",
+            5: "fattn_pf4_kernel(balanced)<f16,D128"}
     for form, name in want.items():
         with fattn.options({fattn.OPT_PF_FORM: form}):
             assert name in fattn.describe(p), (form, fattn.describe(p))
     assert "fattn_pf_kernel<f16,D64" in fattn.describe(_params(NQ=4096, D=64, kt=fattn.TYPE_F16))
-    with pytest.raises(Exception):
-        with fattn.options({fattn.OPT_PF_FORM: 6}):
-            pass
+    for bad in (2, 3, 6):
+        with pytest.raises(Exception):
+            with fattn.options({fattn.OPT_PF_FORM: bad}):
+                pass
 
 
 def test_pf_stage_option_and_workspace():

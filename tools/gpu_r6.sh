@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round 6's GPU passes, one function per pass: bash tools/gpu_r6.sh <pass>
+source tools/gpu_round.sh
+export TMPDIR=/tmp
+
+# First pass: the one-shot read ceiling of config 3's launch shape, the default
+# bench line of the round-5 tree, the world-1 RCCL bench lines (graph, eager).
+pass_a() {
+  run oneshot 300 python -u tools/oneshot.py
+  run bench 500 python -u bench.py
+  run dist_graph 300 python -u bench.py --dist --no-side-line
+  run dist_eager 300 python -u bench.py --dist --no-side-line --eager-gather
+}
+
+
+
+# Second pass: config 3's timeline from the LDS-stamps build (auto plan, then
+# both steps in flight, 16 waves).
+pass_b() {
+  run stamps_auto 200 python -u tools/stamps.py
+  run stamps_inflight2 200 python -u tools/stamps.py --inflight 2
+  run stamps_w16 200 python -u tools/stamps.py --waves 16
+  run stamps_w4 200 python -u tools/stamps.py --waves 4
+}
+
+# Third pass: the loader-wave split kernel -- parity, same-box A/B on configs
+# 3 and 2, its stamps timeline.
+pass_c() {
+  run t_ld 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -m gpu -k "loader_waves or config3 or config2"
+  run ab_ld_c3 300 python -u tools/ab_decode.py --workload config3 --rounds 6 --variant base: --variant ld:SPLIT_LOADERS=2
+  run ab_ld_c2 300 python -u tools/ab_decode.py --workload config2 --rounds 4 --variant base: --variant ld:SPLIT_LOADERS=2
+  run stamps_ld 200 python -u tools/stamps.py --loaders 2
+}
+"$@"

@@ -26,6 +26,8 @@ NWS = 16  # wave slots per block
 
 NAMES = {0: "start", 1: "first steps issued", 10: "loop done", 11: "waves merged",
          12: "published+drained", 14: "atomic returned", 15: "merger loads in", 13: "tile merged+stored"}
+# waves of <= 4 steps (stamps in LDS since round 6, stored at the kernel's end)
+NAMES_SHORT = {6: "step 0 computed", 7: "step 0+nbuf issued", 8: "step 1 computed", 9: "step 1+nbuf issued"}
 
 
 def main():
@@ -39,10 +41,11 @@ def main():
     ap.add_argument("--spw", type=int, default=0)
     ap.add_argument("--inflight", type=int, default=0)
     ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--loaders", type=int, default=0, help="FATTN_OPT_SPLIT_LOADERS (2: loader waves)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     for val, opt in ((args.spw, fattn.OPT_SPLIT_STEPS), (args.inflight, fattn.OPT_SPLIT_INFLIGHT),
-                     (args.waves, fattn.OPT_SPLIT_WAVES)):
+                     (args.waves, fattn.OPT_SPLIT_WAVES), (args.loaders, fattn.OPT_SPLIT_LOADERS)):
         if val:
             fattn.set_option(opt, val)
     D, H, N, NQ = 128, args.heads, args.kv_len, args.n_q
@@ -90,12 +93,16 @@ def main():
           f"stamp span {(s.max() - t0) * 0.01:.2f} us")
     pct = lambda a: " ".join(f"{np.percentile(a, p):6.2f}" for p in (0, 10, 50, 90, 100)) if len(a) else "   -"
     print("                              min    p10    p50    p90    max  (us since the first wave's start)")
+    import re
+    dsc = att.describe()
+    mc, mw = re.search(r"chunk (\d+)", dsc), re.search(r"(\d+)waves", dsc)
+    short = bool(mc and mw) and int(mc.group(1)) // (int(mw.group(1)) * 32) <= 4  # steps per wave <= 4
     for k in (0, 1) + tuple(range(2, 10)) + (10, 11, 12, 14, 15, 13):
         v = s[:, :, k]
         m = live & (v > 0)
         if not m.any():
             continue
-        name = NAMES.get(k, f"data of step {k - 2} in LDS")
+        name = NAMES.get(k) or (NAMES_SHORT.get(k) if short else None) or f"data of step {k - 2} in LDS"
         print(f"{name:28s}", pct((v[m] - t0) * 0.01))
     # per block: last wave's loop done -> phases of the block's epilogue
     last_loop = np.where(live, s[:, :, 10], 0).max(axis=1)
