@@ -57,7 +57,7 @@ harness: $(HARNESS)
 
 $(HARNESS): $(PKG)/host/kernel_test.cpp $(LIB) include/fattn.h
 	@mkdir -p $(BINDIR)
-	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Iinclude $(PKG)/host/kernel_test.cpp -L$(LIBDIR) -lfattn \
+	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Iinclude $(PKG)/host/kernel_test.cpp -L$(LIBDIR) -lfattn -lrccl -pthread \
 	    -Wl,-rpath,'$$ORIGIN/../lib' -o $@
 
 oracle:

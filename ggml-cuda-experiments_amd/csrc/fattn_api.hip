@@ -233,7 +233,7 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     // whole chunk fits the LDS (every step resident), 16-B rows, D = 64 / 128,
     // one K / V type; 4 loader waves issue it all up front
     pl.nld = 0;
-    if (g_opt_split_loaders == 2 && pl.gran == 16 && a.wave_merge == 2 && nwv == 8 && spw <= 2 &&
+    if (g_opt_split_loaders == 2 && pl.gran == 16 && a.wave_merge == 2 && nwv == 8 && spw >= 2 && spw <= 3 &&
         (pl.D == 64 || pl.D == 128) && pl.kt == pl.vt && g_opt_split_nbuf == 0 &&
         G.lds_bytes(spw, nwv) + kSplitLdFlagBytes <= kLdsPerCU) {
         pl.nld = kSplitLoaders;
@@ -584,7 +584,10 @@ int make_plan(const fattn_params* p, Plan& pl) {
         pl.cnt_bytes = pl.ml_bytes = pl.ws_bytes = 0;
         // Q8_0 / Q4_0: staged to f16 rows in the workspace, then the f16 kernel
         // (each K/V tile is otherwise dequantised once per 256-row query tile)
-        pl.pf_stage = is_quant(pl.kt) && g_opt_pf_stage != 1;
+        // (only while the f16 rows stay addressable by the kernels' 32-bit
+        // descriptors and tile offsets, N * D * 2 bytes per (kv head, seq): a
+        // longer cache keeps the in-kernel dequantisation rather than wrap)
+        pl.pf_stage = is_quant(pl.kt) && g_opt_pf_stage != 1 && (int64_t)N * D * 2 <= (int64_t)0xFFFFFFF0;
         if (pl.pf_stage) {
             pl.stage_kt = pl.kt;
             pl.kt = pl.vt = FATTN_TYPE_F16;
@@ -612,13 +615,15 @@ int make_plan(const fattn_params* p, Plan& pl) {
                  : D == 96 ? pf_lds(std::integral_constant<int, 96>())
                            : pf_lds(std::integral_constant<int, 128>());
         // f16 rows (native or staged) at D = 128: the one-wave-per-SIMD body
-        // (auto: the balanced pipelined schedule -- 0-4 % faster than the 8-wave
-        // body on f16 rows, 12-21 % on staged Q8_0 with the zero mask, and 1-3 %
-        // faster than the pipelined form 4, profiles/r05_h, r05_p; form 1 keeps
-        // the 8-wave body)
-        const int form = g_opt_pf_form == 0 ? 5 : (int)g_opt_pf_form;
+        // (auto: the lean balanced schedule, form 6 -- the balanced form 5 was
+        // 0-4 % faster than the 8-wave body on f16 rows, 12-21 % on staged Q8_0
+        // with the zero mask and 1-3 % faster than the pipelined form 4
+        // (profiles/r05_h, r05_p); the lean form's chains started from -m / c
+        // take 1.5 % (f16) to 3.6 % (Q8_0 zero mask) off it, profiles/r06_e;
+        // form 1 keeps the 8-wave body)
+        const int form = g_opt_pf_form == 0 ? 6 : (int)g_opt_pf_form;
         pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && form >= 4;
-        pl.pf4_sched = form - 2;  // 4: pipelined (SCHED 2), 5: balanced (SCHED 3)
+        pl.pf4_sched = form - 2;  // 4: pipelined (SCHED 2), 5: balanced (SCHED 3), 6: lean (SCHED 4)
         if (pl.pf4) pl.lds = Pf4Cfg<128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
@@ -737,7 +742,7 @@ int fattn_set_option(int option, int value) {
             return FATTN_OK;
         case FATTN_OPT_PF_FORM:
             // 2, 3: round 5's unpipelined one-wave-per-SIMD forms, removed (slower)
-            if (value < 0 || value > 5 || value == 2 || value == 3) return FATTN_ERR_INVALID_ARG;
+            if (value < 0 || value > 6 || value == 2 || value == 3) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_form = value;
             return FATTN_OK;
         case FATTN_OPT_PF_STAGE:
@@ -805,7 +810,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
                       pl.pf_stage ? (pl.stage_kt == FATTN_TYPE_Q8_0 ? "kv_stage_f16<q8_0> + " : "kv_stage_f16<q4_0> + ")
                                   : "",
                       pl.pf_flags ? "pf_mask_flags_kernel + " : "",
-                      pl.pf4 ? (pl.pf4_sched == 3 ? "fattn_pf4_kernel(balanced)" : "fattn_pf4_kernel(pipelined)") : "fattn_pf_kernel",
+                      pl.pf4 ? (pl.pf4_sched == 4 ? "fattn_pf4_kernel(lean)" : pl.pf4_sched == 3 ? "fattn_pf4_kernel(balanced)" : "fattn_pf4_kernel(pipelined)") : "fattn_pf_kernel",
                       tn(pl.kt), pl.D, hm);
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,

@@ -109,9 +109,11 @@ int launch_split_e(const Plan& pl, hipStream_t st, const Events& ev) {
             // as few load slots per lane as the chunk count allows (the slots
             // past it still cost issue cycles) -- unless they merge in-kernel (2)
             if (pl.a.merge_launch == 1) {
-                // one wave per packed row a tile can hold (config 4's 4-row GQA
-                // tiles: one workgroup per tile, not four)
-                const int rows = pl.a.QPT * pl.a.R < kRows ? pl.a.QPT * pl.a.R : kRows;
+                // one wave per packed row a tile can hold: R heads x the query
+                // rows it really has (config 4's 4-row GQA tiles, QPT 4 but one
+                // query row: one workgroup per tile, not four)
+                const int qrows = pl.a.QPT < pl.a.NQ ? pl.a.QPT : pl.a.NQ;
+                const int rows = qrows * pl.a.R < kRows ? qrows * pl.a.R : kRows;
                 const dim3 g((unsigned)((rows + 3) / 4), pl.grid.y, pl.grid.z);
                 const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
                 if (need <= 2) hipLaunchKernelGGL((fattn_merge_kernel<D, 2>), g, dim3(256), 0, st, pl.a);
@@ -197,8 +199,9 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     const void* main_kern = (const void*)kern;
     if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
         if (pl.pf4)
-            main_kern = pl.pf4_sched == 3 ? (const void*)fattn_pf4_kernel<D, HM, 3>
-                                          : (const void*)fattn_pf4_kernel<D, HM, 2>;
+            main_kern = pl.pf4_sched == 4   ? (const void*)fattn_pf4_kernel<D, HM, 4>
+                        : pl.pf4_sched == 3 ? (const void*)fattn_pf4_kernel<D, HM, 3>
+                                            : (const void*)fattn_pf4_kernel<D, HM, 2>;
     }
     return launch_kernel(main_kern, pl, st, ev, [&] {
         if constexpr (KT == FATTN_TYPE_F16 && D % QK == 0) {
@@ -218,7 +221,9 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
                                pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
         if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
             if (pl.pf4) {
-                if (pl.pf4_sched == 3)
+                if (pl.pf4_sched == 4)
+                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 4>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
+                else if (pl.pf4_sched == 3)
                     hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 3>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
                 else
                     hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 2>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);

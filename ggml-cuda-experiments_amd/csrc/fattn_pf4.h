@@ -177,6 +177,20 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     constexpr int NDB = D / 32;  // 32-dim blocks of O^T
     constexpr float kNegInf = -__builtin_inff();
     constexpr float kDeferLog2 = 8.0f;
+    // SCHED 4 ("lean"): each S^T chain starts from the row's -m / c (m its
+    // running max in log2 units, c = scale * log2(e)) instead of 0, so one
+    // multiply by c turns the accumulator into the exponent argument c s - m:
+    // per score an accumulator read, that multiply, one max, one exponential,
+    // one row-sum add and half a pack -- not the balanced form's separate
+    // scale fma and "x * log2(e) - m" (bodies without mask values: the zero
+    // mask, no mask; a masked body runs the balanced arithmetic -- its extra
+    // fma per score pushed the lean form into scratch); the rescale decisions
+    // move to the phase tails, where the rare
+    // branch also shifts the tile's arguments and the chains' start.  Q^T
+    // stays h(q) (src/utils.h:10): pre-scaling it by c instead (one rounding
+    // more) cost 5e-3 on large scores.  Not bit-identical to the 8-wave body
+    // (the -m / c enters the f32 chain): the oracle's 1e-3 is the bar.
+    constexpr bool LEAN = SCHED == 4;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -329,6 +343,15 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         }
     }
     f32x16 s0[2], s1[2];  // S^T of rb 0 and rb 1 (both computed in A_j), per subtile
+    f32x16 ci[2];         // (SCHED 4) each row block's S^T chain start: -m / c of the row (0 while m = -inf)
+#pragma unroll
+    for (int rb = 0; rb < 2; rb++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) ci[rb][j] = 0.0f;
+        // (held in AGPRs, where the MFMAs take it as srcC: from VGPRs hipcc
+        // copied it to AGPRs before every chain, 32 v_accvgpr_write a tile)
+        if constexpr (SCHED == 4) asm volatile("" : "+a"(ci[rb]));
+    }
 
     // mask values of row block rb for tile s (a +-0 block's slot holds the
     // zeros its empty DMA wrote)
@@ -349,7 +372,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     // subtile t is key 32t + 8(j/4) + 4h + (j%4)); row sums as scalar f32 adds
     // (the last tile's, after the loop; the loop stages the same operations
     // over its steps, e1 / e2 / e3 below)
-    auto sexp = [&](int rb, int t, const float (&us)[2][16], f16x8 (&pb)[2][2]) {
+    auto sexp = [&](int rb, int t, const float (&us)[2][16], f16x8 (&pb)[2][2], bool lean) {
         const float nm = (m_run[rb] == kNegInf) ? 0.0f : -m_run[rb];
         float la = l2[rb].x, lb = l2[rb].y;
 #pragma unroll
@@ -357,8 +380,9 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             f16x8 x;
 #pragma unroll
             for (int e = 0; e < 8; e += 2) {
-                const float pa = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e], cexp, nm));
-                const float pb2 = __builtin_amdgcn_exp2f(fmaf(us[t][8 * q + e + 1], cexp, nm));
+                const float pa = __builtin_amdgcn_exp2f(lean ? us[t][8 * q + e] : fmaf(us[t][8 * q + e], cexp, nm));
+                const float pb2 =
+                    __builtin_amdgcn_exp2f(lean ? us[t][8 * q + e + 1] : fmaf(us[t][8 * q + e + 1], cexp, nm));
                 la = add_f32(la, pa);
                 lb = add_f32(lb, pb2);
                 x[e] = (f16)pa;
@@ -392,6 +416,10 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         auto body2 = [&](auto zm_tag) {
             constexpr bool ZM = decltype(zm_tag)::value;
             constexpr bool MM = HM && !ZM;  // mask values through LDS
+            // (the lean arithmetic for the bodies without mask values -- the bench's
+            // zero-mask prefill, no mask; masked bodies keep the balanced form's:
+            // its extra fma per score pushed the masked lean body into scratch)
+            constexpr bool LN = LEAN && !MM;
             // the pipelined schedule (cdna_hip_programming.md 'Fused attention
             // prefill', 4-wave structure): per tile two phases of 32 MFMAs,
             //   A_j: S_j = K_j . Q^T for both row blocks  ||  rb 1's exponentials
@@ -563,6 +591,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 sE[pc][1] = __builtin_amdgcn_exp2f(sA[pc][1]);
                 asm volatile("" : "+v"(sE[pc][0]), "+v"(sE[pc][1]));
             };
+            auto e2u = [&](const float (&us)[2][16], int pc) {  // (SCHED 4: the argument is the score)
+                const int t = pc >> 3, k = 2 * (pc & 7);
+                sE[pc][0] = __builtin_amdgcn_exp2f(us[t][k]);
+                sE[pc][1] = __builtin_amdgcn_exp2f(us[t][k + 1]);
+                asm volatile("" : "+v"(sE[pc][0]), "+v"(sE[pc][1]));
+            };
             auto e3 = [&](f16x8 (&pb)[2][2], float& la, float& lb, int pc) {
                 const int t = pc >> 3, k = 2 * (pc & 7);
                 la = add_f32(la, sE[pc][0]);
@@ -576,6 +610,13 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 mX[pc][0] = st[t][k];
                 mX[pc][1] = st[t][k + 1];
                 asm volatile("" : "+v"(mX[pc][0]), "+v"(mX[pc][1]));
+            };
+            // (SCHED 4 without mask values: the accumulator times c IS the argument)
+            auto m1u = [&](const f32x16 (&st)[2], float (&us)[2][16], int pc) {
+                const int t = pc >> 3, k = 2 * (pc & 7);
+                us[t][k] = st[t][k] * a.scale_log2;
+                us[t][k + 1] = st[t][k + 1] * a.scale_log2;
+                asm volatile("" : "+v"(us[t][k]), "+v"(us[t][k + 1]));
             };
             auto m2 = [&](const u32x2 (&mk)[2][4], float (&us)[2][16], int pc) {
                 const int t = pc >> 3, k0 = 2 * (pc & 7);
@@ -593,6 +634,33 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     us[t][k] = x;
                 }
                 asm volatile("" : "+v"(us[t][k0]), "+v"(us[t][k0 + 1]));
+            };
+            // (SCHED 4) the rescale decision of row block rb at a phase tail: trel is
+            // the tile max relative to the chains' start -m_ref; a rare,
+            // wave-uniform branch applies a new max to the tile's arguments,
+            // l, and the next chains' start (O's factor: rescale_acc, end of B)
+            auto lean_decide = [&](int rb, float trel, float (&us)[2][16], float& alpha, bool& resc) {
+                const float mref = m_run[rb] == kNegInf ? 0.0f : m_run[rb];
+                const float tabs = trel + mref;
+                resc = __builtin_amdgcn_ballot_w64(tabs > m_run[rb] + kDeferLog2) != 0;
+                alpha = 1.0f;
+                if (__builtin_expect(resc, 0)) {
+                    asm volatile("; lean rescale" ::: "memory");
+                    const float m_new = fmaxf(m_run[rb], tabs);
+                    alpha = m_new == kNegInf ? 1.0f : __builtin_amdgcn_exp2f(m_run[rb] - m_new);
+                    const float dlt = m_new == kNegInf ? 0.0f : m_new - mref;
+#pragma unroll
+                    for (int t = 0; t < 2; t++) {
+#pragma unroll
+                        for (int k = 0; k < 16; k++) us[t][k] -= dlt;
+                    }
+                    l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
+                    m_run[rb] = m_new;
+                    const float nci = m_new == kNegInf ? 0.0f : -m_new / a.scale_log2;
+#pragma unroll
+                    for (int j = 0; j < 16; j++) ci[rb][j] = nci;
+                    asm volatile("" : "+a"(ci[rb]));
+                }
             };
             auto m3 = [&](const float (&us)[2][16], float& tmax, int pc) {
                 const int t = pc >> 3, k = 2 * (pc & 7);
@@ -854,22 +922,38 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     if constexpr (!F && !kDiagNoValu) {
                         // rb 0's exponentials of tile j-1: piece p at 2p, 2p+1, 2p+2
                         if (i >= 2 && !(i & 1)) e3(p0, la0, lb0, (i - 2) >> 1);
-                        if (i & 1) e2(i >> 1);
-                        if (!(i & 1)) e1(us0, nm0, i >> 1);
+                        if constexpr (LN) {
+                            if (i & 1) e2u(us0, i >> 1);
+                        } else {
+                            if (i & 1) e2(i >> 1);
+                            if (!(i & 1)) e1(us0, nm0, i >> 1);
+                        }
                     }
                     if constexpr (!kDiagNoValu) {
                         const int q3 = sched_inv<22, 15, 9>(i - 2), q2 = sched_inv<22, 15, 9>(i - 1),
                                   q1 = sched_inv<22, 15, 9>(i);
                         if (q3 >= 0) m3(us1, tmax1, q3);
-                        if (q2 >= 0) m2(mk1, us1, q2);
-                        if (q1 >= 0) m1(s1, q1);
+                        if constexpr (LN && !MM) {
+                            if (q1 >= 0) m1u(s1, us1, q1);
+                        } else {
+                            if (q2 >= 0) m2(mk1, us1, q2);
+                            if (q1 >= 0) m1(s1, q1);
+                        }
                     }
                     if (i < 16) {
-                        if (kk == 0) s1[t] = f32x16{};
-                        s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
+                        if constexpr (LN) {
+                            s1[t] = mfma32(kr[t][kk], qop[1][kk], kk == 0 ? ci[1] : s1[t]);
+                        } else {
+                            if (kk == 0) s1[t] = f32x16{};
+                            s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
+                        }
                     } else {
-                        if (kk == 0) s0[t] = f32x16{};
-                        s0[t] = mfma32(kr[t][kk], qop[0][kk], s0[t]);
+                        if constexpr (LN) {
+                            s0[t] = mfma32(kr[t][kk], qop[0][kk], kk == 0 ? ci[0] : s0[t]);
+                        } else {
+                            if (kk == 0) s0[t] = f32x16{};
+                            s0[t] = mfma32(kr[t][kk], qop[0][kk], s0[t]);
+                        }
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -878,9 +962,13 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     // (the stages of the last pieces past step 31)
                     const int q2 = sched_inv<22, 15, 9>(31), q3a = sched_inv<22, 15, 9>(30),
                               q3b = sched_inv<22, 15, 9>(31);
-                    if (q2 >= 0) m2(mk1, us1, q2);
+                    if (q2 >= 0 && !(LN && !MM)) m2(mk1, us1, q2);
                     if (q3a >= 0) m3(us1, tmax1, q3a);
                     if (q3b >= 0) m3(us1, tmax1, q3b);
+                }
+                if constexpr (LN) {
+                    // rb 1's decision of tile j, at A's tail (its exponentials run in B)
+                    lean_decide(1, PF4_XOR32(tmax1, true), us1, al1, rs1);
                 }
                 if constexpr (kDiagNoValu) asm volatile("" ::"v"(s1[0][0]), "v"(s1[1][0]), "v"(s0[0][0]), "v"(s0[1][0]));
                 PF4_T(1);
@@ -893,7 +981,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 PF4_T(2);
                 // ---- B_j
                 PF4_T(3);
-                float tmax0 = kNegInf, nm1 = 0.0f, la1 = 0.0f, lb1 = 0.0f;
+                float tmax0 = kNegInf, nm1 = 0.0f, la1 = LN ? l2[1].x : 0.0f, lb1 = LN ? l2[1].y : 0.0f;
                 f16x8 p1n[2][2];
                 const bool mskip = MM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
                 PF4_T(4);
@@ -902,11 +990,11 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 const uint32_t kbn = k_base(j + 1);
 #pragma unroll
                 for (int i = 0; i < 32; i++) {
-                    if (i == 0) {
+                    if (i == 0 && !LN) {
                         tred1 = PF4_XOR32(tmax1, true) * cexp;
                         asm volatile("" : "+v"(tred1));
                     }
-                    if (i == 1) {
+                    if (i == 1 && !LN) {
                         smax_decide(1, tred1, al1, rs1);
                         nm1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];
                         la1 = l2[1].x;
@@ -919,17 +1007,25 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                         const int m3p = sched_inv<26, 15, 0>(i - 2), m2p = sched_inv<26, 15, 0>(i - 1),
                                   m1p = sched_inv<26, 15, 0>(i);
                         if (e3p >= 0) e3(p1n, la1, lb1, e3p);
-                        if (e2p >= 0) e2(e2p);
-                        if (e1p >= 0) e1(us1, nm1, e1p);
+                        if constexpr (LN) {
+                            if (e2p >= 0) e2u(us1, e2p);
+                        } else {
+                            if (e2p >= 0) e2(e2p);
+                            if (e1p >= 0) e1(us1, nm1, e1p);
+                        }
                         if (m3p >= 0) m3(us0, tmax0, m3p);
-                        if (m2p >= 0) m2(mk0, us0, m2p);
-                        if (m1p >= 0) m1(s0, m1p);
+                        if constexpr (LN && !MM) {
+                            if (m1p >= 0) m1u(s0, us0, m1p);
+                        } else {
+                            if (m2p >= 0) m2(mk0, us0, m2p);
+                            if (m1p >= 0) m1(s0, m1p);
+                        }
                     }
-                    if (i == 29) {
+                    if (i == 29 && !LN) {
                         tred0 = PF4_XOR32(tmax0, true) * cexp;
                         asm volatile("" : "+v"(tred0));
                     }
-                    if (i == 30) smax_decide(0, tred0, al0, rs0);
+                    if (i == 30 && !LN) smax_decide(0, tred0, al0, rs0);
                     if constexpr (!F) {
                         if (!(i & 1) && i < 24) v_read1((i >> 1) + 4);
                         const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
@@ -944,13 +1040,20 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     // (the stages of the last pieces past step 31)
                     const int e2p = sched_inv<28, 15, 2>(31), e3a = sched_inv<28, 15, 2>(30),
                               e3b = sched_inv<28, 15, 2>(31);
-                    if (e2p >= 0) e2(e2p);
+                    if (e2p >= 0) {
+                        if constexpr (LN) e2u(us1, e2p);
+                        else e2(e2p);
+                    }
                     if (e3a >= 0) e3(p1n, la1, lb1, e3a);
                     if (e3b >= 0) e3(p1n, la1, lb1, e3b);
                 }
                 PF4_T(5);
                 l2[1] = f32x2{la1, lb1};
                 pin_p(p1n);
+                if constexpr (LN) {
+                    // rb 0's decision of tile j, at B's tail (its exponentials run in A_{j+1})
+                    lean_decide(0, PF4_XOR32(tmax0, true), us0, al0, rs0);
+                }
                 pin16(us0[0]);
                 pin16(us0[1]);
                 rescale_acc(0, rs0, al0);  // the decisions of tile j
@@ -962,14 +1065,14 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 }
                 PF4_T(6);
             };
-            if constexpr (SCHED == 3) {
+            if constexpr (SCHED >= 3) {
                 if (nt > 0) iter_bal(0, std::true_type());
                 for (int j = 1; j < nt; j++) iter_bal(j, std::false_type());
                 if (nt > 0) {
                     // ---- A_nt, B_nt: rb 0's exponentials of the last tile, its P.V
                     wait_vmcnt_c<0>();
-                    sexp(0, 0, us0, p0);
-                    sexp(0, 1, us0, p0);
+                    sexp(0, 0, us0, p0, LN);
+                    sexp(0, 1, us0, p0, LN);
                     __syncthreads();  // every wave's pieces of V nt-1 landed
                     pv2(nt - 1, p0, p1);
                 }
@@ -979,8 +1082,8 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             if (nt > 0) {
                 // ---- A_nt, B_nt: rb 1's exponentials of the last tile, its P.V
                 wait_vmcnt_c<0>();
-                sexp(1, 0, us1, p1);
-                sexp(1, 1, us1, p1);
+                sexp(1, 0, us1, p1, false);
+                sexp(1, 1, us1, p1, false);
                 __syncthreads();  // every wave's pieces of V nt-1 landed
                 pv2(nt - 1, p0, p1);  // (tile nt-1's rescale: at the end of B_{nt-1})
             }

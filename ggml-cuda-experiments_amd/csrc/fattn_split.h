@@ -1544,19 +1544,22 @@ __global__ __launch_bounds__(NWV * kWave, (KT == FATTN_TYPE_F16 || GRAN == 4 || 
 }
 
 // ---------------------------------------------------------------- loader waves
-// The split kernel with its DMA issue taken off the compute waves (one-row
-// tiles whose whole chunk fits the LDS; config 3).  In fattn_split_kernel each
-// wave issues its own steps: a wave that issues step s + 1 before computing
-// step s stalls on the CU's full memory queue before it can compute (both
-// steps in flight: 12.2 vs 11.3 us), and a wave that issues it after computing
-// step s leaves that queue idle for the whole of step s's compute (stamps,
-// round 6: step 0 lands at 3.9 us, is computed by 5.7, step 1 issued at 6.2).
-// Here NLD loader waves issue every step of the workgroup up front -- step 0
-// of every compute wave first, then step 1 -- and hand each (wave, step) over
-// by two LDS flags (K + mask landed, V landed), set behind counted vmcnt
-// waits; the NWV compute waves never issue a DMA, so step 1 streams in while
-// step 0 computes.  Same compute (split_step) and epilogue (wg_row_merge).
-// Every step of the chunk is resident: LDS = NWV x steps x stepBytes + flags.
+// The split kernel with the refill of its later steps taken off the compute
+// waves (one-row tiles whose whole chunk fits the LDS; config 3).  In
+// fattn_split_kernel each wave issues its own steps: a wave that issues step
+// s + 1 before computing step s stalls on the CU's full memory queue before it
+// can compute (both steps in flight: 12.2 vs 11.3 us), and a wave that issues
+// it after computing step s leaves that queue idle for the whole of step s's
+// compute (stamps, round 6: step 0 lands at 3.9 us, is computed by 5.7, step 1
+// issued at 6.2).  Here each compute wave issues its step 0 (as before), the
+// workgroup meets at one barrier, and NLD loader waves then issue every later
+// step of every compute wave -- into the queue behind all of step 0 -- and hand
+// each (wave, step) over by two LDS flags (K + mask landed, V landed), set
+// behind counted vmcnt waits; the compute waves never wait on an issue.  (A
+// first form whose loaders issued step 0 too took 13.5 us: the loaders could
+// flag step 0 only after issuing everything, profiles/r06_c.)  Same compute
+// (split_step) and epilogue (wg_row_merge).  Every step of the chunk is
+// resident: LDS = NWV x steps x stepBytes + flags.
 constexpr int kSplitLoaders = 4;
 constexpr int kSplitLdFlagBytes = 256;  // [8 waves][<= 2 steps][2] u32 flags, past the step buffers
 
@@ -1599,30 +1602,30 @@ __global__ __launch_bounds__((NWV + NLD) * kWave, 1) void fattn_split_ld_kernel(
     const int spw = a.nbuf;              // steps per compute wave, all resident (planner: nbuf == steps)
     const int mrow0 = qt * a.QPT;
     const int c_hi = min(a.N, (chunk + 1) * a.chunk_len);
-    uint32_t* flags = (uint32_t*)(smem + NWV * a.wave_bytes);  // [NWV][spw][2]: K + mask, V
-    if (threadIdx.x < NWV * spw * 2) flags[threadIdx.x] = 0u;
-    __syncthreads();
+    uint32_t* flags = (uint32_t*)(smem + NWV * a.wave_bytes);  // [NWV][spw][2]: K + mask, V (step 0 unused)
+    StepSrc rs;
+    rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
+    rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
+    rs.m = make_srd(a.mask, HM ? a.m_span : 0);
 
     if (wave >= NWV) {
-        // ---- loader: units u = s * NWV + w (every wave's step 0 first), dealt
-        // round-robin; U units per loader, issued back to back, then handed
-        // over oldest first (K + mask when all but the unit's V and the later
+        // ---- loader: zero the flags, meet the compute waves once they have
+        // issued their step 0, then units u = (s - 1) * NWV + w, s >= 1, dealt
+        // round-robin; U units per loader, issued back to back, handed over
+        // oldest first (K + mask when all but the unit's V and the later
         // units landed, V when all but the later units)
-        __builtin_amdgcn_s_setprio(3);
         const int L = wave - NWV;
-        const int U = spw * NWV / NLD;  // (planner: <= 4, a whole number)
-        StepSrc rs;
-        rs.k = make_srd(a.k + (int64_t)ik2 * a.k_nb2 + (int64_t)ik3 * a.k_nb3, a.k_span);
-        rs.v = make_srd(a.v + (int64_t)ik2 * a.v_nb2 + (int64_t)ik3 * a.v_nb3, a.v_span);
-        rs.m = make_srd(a.mask, HM ? a.m_span : 0);
+        if (L == 0 && lane < NWV * spw * 2) flags[lane] = 0u;
+        __syncthreads();
+        const int U = (spw - 1) * NWV / NLD;  // (planner: <= 4, a whole number)
         for (int k = 0; k < U; k++) {
-            const int u = L + NLD * k, w = u % NWV, s = u / NWV;
+            const int u = L + NLD * k, w = u % NWV, s = 1 + u / NWV;
             const int n0 = chunk * a.chunk_len + w * wl + s * kStep;
             issue_step<KT, VT, D, 16, HM>(a, rs, n0, mrow0, smem + w * a.wave_bytes + s * C::stepBytes, lane);
         }
         FATTN_SSTAMP(1);
         for (int k = 0; k < U; k++) {
-            const int u = L + NLD * k, w = u % NWV, s = u / NWV;
+            const int u = L + NLD * k, w = u % NWV, s = 1 + u / NWV;
             uint32_t* f = flags + (w * spw + s) * 2;
             wait_steps_plus<NI, P::NIV>(U - 1 - k);
             if (lane == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1634,7 +1637,7 @@ __global__ __launch_bounds__((NWV + NLD) * kWave, 1) void fattn_split_ld_kernel(
         return;
     }
 
-    // ---- compute wave: the split kernel's, minus the DMA
+    // ---- compute wave: the split kernel's, its later steps refilled by the loaders
     const int m = i16;
     const int mq = div_R(a, m);
     const int mh = hs * a.R + (m - mq * a.R);
@@ -1644,23 +1647,40 @@ __global__ __launch_bounds__((NWV + NLD) * kWave, 1) void fattn_split_ld_kernel(
     const int w_lo = chunk * a.chunk_len + wave * wl;
     const int w_hi = min(c_hi, w_lo + wl);
     const int nsteps = w_hi > w_lo ? (w_hi - w_lo + kStep - 1) / kStep : 0;
-    f16x8 qop[NB];
+    uint8_t* wbuf = smem + wave * a.wave_bytes;
+    // Q first, untracked (its wait leaves step 0's DMA in flight), then step 0
+    // (fetched whatever the wave's slice: the loaders' counts assume it)
+    u32x4 qraw[NB][2];
     {
-        const __amdgpu_buffer_rsrc_t qs = make_rsrc(a.q + (int64_t)iq3 * a.q_nb3, a.q_span);
+        const i32x4 qs = make_srd(a.q + (int64_t)iq3 * a.q_nb3, a.q_span);
         const uint32_t qoff = row_ok ? (uint32_t)iq1 * (uint32_t)a.q_nb1 + (uint32_t)iq2 * (uint32_t)a.q_nb2 + 32 * g
                                      : a.q_span;
 #pragma unroll
         for (int b = 0; b < NB; b++) {
             const uint32_t qb = (D % QK == 0 || 32 * b + 8 * g < D) ? qoff + 128 * b : a.q_span;
-            const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qb, 0, 0));
-            const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qs, qb + 16, 0, 0));
-            f16x8 h;
-            h.s0 = (f16)x0.x; h.s1 = (f16)x0.y; h.s2 = (f16)x0.z; h.s3 = (f16)x0.w;
-            h.s4 = (f16)x1.x; h.s5 = (f16)x1.y; h.s6 = (f16)x1.z; h.s7 = (f16)x1.w;
-            qop[b] = h;
+            qraw[b][0] = ld_buf_untracked<kTagQ>(qs, qb);
+            qraw[b][1] = ld_buf_untracked<kTagQ>(qs, qb + 16);
         }
     }
+    issue_step<KT, VT, D, 16, HM>(a, rs, w_lo, mrow0, wbuf, lane);
     if (a.n_chunks > 1 && lane == 0 && wave == 0) arrival_begin(a, (int64_t)iq3 * gridDim.y + y);
+    FATTN_SSTAMP(1);
+    __syncthreads();  // every compute wave's step 0 is in the queue: the loaders may issue
+    wait_steps<NI>(1);  // Q landed (step 0 may fly on)
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        reg_fence<kTagQ>(qraw[b][0]);
+        reg_fence<kTagQ>(qraw[b][1]);
+    }
+    f16x8 qop[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const f32x4 x0 = __builtin_bit_cast(f32x4, qraw[b][0]), x1 = __builtin_bit_cast(f32x4, qraw[b][1]);
+        f16x8 h;
+        h.s0 = (f16)x0.x; h.s1 = (f16)x0.y; h.s2 = (f16)x0.z; h.s3 = (f16)x0.w;
+        h.s4 = (f16)x1.x; h.s5 = (f16)x1.y; h.s6 = (f16)x1.z; h.s7 = (f16)x1.w;
+        qop[b] = h;
+    }
 
     float m_run = kNegInf;
     float l_run = 0.0f;
@@ -1670,19 +1690,22 @@ __global__ __launch_bounds__((NWV + NLD) * kWave, 1) void fattn_split_ld_kernel(
     float corr[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) corr[b] = 0.0f;
-    uint8_t* wbuf = smem + wave * a.wave_bytes;
     for (int s = 0; s < nsteps; s++) {
         const uint32_t* f = flags + (wave * spw + s) * 2;
-        wait_lds_flag(f);
+        if (s == 0) wait_steps_plus<NI, P::NIV>(0);  // own DMA: K + mask landed
+        else wait_lds_flag(f);
         if (s < 2) FATTN_SSTAMP(2 + s);
         const int n0 = w_lo + s * kStep;
         int s_opaque = s;
         asm volatile("" : "+s"(s_opaque));
         split_step<KT, VT, D, HM>(a, wbuf + s * C::stepBytes, qop, mq, g, i16, min(kStep, w_hi - n0), s_opaque == 0,
-                                  m_run, l_run, o, corr, [&] { wait_lds_flag(f + 1); });
+                                  m_run, l_run, o, corr, [&] {
+                                      if (s == 0) wait_vmcnt_c<0>();
+                                      else wait_lds_flag(f + 1);
+                                  });
         if (s < 2) FATTN_SSTAMP(6 + 2 * s);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     FATTN_SSTAMP(10);
     split_epilogue<KT, VT, D, NWV, 2>(a, o, m_run, l_run, corr, wave, lane, qt, hs, ik2, iq3, y, chunk, smem,
                                       a.wave_bytes, true, false);

@@ -6,6 +6,7 @@
 #include "../../ggml-cuda-experiments_amd/csrc/fattn_split.h"
 
 using namespace fattn;
+typedef float pf32x16 __attribute__((ext_vector_type(16)));
 
 // correct: load, wait, fence, use
 __global__ void probe_clean(const uint8_t* p, uint32_t* out, uint32_t bytes) {
@@ -54,4 +55,24 @@ __global__ void probe_trans_asm_padded(const float* x, float* out) {
     float r;
     asm volatile("s_nop 0\n\tv_add_f32_e32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(e));
     out[threadIdx.x] = r;
+}
+
+// XDL MFMA result -> asm read (the checker's third audit, round 6): a
+// 32x32x16 MFMA's accumulator read only by an asm v_accvgpr_read behind a
+// branch (fattn_pf4.h's scale_acc16 in the rescale path, without its s_nop
+// pad) -- hipcc pads its own reads, not the asm's -- and the same with the pad
+__global__ void probe_xdl_asm_read(const f16x8* a, float* out, int flag) {
+    pf32x16 acc = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[threadIdx.x], a[threadIdx.x + 64], acc, 0, 0, 0);
+    float t = 0.0f;
+    if (__builtin_amdgcn_readfirstlane(flag)) asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(t) : "a"(acc[0]));
+    out[threadIdx.x] = t;
+}
+__global__ void probe_xdl_asm_read_padded(const f16x8* a, float* out, int flag) {
+    pf32x16 acc = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[threadIdx.x], a[threadIdx.x + 64], acc, 0, 0, 0);
+    float t = 0.0f;
+    if (__builtin_amdgcn_readfirstlane(flag))
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tv_accvgpr_read_b32 %0, %1" : "=v"(t) : "a"(acc[0]));
+    out[threadIdx.x] = t;
 }

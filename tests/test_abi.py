@@ -239,20 +239,21 @@ def test_mq_min_rows_explicit_default_lifts_the_wide_gate():
 
 
 def test_pf_form_option():
-    """The prefill body over f16 rows at D = 128: the balanced pipelined
-    one-wave-per-SIMD body by default, the 8-wave body with FATTN_OPT_PF_FORM = 1,
-    the pipelined one with 4, the balanced one with 5; 2 and 3 (round 5's
+    """The prefill body over f16 rows at D = 128: the lean balanced
+    one-wave-per-SIMD body (chains started from -m / c) by default and with
+    FATTN_OPT_PF_FORM = 6, the 8-wave body with 1, the pipelined one with 4,
+    the balanced one with 5; 2 and 3 (round 5's
     unpipelined one-wave-per-SIMD forms) were removed and are rejected; other
     head dims keep the 8-wave body."""
     p = _params(NQ=4096, kt=fattn.TYPE_F16)
-    assert "fattn_pf4_kernel(balanced)<f16,D128" in fattn.describe(p)
+    assert "fattn_pf4_kernel(lean)<f16,D128" in fattn.describe(p)
     want = {1: "fattn_pf_kernel<f16,D128", 4: "fattn_pf4_kernel(pipelined)<f16,D128",
-            5: "fattn_pf4_kernel(balanced)<f16,D128"}
+            5: "fattn_pf4_kernel(balanced)<f16,D128", 6: "fattn_pf4_kernel(lean)<f16,D128"}
     for form, name in want.items():
         with fattn.options({fattn.OPT_PF_FORM: form}):
             assert name in fattn.describe(p), (form, fattn.describe(p))
     assert "fattn_pf_kernel<f16,D64" in fattn.describe(_params(NQ=4096, D=64, kt=fattn.TYPE_F16))
-    for bad in (2, 3, 6):
+    for bad in (2, 3, 7):
         with pytest.raises(Exception):
             with fattn.options({fattn.OPT_PF_FORM: bad}):
                 pass
@@ -264,7 +265,7 @@ def test_pf_stage_option_and_workspace():
     FATTN_OPT_PF_STAGE = 1; f16 caches are never staged."""
     p = _params(NQ=4096)
     d = fattn.describe(p)
-    assert d.startswith("kv_stage_f16<q8_0> + pf_mask_flags_kernel + fattn_pf4_kernel(balanced)<f16,D128"), d
+    assert d.startswith("kv_stage_f16<q8_0> + pf_mask_flags_kernel + fattn_pf4_kernel(lean)<f16,D128"), d
     ws = fattn.workspace_size(p)
     with fattn.options({fattn.OPT_PF_STAGE: 1}):
         d1 = fattn.describe(p)
@@ -395,3 +396,15 @@ def test_positional_launch_rejects_mixed_types():
         ptr, ptr, ptr, None, ptr, 0.088, D, 1, H, 1, D, N, H, 1, 1, N * 2, D * 4 * H, D * 4, D * H * 4,
         136, 136 * N, 136 * N * H, D, H, 1, 1, fattn.TYPE_Q8_0, fattn.TYPE_F16, None, 0, None)
     assert rc == -1
+
+
+def test_pf_stage_falls_back_past_32bit_f16_span():
+    """A Q8_0 cache whose staged f16 rows would pass the 32-bit descriptor span
+    (N x D x 2 > 4 GiB per kv head, here 2^24 keys at D = 128: 4 GiB of f16,
+    2.1 GiB of Q8_0) keeps the in-kernel dequantisation instead of wrapping its
+    offsets; a shorter cache is staged."""
+    big = _params(NQ=4096, H=32, Hkv=32, N=1 << 24, mask=False)
+    d = fattn.describe(big)
+    assert "kv_stage_f16" not in d and "fattn_pf_kernel<q8_0" in d, d
+    small = _params(NQ=4096, H=32, Hkv=32, N=1 << 20, mask=False)
+    assert fattn.describe(small).startswith("kv_stage_f16<q8_0>"), fattn.describe(small)

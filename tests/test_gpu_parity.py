@@ -664,8 +664,8 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture(params=[(0, 1), (1, 1), (0, 4), (0, 5)],
-                ids=["staged", "inkernel_deq", "staged_pf4p", "staged_pf4b"])
+@pytest.fixture(params=[(0, 1), (1, 1), (0, 4), (0, 5), (0, 6)],
+                ids=["staged", "inkernel_deq", "staged_pf4p", "staged_pf4b", "staged_pf4l"])
 def pf_force(request):
     """The prefill kernels on every eligible problem: Q8_0 / Q4_0 K/V staged
     to f16 first (the default) or dequantised inside the kernel
@@ -702,12 +702,13 @@ def test_pf4_bit_identical_to_pf(dev, case):
     outs = {}
     fattn.set_option(fattn.OPT_PF, 2)
     try:
-        for form in (1, 4, 5):
+        for form in (1, 4, 5, 6):
             fattn.set_option(fattn.OPT_PF_FORM, form)
             t = upload(p)
             att = fattn.Attention(*views(p, t), t["dst"], p.scale)
             assert ("fattn_pf4_kernel" in att.describe()) == (form >= 4), att.describe()
             assert ("(pipelined)" in att.describe()) == (form == 4), att.describe()
+            assert ("(lean)" in att.describe()) == (form == 6), att.describe()
             assert ("(balanced)" in att.describe()) == (form == 5), att.describe()
             att()
             outs[form] = t["dst"].cpu().numpy()
@@ -715,6 +716,12 @@ def test_pf4_bit_identical_to_pf(dev, case):
         fattn.set_option(fattn.OPT_PF, 0)
         fattn.set_option(fattn.OPT_PF_FORM, 0)
     assert np.array_equal(outs[1], outs[4], equal_nan=True)
+    # the lean form (Q^T pre-scaled, chains started from -m) is not bit-identical
+    # -- one more f16 rounding of q * scale * log2(e) -- but within the oracle's bar,
+    # with the same NaN rows
+    assert np.array_equal(np.isnan(outs[6]), np.isnan(outs[1]))
+    assert attn_rel_err(outs[6], p.oracle()) <= RTOL
+    assert attn_elem_err(outs[6], p.oracle()) <= 1.0
     assert np.array_equal(outs[1], outs[5], equal_nan=True)
     assert attn_rel_err(outs[4], p.oracle()) <= RTOL
 
@@ -962,15 +969,15 @@ def test_pf_prefill_full_zero_mask_bench_plan(dev):
     """bench.py's prefill line, pinned at its full size: n_q = N = 4096, 32
     heads, Q8_0 K/V, SURVEY §8d's zero mask, auto plan -- the rows staged to
     f16 (kv_stage_f16), the mask-flags pass (every block flagged +-0, so every
-    workgroup runs the balanced body's ZM form: no mask DMA, reads or waits)
-    and fattn_pf4_kernel(balanced).  All 32 heads x three 128-row blocks
+    workgroup runs the lean body's ZM form: no mask DMA, reads or waits)
+    and fattn_pf4_kernel(lean).  All 32 heads x three 128-row blocks
     against the oracle, and the whole output against the multi-query kernel."""
     p = make_problem(D=128, NQ=4096, H=32, N=4096, kv_type="q8_0", mask="zero", seed=31)
     assert not p.mask_bits.any() or np.all((p.mask_bits & 0x7FFF) == 0)
     t = upload(p)
     att = fattn.Attention(*views(p, t), t["dst"], p.scale)
     d = att.describe()
-    assert d.startswith("kv_stage_f16<q8_0> + pf_mask_flags_kernel + fattn_pf4_kernel(balanced)<f16,D128,mask>"), d
+    assert d.startswith("kv_stage_f16<q8_0> + pf_mask_flags_kernel + fattn_pf4_kernel(lean)<f16,D128,mask>"), d
     a = run_gpu(p)
     assert np.isfinite(a).all()
     fattn.set_option(fattn.OPT_PF, 1)

@@ -65,10 +65,16 @@ def test_audit_catches_injected_early_touch(tmp_path, capsys):
     for name, body in funcs.items():
         findings, loads, rets = ihc.check_function(name, body)
         key = next(k for k in ("probe_clean", "probe_early_store", "probe_early_copy", "probe_trans_asm_use",
-                               "probe_trans_asm_padded") if k in name)
-        by[key] = (findings, loads, rets, ihc.check_wait_states(name, body))
+                               "probe_trans_asm_padded", "probe_xdl_asm_read_padded", "probe_xdl_asm_read")
+                   if k in name)
+        by[key] = (findings, loads, rets, ihc.check_wait_states(name, body) + ihc.check_xdl_asm_reads(name, body))
     assert set(by) == {"probe_clean", "probe_early_store", "probe_early_copy", "probe_trans_asm_use",
-                       "probe_trans_asm_padded"}
+                       "probe_trans_asm_padded", "probe_xdl_asm_read", "probe_xdl_asm_read_padded"}
+    # the third audit: an asm accumulator read right behind an XDL MFMA (across
+    # the branch) is flagged; with 24 wait states of s_nop it is not
+    xw = by["probe_xdl_asm_read"][3]
+    assert xw and xw[0][0].mnem.startswith("v_mfma") and xw[0][1].mnem.startswith("v_accvgpr_read"), xw
+    assert by["probe_xdl_asm_read_padded"][3] == []
     ws = by["probe_trans_asm_use"][3]
     assert ws and ws[0][0].mnem.startswith("v_exp") and ws[0][1].mnem.startswith("v_add"), ws
     assert by["probe_trans_asm_padded"][3] == []

@@ -31,4 +31,26 @@ pass_c() {
   run ab_ld_c2 300 python -u tools/ab_decode.py --workload config2 --rounds 4 --variant base: --variant ld:SPLIT_LOADERS=2
   run stamps_ld 200 python -u tools/stamps.py --loaders 2
 }
+
+# Fourth pass: loader waves v2 (compute waves issue step 0) -- parity, A/B,
+# stamps; the lean prefill body (form 6) -- parity, A/B against the balanced
+# body (form 5) on the bench's prefill shapes.
+pass_d() {
+  run t_d 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -m gpu -k "loader_waves or pf4 or pf_sweep or pf_staged or zero_mask_bench"
+  run ab_ld2_c3 300 python -u tools/ab_decode.py --workload config3 --rounds 6 --variant base: --variant ld:SPLIT_LOADERS=2
+  run ab_ld2_c2 300 python -u tools/ab_decode.py --workload config2 --rounds 4 --variant base: --variant ld:SPLIT_LOADERS=2
+  run stamps_ld2 200 python -u tools/stamps.py --loaders 2
+  run ab_lean_q8z 400 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 3 --variant bal:PF_FORM=5 --variant lean:PF_FORM=6
+  run ab_lean_f16 300 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 3 --variant bal:PF_FORM=5 --variant lean:PF_FORM=6
+  run ab_lean_q8r 300 python -u tools/ab_prefill.py --kv q8_0 --mask random --rounds 2 --variant bal:PF_FORM=5 --variant lean:PF_FORM=6
+}
+
+# Fifth pass: the lean prefill body (exact Q, chains from -m / c; masked bodies
+# balanced) -- parity, then a longer same-box A/B against the balanced body.
+pass_e() {
+  run t_e 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -m gpu -k "pf4 or pf_sweep or pf_staged or zero_mask_bench"
+  run ab_lean2_q8z 500 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 6 --variant bal:PF_FORM=5 --variant lean:PF_FORM=6
+  run ab_lean2_f16 400 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 5 --variant bal:PF_FORM=5 --variant lean:PF_FORM=6
+  run ab_lean2_q8r 300 python -u tools/ab_prefill.py --kv q8_0 --mask random --rounds 3 --variant bal:PF_FORM=5 --variant lean:PF_FORM=6
+}
 "$@"

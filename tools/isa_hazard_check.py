@@ -33,6 +33,12 @@ asm statement is checked along straight-line code (a block and its
 fall-through), counting one wait state per instruction between and N + 1 per
 `s_nop N` (fattn_pf4.h's row sums once read a stale exponential this way).
 
+Third audit (round 6): an XDL MFMA's result read by an asm instruction (e.g.
+fattn_pf4.h's scale_acc16 `v_accvgpr_read` of O in the rare rescale branch)
+needs the MFMA's passes + 3 wait states, which only a hand-placed `s_nop` can
+give it: every path from each MFMA, across branches, is walked up to 40
+instructions for an asm read of its destination registers.
+
 `--same-as LIB.so` additionally checks that the audited ISA is the shipped
 code: every function's instruction sequence (alignment nops aside) equals the
 disassembly of the gfx950 code objects inside the library.
@@ -285,6 +291,84 @@ def required_waits(prod: Insn, cons: Insn) -> int:
     return 0
 
 
+AREG = re.compile(r"\ba\[(\d+):(\d+)\]|\ba(\d+)\b")
+
+
+def aregs(text: str) -> set[int]:
+    out = set()
+    for m in AREG.finditer(text):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def xdl_waits(mnem: str) -> int:
+    """Wait states a VALU read (v_accvgpr_read included) of an XDL MFMA's result
+    needs on gfx950: the MFMA's passes + 3 (2-pass 5, 4-pass 7, 8-pass 11,
+    16-pass 19; LLVM's GCNHazardRecognizer, the XDL-write -> VALU-read rows).
+    Passes from the shape: 32x32 16, 16x16 8, 4x4 4 -- the larger form of each
+    (conservative: 32x32x16 f16 is 8 passes on gfx950)."""
+    if "32x32" in mnem:
+        return 19
+    if "16x16" in mnem:
+        return 11
+    return 7
+
+
+def check_xdl_asm_reads(name, body, horizon=40):
+    """XDL MFMA result -> an asm instruction reading it (round-6 advisor item):
+    hipcc pads the wait states of its own VALU reads of an MFMA's result, not
+    those of an asm statement's (fattn_pf4.h's scale_acc16 reads O's AGPRs in
+    the rare rescale branch, behind a hand-placed s_nop pad).  Every path from
+    each MFMA, through branches, up to `horizon` instructions or a
+    redefinition, is walked; an asm instruction that names one of the MFMA's
+    destination registers before the wait states have passed is a finding."""
+    blocks, succ = build_blocks(body)
+    findings = []
+    for bi, (_, insns) in enumerate(blocks):
+        for a, prod in enumerate(insns):
+            if not prod.mnem.startswith("v_mfma"):
+                continue
+            first, _, _ = prod.ops.partition(",")
+            dv, da = vregs(first), aregs(first)
+            need = xdl_waits(prod.mnem)
+            # depth-first over (block, start index, waits so far, steps so far)
+            stack = [(bi, a + 1, 0, 0)]
+            seen = set()
+            while stack:
+                b, k, waits, steps = stack.pop()
+                if (b, k, waits) in seen:
+                    continue
+                seen.add((b, k, waits))
+                ins_list = blocks[b][1]
+                stopped = False
+                while k < len(ins_list):
+                    cons = ins_list[k]
+                    if waits >= need or steps >= horizon:
+                        stopped = True
+                        break
+                    if cons.in_asm and cons.mnem.startswith("v_"):
+                        if (vregs(cons.ops) & dv) or (aregs(cons.ops) & da):
+                            findings.append((prod, cons, need, waits))
+                            stopped = True
+                            break
+                    if cons.mnem == "s_nop":
+                        try:
+                            waits += int(cons.ops.split()[0], 0) + 1
+                        except ValueError:
+                            waits += 1
+                    else:
+                        waits += 1
+                    steps += 1
+                    k += 1
+                if not stopped:
+                    for nb in succ[b]:
+                        stack.append((nb, 0, waits, steps))
+    return findings
+
+
 def check_wait_states(name, body):
     """Producer/consumer pairs with an asm side that lack their wait states."""
     blocks, succ = build_blocks(body)
@@ -395,7 +479,7 @@ def main(argv=None):
                 return 2
             total_loads += loads
             total_ret += rets
-            for prod, cons, need, got in check_wait_states(name, body):
+            for prod, cons, need, got in check_wait_states(name, body) + check_xdl_asm_reads(name, body):
                 bad += 1
                 nws += 1
                 print(f"WAITSTATE {os.path.basename(path)}:{cons.line} {name}: `{cons.text}` reads the result of "
