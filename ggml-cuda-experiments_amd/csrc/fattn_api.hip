@@ -805,11 +805,11 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
     };
     char kern[160];
     const char* hm = pl.a.has_mask ? "mask" : "nomask";
-    if (pl.pf)
-        std::snprintf(kern, sizeof kern, "%s%s%s<%s,D%d,%s>",
-                      pl.pf_stage ? (pl.stage_kt == FATTN_TYPE_Q8_0 ? "kv_stage_f16<q8_0> + " : "kv_stage_f16<q4_0> + ")
-                                  : "",
-                      pl.pf_flags ? "pf_mask_flags_kernel + " : "",
+    if (pl.pf)  // (the pre-pass: one launch, pf_prepass_kernel)
+        std::snprintf(kern, sizeof kern, "%s%s%s%s%s%s<%s,D%d,%s>", (pl.pf_stage || pl.pf_flags) ? "pf_prepass[" : "",
+                      pl.pf_stage ? (pl.stage_kt == FATTN_TYPE_Q8_0 ? "kv_stage_f16<q8_0>" : "kv_stage_f16<q4_0>") : "",
+                      pl.pf_stage && pl.pf_flags ? " + " : "", pl.pf_flags ? "pf_mask_flags" : "",
+                      (pl.pf_stage || pl.pf_flags) ? "] + " : "",
                       pl.pf4 ? (pl.pf4_sched == 4 ? "fattn_pf4_kernel(lean)" : pl.pf4_sched == 3 ? "fattn_pf4_kernel(balanced)" : "fattn_pf4_kernel(pipelined)") : "fattn_pf_kernel",
                       tn(pl.kt), pl.D, hm);
     else if (pl.bd)

@@ -204,21 +204,28 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
                                             : (const void*)fattn_pf4_kernel<D, HM, 2>;
     }
     return launch_kernel(main_kern, pl, st, ev, [&] {
-        if constexpr (KT == FATTN_TYPE_F16 && D % QK == 0) {
-            if (pl.pf_stage) {  // the quantised cache's rows -> f16 rows in the workspace
-                const int64_t nblk = (int64_t)pl.a.N * D / QK;
-                const dim3 g((unsigned)((4 * nblk + 255) / 256), (unsigned)pl.stage_hkv, (unsigned)pl.stage_skv);
-                auto sk = pl.stage_kt == FATTN_TYPE_Q8_0 ? kv_stage_f16_kernel<FATTN_TYPE_Q8_0>
-                                                         : kv_stage_f16_kernel<FATTN_TYPE_Q4_0>;
-                hipLaunchKernelGGL(sk, g, dim3(256), 0, st, pl.stage_k, pl.stage_k_nb2, pl.stage_k_nb3,
-                                   (uint16_t*)pl.a.k, nblk);
-                hipLaunchKernelGGL(sk, g, dim3(256), 0, st, pl.stage_v, pl.stage_v_nb2, pl.stage_v_nb3,
-                                   (uint16_t*)pl.a.v, nblk);
-            }
+        // the pre-pass, one launch: the quantised cache's rows -> f16 rows in the
+        // workspace (K and V), and the mask's live / +-0 block flags
+        bool staged = false;
+        if constexpr (KT == FATTN_TYPE_F16 && D % QK == 0) staged = pl.pf_stage;
+        const bool flags = HM && pl.a.pf_flags;
+        if (staged || flags) {
+            PfPrepassArgs pa{};
+            pa.nblk = (int64_t)pl.a.N * D / QK;
+            pa.per_head = staged ? (int)((4 * pa.nblk + 255) / 256) : 0;
+            pa.hkv = pl.stage_hkv, pa.skv = pl.stage_skv;
+            pa.k = pl.stage_k, pa.v = pl.stage_v;
+            pa.k_nb2 = pl.stage_k_nb2, pa.k_nb3 = pl.stage_k_nb3, pa.v_nb2 = pl.stage_v_nb2, pa.v_nb3 = pl.stage_v_nb3;
+            pa.k16 = (uint16_t*)pl.a.k, pa.v16 = (uint16_t*)pl.a.v;
+            pa.mask = pl.a.mask, pa.m_nb1 = pl.a.m_nb1, pa.NQ = pl.a.NQ, pa.QPT = pl.a.QPT;
+            pa.ntiles = pl.a.N / kPfKeys, pa.flags = (uint8_t*)pl.a.pf_flags;
+            const int64_t nfl = flags ? (int64_t)pa.ntiles * pl.a.n_qt : 0;
+            const int64_t nst = staged ? 2 * (int64_t)pa.per_head * pa.hkv * pa.skv : 0;
+            const dim3 g((unsigned)(nst + nfl));
+            if (!staged) hipLaunchKernelGGL(pf_prepass_kernel<0>, g, dim3(256), 0, st, pa);
+            else if (pl.stage_kt == FATTN_TYPE_Q8_0) hipLaunchKernelGGL(pf_prepass_kernel<FATTN_TYPE_Q8_0>, g, dim3(256), 0, st, pa);
+            else hipLaunchKernelGGL(pf_prepass_kernel<FATTN_TYPE_Q4_0>, g, dim3(256), 0, st, pa);
         }
-        if (HM && pl.a.pf_flags)
-            hipLaunchKernelGGL(pf_mask_flags_kernel, dim3(pl.a.N / kPfKeys, pl.a.n_qt), dim3(256), 0, st, pl.a.mask,
-                               pl.a.m_nb1, pl.a.NQ, pl.a.QPT, pl.a.N / kPfKeys, (uint8_t*)pl.a.pf_flags);
         if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
             if (pl.pf4) {
                 if (pl.pf4_sched == 4)

@@ -39,6 +39,7 @@
 #pragma once
 
 #include "fattn_mq.h"
+#include "fattn_quant.h"
 
 namespace fattn {
 
@@ -774,9 +775,8 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
 // DMA is skipped), else 1.  One workgroup per block; every flag is written on
 // every launch, so the array needs no initialisation.  Reads the mask once
 // (f16 [NQ][N]).
-static __global__ __launch_bounds__(256) void pf_mask_flags_kernel(const uint8_t* __restrict__ mask, int64_t m_nb1, int NQ,
-                                                            int QPT, int ntiles, uint8_t* __restrict__ flags) {
-    const int s = blockIdx.x, qt = blockIdx.y;
+__device__ __forceinline__ void pf_mask_flags_block(const uint8_t* __restrict__ mask, int64_t m_nb1, int NQ, int QPT,
+                                                    int ntiles, uint8_t* __restrict__ flags, int s, int qt) {
     // thread -> (row qt*QPT + r, 16-B piece pc of the tile's 128 B): 8 pieces per row
     uint32_t open = 0, nonzero = 0;
     for (int i = threadIdx.x; i < QPT * 8; i += 256) {
@@ -791,6 +791,52 @@ static __global__ __launch_bounds__(256) void pf_mask_flags_kernel(const uint8_t
     const int any_open = __syncthreads_or(open != 0);
     const int any_nonzero = __syncthreads_or(nonzero != 0);
     if (threadIdx.x == 0) flags[(int64_t)qt * ntiles + s] = !any_open ? 0 : any_nonzero ? 1 : 2;
+}
+static __global__ __launch_bounds__(256) void pf_mask_flags_kernel(const uint8_t* __restrict__ mask, int64_t m_nb1, int NQ,
+                                                            int QPT, int ntiles, uint8_t* __restrict__ flags) {
+    pf_mask_flags_block(mask, m_nb1, NQ, QPT, ntiles, flags, blockIdx.x, blockIdx.y);
+}
+
+// The prefill's pre-pass in ONE launch (round 6): the K rows staged to f16,
+// the V rows staged, and the mask-flags blocks are independent jobs that ran
+// as three serial launches (two kernel boundaries and two ramp-down tails on
+// the plan's critical path).  Workgroups [0, nsk) stage K, [nsk, 2 nsk) stage
+// V (each the kv_stage_f16 work of one (256-thread x 8-value) slice of one
+// (kv head, seq)), the rest flag one (query tile, KV tile) block each; every
+// workgroup has one role, so the flags' workgroup reductions stay uniform.
+// STK: the cache's type, or 0 (f16 cache: flags only).
+struct PfPrepassArgs {
+    const uint8_t* k;
+    const uint8_t* v;
+    int64_t k_nb2, k_nb3, v_nb2, v_nb3;
+    uint16_t* k16;
+    uint16_t* v16;
+    int64_t nblk;      // 32-value blocks per (kv head, seq)
+    int per_head;      // staging workgroups per (kv head, seq)
+    int hkv, skv;
+    const uint8_t* mask;
+    int64_t m_nb1;
+    int NQ, QPT, ntiles, flags_on;
+    uint8_t* flags;
+};
+template <int STK>
+__global__ __launch_bounds__(256) void pf_prepass_kernel(const PfPrepassArgs p) {
+    int64_t b = blockIdx.x;
+    if constexpr (STK != 0) {
+        const int64_t nsk = (int64_t)p.per_head * p.hkv * p.skv;
+        if (b < 2 * nsk) {
+            const bool isv = b >= nsk;
+            if (isv) b -= nsk;
+            const int64_t x = b % p.per_head;
+            const int head = (int)((b / p.per_head) % p.hkv);
+            const int seq = (int)(b / ((int64_t)p.per_head * p.hkv));
+            kv_stage_f16_block<STK>(isv ? p.v : p.k, isv ? p.v_nb2 : p.k_nb2, isv ? p.v_nb3 : p.k_nb3,
+                                    isv ? p.v16 : p.k16, p.nblk, x, head, seq, p.hkv);
+            return;
+        }
+        b -= 2 * nsk;
+    }
+    pf_mask_flags_block(p.mask, p.m_nb1, p.NQ, p.QPT, p.ntiles, p.flags, (int)(b % p.ntiles), (int)(b / p.ntiles));
 }
 
 }  // namespace fattn

@@ -173,14 +173,15 @@ __global__ __launch_bounds__(256) void cpy_f32_kernel(const CpyArgs a, int64_t u
 // prefill shape) instead of 16 times in the MFMA loop.  Thread = 8 values of
 // one block (16 B of f16 written); grid (blocks * 4 / 256, Hkv, Skv).
 template <int KT>
-__global__ __launch_bounds__(256) void kv_stage_f16_kernel(const uint8_t* __restrict__ src, int64_t nb2, int64_t nb3,
-                                                           uint16_t* __restrict__ dst, int64_t nblk) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void kv_stage_f16_block(const uint8_t* __restrict__ src, int64_t nb2, int64_t nb3,
+                                                   uint16_t* __restrict__ dst, int64_t nblk, int64_t bx, int head,
+                                                   int seq, int gy) {
+    const int64_t t = bx * 256 + threadIdx.x;
     if (t >= 4 * nblk) return;
     const int64_t b = t >> 2;
     const int j = (int)(t & 3);
     constexpr int BB = KT == FATTN_TYPE_Q8_0 ? kQ8Bytes : kQ4Bytes;
-    const uint8_t* blk = src + (int64_t)blockIdx.z * nb3 + (int64_t)blockIdx.y * nb2 + b * BB;
+    const uint8_t* blk = src + (int64_t)seq * nb3 + (int64_t)head * nb2 + b * BB;
     const float d = (float)__builtin_bit_cast(f16, *(const uint16_t*)blk);  // (blocks are 2-byte aligned)
     const uint16_t* qw = (const uint16_t*)(blk + 2 + (KT == FATTN_TYPE_Q8_0 ? 8 * j : 8 * (j & 1)));
     uint32_t by[8];
@@ -198,8 +199,13 @@ __global__ __launch_bounds__(256) void kv_stage_f16_kernel(const uint8_t* __rest
         else q = (float)((int)(j < 2 ? by[e] & 0x0F : by[e] >> 4) - 8);  // elements 0-15 low nibbles, 16-31 high
         h[e] = (f16)(q * d);  // exact product (<= 19 significant bits), one rounding to f16
     }
-    uint16_t* y = dst + (((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * nblk + b) * QK + 8 * j;
+    uint16_t* y = dst + (((int64_t)seq * gy + head) * nblk + b) * QK + 8 * j;
     *(f16x8*)y = h;
+}
+template <int KT>
+__global__ __launch_bounds__(256) void kv_stage_f16_kernel(const uint8_t* __restrict__ src, int64_t nb2, int64_t nb3,
+                                                           uint16_t* __restrict__ dst, int64_t nblk) {
+    kv_stage_f16_block<KT>(src, nb2, nb3, dst, nblk, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.y);
 }
 
 }  // namespace fattn

@@ -535,25 +535,23 @@ int main(int argc, const char* argv[]) {
     }
     print_array(parallel_kv ? "Parallel KV HIP" : "No paralell KV HIP", qkv_gpu.data(), 16);
 
-    // kernel_test.h:215-234 (+ a normwise relative error per checked row and a
-    // threshold), over the checked rows
-    float max_diff = 0.0f, worst_rel = 0.0f;
+    // kernel_test.h:215-234 (+ a normwise relative error -- the max |diff| over
+    // the max |reference| -- and a threshold), over the checked rows
+    float max_diff = 0.0f, max_ref = 0.0f;
     int row_idx = 0, head_idx = 0, dim_idx = 0;
     for (int r : rows)
         for (int h = 0; h < H; h++) {
             const size_t o = ((size_t)r * H + h) * D;
-            float rmax = 0.0f, rdiff = 0.0f;
             for (int i = 0; i < D; i++) {
                 const float dd = fabsf(qkv[o + i] - qkv_gpu[o + i]);
-                rmax = std::max(rmax, fabsf(qkv[o + i]));
-                rdiff = std::isnan(dd) ? INFINITY : std::max(rdiff, dd);
+                max_ref = std::max(max_ref, fabsf(qkv[o + i]));
                 if (dd > max_diff || std::isnan(dd)) {
                     max_diff = std::isnan(dd) ? INFINITY : dd;
                     row_idx = r, head_idx = h, dim_idx = i;
                 }
             }
-            worst_rel = std::max(worst_rel, rdiff / std::max(rmax, 1e-30f));
         }
+    const float worst_rel = max_diff / std::max(max_ref, 1e-30f);
     const double bytes = (double)D * H * NQ * 4 * 2 + 2.0 * rb * N * Hkv + (has_mask ? 2.0 * N * NQ : 0.0);
     const double flops = 4.0 * N * D * H * NQ;
     printf("\ncuda time: %.4f ms  (%.1f GB/s, %.3f TFLOP/s; median of %d%s)\n", millis, bytes / millis / 1e6,

@@ -265,15 +265,15 @@ def test_pf_stage_option_and_workspace():
     FATTN_OPT_PF_STAGE = 1; f16 caches are never staged."""
     p = _params(NQ=4096)
     d = fattn.describe(p)
-    assert d.startswith("kv_stage_f16<q8_0> + pf_mask_flags_kernel + fattn_pf4_kernel(lean)<f16,D128"), d
+    assert d.startswith("pf_prepass[kv_stage_f16<q8_0> + pf_mask_flags] + fattn_pf4_kernel(lean)<f16,D128"), d
     ws = fattn.workspace_size(p)
     with fattn.options({fattn.OPT_PF_STAGE: 1}):
         d1 = fattn.describe(p)
         ws1 = fattn.workspace_size(p)
-    assert d1.startswith("pf_mask_flags_kernel + fattn_pf_kernel<q8_0,D128"), d1
+    assert d1.startswith("pf_prepass[pf_mask_flags] + fattn_pf_kernel<q8_0,D128"), d1
     assert ws == ws1 + 2 * 32 * 4096 * 128 * 2
     with fattn.options({fattn.OPT_PF_STAGE: 2}):
-        assert fattn.describe(_params(NQ=4096, kt=fattn.TYPE_Q4_0)).startswith("kv_stage_f16<q4_0>")
+        assert "kv_stage_f16<q4_0>" in fattn.describe(_params(NQ=4096, kt=fattn.TYPE_Q4_0))
         assert "kv_stage" not in fattn.describe(_params(NQ=4096, kt=fattn.TYPE_F16))
     with pytest.raises(Exception):
         fattn.set_option(fattn.OPT_PF_STAGE, 3)
@@ -407,4 +407,4 @@ def test_pf_stage_falls_back_past_32bit_f16_span():
     d = fattn.describe(big)
     assert "kv_stage_f16" not in d and "fattn_pf_kernel<q8_0" in d, d
     small = _params(NQ=4096, H=32, Hkv=32, N=1 << 20, mask=False)
-    assert fattn.describe(small).startswith("kv_stage_f16<q8_0>"), fattn.describe(small)
+    assert fattn.describe(small).startswith("pf_prepass[kv_stage_f16<q8_0>"), fattn.describe(small)

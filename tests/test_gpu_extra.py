@@ -171,7 +171,7 @@ def test_workspace_prefill_then_decode(dev):
     try:
         ap = fattn.Attention(*views(pre, tp), tp["dst"], pre.scale)
         ad = fattn.Attention(*views(dec, td), td["dst"], dec.scale)
-        assert "pf_mask_flags_kernel" in ap.describe(), ap.describe()
+        assert "pf_mask_flags" in ap.describe(), ap.describe()
         assert int(ad.describe().split("grid(")[1].split(",")[0]) > 1, ad.describe()  # several chunks
         need = max(fattn.workspace_size(ap.p), fattn.workspace_size(ad.p))
         ws = torch.zeros(need, dtype=torch.uint8, device=dev)

@@ -967,8 +967,8 @@ def test_pf_prefill_full_matches_mq(dev):
 
 def test_pf_prefill_full_zero_mask_bench_plan(dev):
     """bench.py's prefill line, pinned at its full size: n_q = N = 4096, 32
-    heads, Q8_0 K/V, SURVEY §8d's zero mask, auto plan -- the rows staged to
-    f16 (kv_stage_f16), the mask-flags pass (every block flagged +-0, so every
+    heads, Q8_0 K/V, SURVEY §8d's zero mask, auto plan -- one pre-pass launch
+    staging the rows to f16 (kv_stage_f16) and flagging the mask blocks (every block flagged +-0, so every
     workgroup runs the lean body's ZM form: no mask DMA, reads or waits)
     and fattn_pf4_kernel(lean).  All 32 heads x three 128-row blocks
     against the oracle, and the whole output against the multi-query kernel."""
@@ -977,7 +977,7 @@ def test_pf_prefill_full_zero_mask_bench_plan(dev):
     t = upload(p)
     att = fattn.Attention(*views(p, t), t["dst"], p.scale)
     d = att.describe()
-    assert d.startswith("kv_stage_f16<q8_0> + pf_mask_flags_kernel + fattn_pf4_kernel(lean)<f16,D128,mask>"), d
+    assert d.startswith("pf_prepass[kv_stage_f16<q8_0> + pf_mask_flags] + fattn_pf4_kernel(lean)<f16,D128,mask>"), d
     a = run_gpu(p)
     assert np.isfinite(a).all()
     fattn.set_option(fattn.OPT_PF, 1)

@@ -53,4 +53,20 @@ pass_e() {
   run ab_lean2_f16 400 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 5 --variant bal:PF_FORM=5 --variant lean:PF_FORM=6
   run ab_lean2_q8r 300 python -u tools/ab_prefill.py --kv q8_0 --mask random --rounds 3 --variant bal:PF_FORM=5 --variant lean:PF_FORM=6
 }
+
+# Sixth pass: the harness's new flags on the GPU, the merge-grid change's
+# parity (config 4, shards), and the default bench line with the lean prefill.
+pass_f() {
+  run t_harness 600 python -u -m pytest tests/test_harness.py -x -q --timeout 300 --timeout-method thread -m gpu
+  run t_merge 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py -x -q --timeout 300 --timeout-method thread -m gpu -k "config4 or merge or shard or workspace or config5"
+  run ab_c4 300 python -u tools/ab_decode.py --workload config4 --rounds 5 --variant base:
+  run bench 500 python -u bench.py
+}
+
+# Seventh pass: the one-launch prefill pre-pass -- prefill parity, harness,
+# the bench line.
+pass_g() {
+  run t_g 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py tests/test_harness.py -x -q --timeout 300 --timeout-method thread -m gpu -k "pf or prefill or harness or flags"
+  run bench 500 python -u bench.py
+}
 "$@"
