@@ -69,4 +69,14 @@ pass_g() {
   run t_g 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py tests/test_harness.py -x -q --timeout 300 --timeout-method thread -m gpu -k "pf or prefill or harness or flags"
   run bench 500 python -u bench.py
 }
+
+# Eighth pass: rocprofv3 kernel stats of config 4, the 8-rank config-5 shard
+# and the prefill plan (the pre-pass launch vs the body), to size the merge
+# launch and the pre-pass.
+pass_h() {
+  local Q="--no-prefill --no-scale-ref --no-cpu-baseline --no-copy-peak --steps 100 --warmup 10"
+  run kt_c4 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6h_c4 -o run -- python3 -u bench.py $Q --kv-type q4_0 --heads 32 --kv-heads 8 --kv-len 8192
+  run kt_s8 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6h_s8 -o run -- python3 -u bench.py $Q --workload config5 --heads 4 --kv-heads 4
+  run kt_pf 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6h_pf -o run -- python3 -u bench.py --prefill-only
+}
 "$@"
