@@ -61,6 +61,7 @@ std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and compute
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
+std::atomic<int> g_opt_merge_plain{0};      // second-launch merges: 0 auto (sc1 loads), 1 sc1, 2 plain loads
 std::atomic<int> g_opt_split_loaders{0};    // split kernel, one-row tiles: loader waves (FATTN_OPT_SPLIT_LOADERS): 0 auto, 1 off, 2 on
 std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto, 1 off, 2 on
 std::atomic<int> g_opt_pf_form{0};          // prefill body at D = 128 over f16 rows: 0 auto (5), 1 the 8-wave form, 4-5 one wave per SIMD (fattn_pf4.h)
@@ -397,6 +398,7 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
 int make_plan(const fattn_params* p, Plan& pl) {
     if (!p || !p->q.data || !p->k.data || !p->v.data || !p->dst) return FATTN_ERR_INVALID_ARG;
     pl.cus = device_cus();
+    pl.merge_plain = g_opt_merge_plain == 2;
     const fattn_tensor &q = p->q, &k = p->k, &v = p->v, &mk = p->mask;
     if (q.type != FATTN_TYPE_F32 || q.nb[0] != 4) return FATTN_ERR_UNSUPPORTED_TYPE;
     const int64_t D = q.ne[0];
@@ -732,6 +734,10 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_bd_xcd = value;
             return FATTN_OK;
+        case FATTN_OPT_MERGE_PLAIN:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_merge_plain = value;
+            return FATTN_OK;
         case FATTN_OPT_SPLIT_LOADERS:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_split_loaders = value;
@@ -815,7 +821,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,
                       hm, pl.a.xcd_group ? " (xcd order)" : "",
-                      pl.a.merge_launch == 1 ? " + fattn_bd_merge_kernel" : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
+                      pl.a.merge_launch == 1 ? (pl.merge_plain ? " + fattn_bd_merge_kernel(plain)" : " + fattn_bd_merge_kernel") : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     else if (pl.mq)
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,
                       pl.a.merge_launch ? " + fattn_mq_merge_kernel" : "");
@@ -823,7 +829,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
         std::snprintf(kern, sizeof kern, "%s<%s,%s,D%d,gran%d,%s,%dwaves%s>%s%s",
                       pl.nld ? "fattn_split_ld_kernel" : "fattn_split_kernel", tn(pl.kt), tn(pl.vt),
                       pl.D, pl.gran, hm, pl.nwv, pl.nld ? "+4loaders" : "", pl.a.xcd_group ? " (xcd order)" : "",
-                      pl.a.merge_launch == 1 ? " + fattn_merge_kernel" : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
+                      pl.a.merge_launch == 1 ? (pl.merge_plain ? " + fattn_merge_kernel(plain)" : " + fattn_merge_kernel") : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     const int n = std::snprintf(out, cap, "%s grid(%u,%u,%u) lds %d chunk %d steps/slots %d ws %zu", kern, pl.grid.x,
                                 pl.grid.y, pl.grid.z, pl.lds, pl.a.chunk_len, pl.a.nbuf, pl.ws_bytes);
     return n < 0 || (size_t)n >= cap ? FATTN_ERR_INVALID_ARG : FATTN_OK;

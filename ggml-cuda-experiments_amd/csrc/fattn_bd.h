@@ -662,7 +662,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
 // row) merges the row's chunk partials (merge_row_parts: the fa_reduce LSE
 // merge of src/flash_row_float.h:415-472 in fp32, fixed order) and writes the
 // normalised dst row.
-template <int D, int KIT>
+template <int D, int KIT, bool PLAIN = false>  // PLAIN: as fattn_merge_kernel
 __global__ __launch_bounds__(256) void fattn_bd_merge_kernel(const SplitArgs a) {
     const int lane = threadIdx.x & 63;
     const int p = blockIdx.x * 4 + (threadIdx.x >> 6);  // packed row of the tile
@@ -676,8 +676,8 @@ __global__ __launch_bounds__(256) void fattn_bd_merge_kernel(const SplitArgs a) 
     const int64_t slot0 = ((int64_t)iq3 * gridDim.y + y) * a.n_chunks * kBdRows + p;  // chunk 0's row
     const int rq = div_R(a, p);
     float* out = a.dst + (((int64_t)iq3 * a.NQ + qt * a.QPT + rq) * a.H + ik2 * a.rk2 + (p - rq * a.R)) * D;
-    merge_row_parts<D, KIT>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kBdRows * D,
-                            2 * kBdRows);
+    merge_row_parts<D, KIT, PLAIN ? 0 : kAuxSc1>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane,
+                                                kBdRows * D, 2 * kBdRows);
 }
 
 }  // namespace fattn

@@ -32,7 +32,8 @@ struct Plan {
     size_t ws_bytes, cnt_bytes, ml_bytes;
     int cus;  // compute units of the device the plan is for
     int nwv;  // split kernel: waves per workgroup (4, 8, 16)
-    int nld = 0;  // split kernel: loader waves beside the nwv compute waves (fattn_split_ld_kernel), 0 = none
+    int nld = 0;
+    bool merge_plain = false;  // second-launch merges (split, batched decode): plain loads (FATTN_OPT_MERGE_PLAIN)  // split kernel: loader waves beside the nwv compute waves (fattn_split_ld_kernel), 0 = none
     bool mq;  // multi-query kernel (fattn_mq.h)
     bool pf;  // prefill kernel (fattn_pf.h)
     bool bd;  // batched-decode kernel (fattn_bd.h)
@@ -116,10 +117,18 @@ int launch_split_e(const Plan& pl, hipStream_t st, const Events& ev) {
                 const int rows = qrows * pl.a.R < kRows ? qrows * pl.a.R : kRows;
                 const dim3 g((unsigned)((rows + 3) / 4), pl.grid.y, pl.grid.z);
                 const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
-                if (need <= 2) hipLaunchKernelGGL((fattn_merge_kernel<D, 2>), g, dim3(256), 0, st, pl.a);
-                else if (need <= 4) hipLaunchKernelGGL((fattn_merge_kernel<D, 4>), g, dim3(256), 0, st, pl.a);
-                else if (need <= 8) hipLaunchKernelGGL((fattn_merge_kernel<D, 8>), g, dim3(256), 0, st, pl.a);
-                else hipLaunchKernelGGL((fattn_merge_kernel<D, 16>), g, dim3(256), 0, st, pl.a);
+                auto go = [&](auto kit, auto plain) {
+                    hipLaunchKernelGGL((fattn_merge_kernel<D, decltype(kit)::value, decltype(plain)::value>), g,
+                                       dim3(256), 0, st, pl.a);
+                };
+                auto pick = [&](auto plain) {
+                    if (need <= 2) go(std::integral_constant<int, 2>(), plain);
+                    else if (need <= 4) go(std::integral_constant<int, 4>(), plain);
+                    else if (need <= 8) go(std::integral_constant<int, 8>(), plain);
+                    else go(std::integral_constant<int, 16>(), plain);
+                };
+                if (pl.merge_plain) pick(std::true_type());
+                else pick(std::false_type());
             }
         }
     });
@@ -257,10 +266,18 @@ int launch_bd_hm(const Plan& pl, hipStream_t st, const Events& ev) {
         if (pl.a.merge_launch == 1) {
             const dim3 g(kBdRows / 4, pl.grid.y, pl.grid.z);
             const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
-            if (need <= 2) hipLaunchKernelGGL((fattn_bd_merge_kernel<D, 2>), g, dim3(256), 0, st, pl.a);
-            else if (need <= 4) hipLaunchKernelGGL((fattn_bd_merge_kernel<D, 4>), g, dim3(256), 0, st, pl.a);
-            else if (need <= 8) hipLaunchKernelGGL((fattn_bd_merge_kernel<D, 8>), g, dim3(256), 0, st, pl.a);
-            else hipLaunchKernelGGL((fattn_bd_merge_kernel<D, 16>), g, dim3(256), 0, st, pl.a);
+            auto go = [&](auto kit, auto plain) {
+                hipLaunchKernelGGL((fattn_bd_merge_kernel<D, decltype(kit)::value, decltype(plain)::value>), g,
+                                   dim3(256), 0, st, pl.a);
+            };
+            auto pick = [&](auto plain) {
+                if (need <= 2) go(std::integral_constant<int, 2>(), plain);
+                else if (need <= 4) go(std::integral_constant<int, 4>(), plain);
+                else if (need <= 8) go(std::integral_constant<int, 8>(), plain);
+                else go(std::integral_constant<int, 16>(), plain);
+            };
+            if (pl.merge_plain) pick(std::true_type());
+            else pick(std::false_type());
         }
     });
 }

@@ -777,15 +777,31 @@ __global__ __launch_bounds__(kPfWaves* kWave, 1) void fattn_pf_kernel(const Spli
 // (f16 [NQ][N]).
 __device__ __forceinline__ void pf_mask_flags_block(const uint8_t* __restrict__ mask, int64_t m_nb1, int NQ, int QPT,
                                                     int ntiles, uint8_t* __restrict__ flags, int s, int qt) {
-    // thread -> (row qt*QPT + r, 16-B piece pc of the tile's 128 B): 8 pieces per row
+    // thread -> (row qt*QPT + r, 16-B piece pc of the tile's 128 B): 8 pieces
+    // per row; batches of 8 loads issued before one wait (a load per loop trip
+    // made the block 8 serial memory round trips); rows past the mask re-read
+    // its last row and count for nothing
+    constexpr int kB = 8;
     uint32_t open = 0, nonzero = 0;
-    for (int i = threadIdx.x; i < QPT * 8; i += 256) {
-        const int r = i >> 3, pc = i & 7;
-        const int q = qt * QPT + r;
-        if (q < NQ) {
-            const u32x4 w = *(const u32x4*)(mask + (int64_t)q * m_nb1 + (int64_t)s * kPfKeys * 2 + pc * 16);
-            open |= (w.x ^ 0xFC00FC00u) | (w.y ^ 0xFC00FC00u) | (w.z ^ 0xFC00FC00u) | (w.w ^ 0xFC00FC00u);
-            nonzero |= (w.x | w.y | w.z | w.w) & 0x7FFF7FFFu;
+    for (int i0 = threadIdx.x; i0 < QPT * 8; i0 += 256 * kB) {
+        u32x4 w[kB];
+        bool ok[kB];
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int i = i0 + 256 * u;
+            const int r = i >> 3, pc = i & 7;
+            const int q = qt * QPT + r;
+            ok[u] = i < QPT * 8 && q < NQ;
+            const int qc = min(q, NQ - 1);
+            w[u] = *(const u32x4*)(mask + (int64_t)qc * m_nb1 + (int64_t)s * kPfKeys * 2 + pc * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const u32x4 x = w[u];
+            const uint32_t op = (x.x ^ 0xFC00FC00u) | (x.y ^ 0xFC00FC00u) | (x.z ^ 0xFC00FC00u) | (x.w ^ 0xFC00FC00u);
+            const uint32_t nz = (x.x | x.y | x.z | x.w) & 0x7FFF7FFFu;
+            open |= ok[u] ? op : 0u;
+            nonzero |= ok[u] ? nz : 0u;
         }
     }
     const int any_open = __syncthreads_or(open != 0);

@@ -194,6 +194,13 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef FATTN_STAMPS
+    // (diagnostic build: the workgroup's timeline -- entry, loop start / end,
+    // exit in shader clocks, entry / exit in the 100-MHz real-time clock)
+    const uint64_t kt_entry = __builtin_amdgcn_s_memtime();
+    const uint64_t kr_entry = __builtin_amdgcn_s_memrealtime();
+    uint64_t kt_loop0 = 0, kt_loop1 = 0;
+#endif
     const int h = lane >> 5;    // k-group of the MFMA operands
     const int c32 = lane & 31;  // MFMA column: this lane's row within a 32-row block
 
@@ -1065,6 +1072,9 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 }
                 PF4_T(6);
             };
+#ifdef FATTN_STAMPS
+            kt_loop0 = __builtin_amdgcn_s_memtime();
+#endif
             if constexpr (SCHED >= 3) {
                 if (nt > 0) iter_bal(0, std::true_type());
                 for (int j = 1; j < nt; j++) iter_bal(j, std::false_type());
@@ -1089,6 +1099,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             }
             }
     #ifdef FATTN_STAMPS
+            kt_loop1 = __builtin_amdgcn_s_memtime();
             if (lane == 0 && g_stamps) {
                 const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
                 for (int k = 0; k < 8; k++) g_stamps[(blk * kPfWaves + wave) * 16 + k] = ph[k];
@@ -1139,6 +1150,22 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             *(f32x4*)(a.dst + (((int64_t)iq3 * a.NQ + q1) * a.H + q2) * D + 4 * c) = v;
         }
     }
+#ifdef FATTN_STAMPS
+    if (lane == 0 && g_stamps) {
+        const uint64_t kt_exit = __builtin_amdgcn_s_memtime(), kr_exit = __builtin_amdgcn_s_memrealtime();
+        const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        unsigned long long* g = g_stamps + (blk * kPfWaves + wave) * 16;
+        g[9] = kt_entry;
+        g[10] = kt_loop0;
+        g[11] = kt_loop1;
+        g[12] = kt_exit;
+        g[13] = kr_entry;
+        g[14] = kr_exit;
+        // HW_ID (CU, SIMD, shader engine) and XCC_ID
+        g[15] = (unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+    }
+#endif
 }
 
 }  // namespace fattn

@@ -786,7 +786,7 @@ __device__ __forceinline__ void wave_merge_epilogue(const SplitArgs& a, const f3
 template <int D>
 constexpr int merge_ppr() { return 64 % (D / 4) == 0 ? 64 / (D / 4) : 1; }  // parts per lane row (4, 2, 1)
 
-template <int D, int kIt = 16>  // kIt: loads per lane per round trip
+template <int D, int kIt = 16, int AUX = kAuxSc1>  // kIt: loads per lane per round trip; AUX: the loads' cache bits
 __device__ __forceinline__ void merge_row_parts(const float* parts_o, const float* parts_ml, int NP, float* out,
                                                 int lane, int ostride = D, int mstride = 2) {
     constexpr float kNegInf = -__builtin_inff();
@@ -800,11 +800,13 @@ __device__ __forceinline__ void merge_row_parts(const float* parts_o, const floa
     u32x4 v[kIt];
     auto issue = [&](int p0) {
 #pragma unroll
-        for (int i = 0; i < kIt; i++) v[i] = ld_sc1_buf(osrd, (uint32_t)(((p0 + PPR * i + h) * ostride + d4) * 4));
+        for (int i = 0; i < kIt; i++)
+            v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 osrd, (uint32_t)(((p0 + PPR * i + h) * ostride + d4) * 4), 0, AUX));
     };
     issue(0);
-    const uint32_t mlm = ld_sc1_buf_b32(msrd, (uint32_t)(lane * mstride * 4));      // lane p: m of part p
-    const uint32_t mll = ld_sc1_buf_b32(msrd, (uint32_t)(lane * mstride * 4 + 4));  //          l of part p
+    const uint32_t mlm = __builtin_amdgcn_raw_buffer_load_b32(msrd, (uint32_t)(lane * mstride * 4), 0, AUX);  // lane p: m of part p
+    const uint32_t mll = __builtin_amdgcn_raw_buffer_load_b32(msrd, (uint32_t)(lane * mstride * 4 + 4), 0, AUX);  // l of part p
     const float mp = lane < NP ? __builtin_bit_cast(float, mlm) : kNegInf;
     const float M = seg_reduce<true>(mp, 64);
     const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M);
@@ -1720,7 +1722,9 @@ __global__ __launch_bounds__((NWV + NLD) * kWave, 1) void fattn_split_ld_kernel(
 // pulls a whole tile's 16 rows x chunks into ONE workgroup (config 5 shard:
 // 128 KB, 6.4 us of a 14.7 us launch); here the same bytes spread over
 // (tiles x rows) waves, and the kernel boundary replaces drain + counter.
-template <int D, int KIT>  // KIT: loads per lane per round trip, >= the tile's chunks / merge_ppr<D>() when possible
+// PLAIN: the partials read with plain loads instead of sc1 (FATTN_OPT_MERGE_PLAIN;
+// the kernel boundary already made the split kernel's stores visible).
+template <int D, int KIT, bool PLAIN = false>  // KIT: loads per lane per round trip, >= the tile's chunks / merge_ppr<D>() when possible
 __global__ __launch_bounds__(256) void fattn_merge_kernel(const SplitArgs a) {
     const int lane = threadIdx.x & 63;
     const int tm = blockIdx.x * 4 + (threadIdx.x >> 6);  // packed row of the tile
@@ -1737,7 +1741,8 @@ __global__ __launch_bounds__(256) void fattn_merge_kernel(const SplitArgs a) {
     const int riq1 = qt * a.QPT + rq;
     const int riq2 = ik2 * a.rk2 + hs * a.R + (tm - rq * a.R);
     float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D;
-    merge_row_parts<D, KIT>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kRows * D, 2 * kRows);
+    merge_row_parts<D, KIT, PLAIN ? 0 : kAuxSc1>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kRows * D,
+                                                2 * kRows);
 }
 
 // ---------------------------------------------------------------- combine

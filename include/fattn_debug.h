@@ -94,13 +94,17 @@ enum {
                                        rows, D = 64 / 128, one K / V type): 0 = auto, 1 = off (every wave issues its
                                        own steps), 2 = 4 loader waves issue every step up front and hand each over
                                        to its compute wave by LDS flags (fattn_split_ld_kernel) */
+    FATTN_OPT_MERGE_PLAIN = 31,     /* second-launch merges of multi-row split / batched-decode plans
+                                       (fattn_merge_kernel, fattn_bd_merge_kernel): 0 = auto (sc1 loads), 1 = sc1
+                                       loads, 2 = plain loads (the kernel boundary already orders the partials) */
     FATTN_OPT_PF_FORM = 29          /* prefill body over f16 rows (native or staged) at D = 128: 0 = auto (6), 1 =
                                        the 8-wave form (fattn_pf_kernel), 4 = one wave per SIMD, pipelined (two
                                        32-MFMA phases per tile, P.V one tile behind S), 5 = pipelined and balanced
                                        (each phase carries one row block's exponentials and the other's scores /
-                                       max, interleaved over its 32 steps), 6 = the balanced form with Q^T pre-scaled
-                                       and each S^T chain started from -m (the accumulator holds the exponent
-                                       argument; not bit-identical to 1 / 4 / 5).  2, 3: round 5's unpipelined
+                                       max, interleaved over its 32 steps), 6 = "lean": the balanced form with each
+                                       S^T chain started from the row's -m / c, so the accumulator times c is the
+                                       exponent argument (bodies without mask values; not bit-identical to 1 / 4
+                                       / 5).  2, 3: round 5's unpipelined
                                        one-wave-per-SIMD forms, removed (slower), rejected */
 };
 int fattn_set_option(int option, int value);

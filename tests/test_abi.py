@@ -238,6 +238,21 @@ def test_mq_min_rows_explicit_default_lifts_the_wide_gate():
     assert fattn.describe(p).startswith("fattn_split_kernel")  # restored
 
 
+def test_merge_plain_option():
+    """FATTN_OPT_MERGE_PLAIN: 0 (auto) and 1 keep the second-launch merges'
+    sc1 loads, 2 names the plain-load kernels in the plan; out of range is
+    rejected."""
+    p = _params(NQ=1, H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0)  # config 4: 4-row tiles, second-launch merge
+    assert "fattn_merge_kernel" in fattn.describe(p) and "(plain)" not in fattn.describe(p)
+    with fattn.options({fattn.OPT_MERGE_PLAIN: 2}):
+        assert "fattn_merge_kernel(plain)" in fattn.describe(p)
+    with fattn.options({fattn.OPT_MERGE_PLAIN: 1}):
+        assert "(plain)" not in fattn.describe(p)
+    for bad in (-1, 3):
+        with pytest.raises(Exception):
+            fattn.set_option(fattn.OPT_MERGE_PLAIN, bad)
+
+
 def test_pf_form_option():
     """The prefill body over f16 rows at D = 128: the lean balanced
     one-wave-per-SIMD body (chains started from -m / c) by default and with

@@ -79,4 +79,16 @@ pass_h() {
   run kt_s8 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6h_s8 -o run -- python3 -u bench.py $Q --workload config5 --heads 4 --kv-heads 4
   run kt_pf 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6h_pf -o run -- python3 -u bench.py --prefill-only
 }
+# Ninth pass: plain-load second-launch merges (parity, same-box A/B on config
+# 4, config 5 and its 8-rank shard), the batched mask-flags loads (prefill
+# parity), the prefill workgroup timeline (stamps build).
+pass_i() {
+  run t_i 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py -x -q --timeout 300 --timeout-method thread -m gpu -k "merge_forms or pf or prefill or flags or config4 or config5"
+  run ab_plain_c4 300 python -u tools/ab_decode.py --workload config4 --rounds 6 --variant base: --variant plain:MERGE_PLAIN=2
+  run ab_plain_c5 300 python -u tools/ab_decode.py --workload config5 --rounds 6 --variant base: --variant plain:MERGE_PLAIN=2
+  run ab_plain_s8 300 python -u tools/ab_decode.py --workload config5_s8 --rounds 6 --variant base: --variant plain:MERGE_PLAIN=2
+  run st_pf_zm 200 python -u tools/pf_stamps.py --kv-type q8_0 --mask-zero
+  run st_pf_f16 200 python -u tools/pf_stamps.py --kv-type f16 --no-mask
+  run ab_pf_q8z 300 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 5 --variant base:
+}
 "$@"
