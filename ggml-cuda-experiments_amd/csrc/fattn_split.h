@@ -245,49 +245,41 @@ __device__ __forceinline__ u32x4 ld_buf_untracked(const i32x4& srd, uint32_t off
 // builtin, hipcc treats the LDS base as a per-lane value, and around an
 // exec-masked (partial) instruction it built per-lane phis of (LDS base,
 // offset) pairs whose readfirstlane'd M0 no longer matched the inactive
-// lanes' offsets.  Here M0 comes from an SGPR operand in the same statement
-// (saved and restored: M0 is compiler-reserved; s_nop 0 = M0 -> LDS-DMA
-// hazard).  Not tracked by the compiler's s_waitcnt bookkeeping: every
-// consumer waits with an explicit vmcnt.
+// lanes' offsets -- and it tracks the DMA in its s_waitcnt bookkeeping, so
+// the first LDS read after it would wait for every DMA in flight.  Here the
+// LDS address is an M0 operand ("{m0}": hipcc writes M0 itself, straight
+// from the address arithmetic -- one s_add per DMA where the asm's own
+// save / set / restore of the reserved M0 cost three s_mov; the prefill
+// body issues 8 DMAs a tile with one wave per SIMD, where every scalar
+// instruction takes an issue slot); s_nop 0 = the M0 -> LDS-DMA hazard.  Not
+// tracked by the compiler's s_waitcnt bookkeeping: every consumer waits with
+// an explicit vmcnt.  (-DFATTN_DMA_M0_SAVE: the round-5 save / restore form,
+// for A/B builds.)
 // NT: non-temporal policy for bytes one CU reads once (the decode KV stream,
 // MI355X_MICROARCH.md 'nt-weights'); never for tiles other workgroups re-read.
 template <int BYTES, bool NT = false>
 __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds_any, uint32_t off) {
+    static_assert(BYTES == 16 || BYTES == 4, "");
     // wave-uniform by construction; readfirstlane keeps it an SGPR operand even
     // where divergent code around the call hides that from the compiler
     const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_any);
+#ifdef FATTN_DMA_M0_SAVE
     uint32_t keep;
-    if constexpr (BYTES == 16 && NT) {
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(off), "s"(srd), "s"(lds)
-            : "memory");
-    } else if constexpr (BYTES == 16) {
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(off), "s"(srd), "s"(lds)
-            : "memory");
-    } else if constexpr (NT) {
-        static_assert(BYTES == 4, "");
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen nt lds\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(off), "s"(srd), "s"(lds)
-            : "memory");
-    } else {
-        static_assert(BYTES == 4, "");
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(off), "s"(srd), "s"(lds)
-            : "memory");
-    }
+#define FATTN_DMA_ASM(INSN, MOD)                                                                         \
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" INSN " %1, %2, 0 offen" MOD \
+                 "\n\ts_mov_b32 m0, %0"                                                                \
+                 : "=&s"(keep)                                                                           \
+                 : "v"(off), "s"(srd), "s"(lds)                                                          \
+                 : "memory")
+#else
+#define FATTN_DMA_ASM(INSN, MOD) \
+    asm volatile("s_nop 0\n\t" INSN " %0, %1, 0 offen" MOD : : "v"(off), "s"(srd), "{m0}"(lds) : "memory")
+#endif
+    if constexpr (BYTES == 16 && NT) FATTN_DMA_ASM("buffer_load_dwordx4", " nt lds");
+    else if constexpr (BYTES == 16) FATTN_DMA_ASM("buffer_load_dwordx4", " lds");
+    else if constexpr (NT) FATTN_DMA_ASM("buffer_load_dword", " nt lds");
+    else FATTN_DMA_ASM("buffer_load_dword", " lds");
+#undef FATTN_DMA_ASM
 }
 
 struct StepSrc {

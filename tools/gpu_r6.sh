@@ -91,4 +91,18 @@ pass_i() {
   run st_pf_f16 200 python -u tools/pf_stamps.py --kv-type f16 --no-mask
   run ab_pf_q8z 300 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 5 --variant base:
 }
+# Tenth pass: the DMA helper's M0 operand (every kernel's LDS-DMA issue: 2
+# scalar instructions fewer per DMA) -- the whole GPU suite, then same-box A/B
+# against the round-5 save / restore form (lib/libfattn_m0save.so), processes
+# alternating.
+pass_j() {
+  run t_j 1000 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu
+  for r in 1 2 3; do
+    for L in libfattn.so libfattn_m0save.so; do
+      FATTN_LIB=$L run ab_m0_pf_${L%.so}_$r 200 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 2 --variant $L:
+      FATTN_LIB=$L run ab_m0_c3_${L%.so}_$r 200 python -u tools/ab_decode.py --workload config3 --rounds 2 --variant $L:
+      FATTN_LIB=$L run ab_m0_c5_${L%.so}_$r 200 python -u tools/ab_decode.py --workload config5 --rounds 2 --variant $L:
+    done
+  done
+}
 "$@"
