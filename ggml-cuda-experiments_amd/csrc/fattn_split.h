@@ -234,7 +234,7 @@ enum : int { kTagQ = 1, kTagMaskWords = 2 };  // bit masks
 template <int TAG>
 __device__ __forceinline__ u32x4 ld_buf_untracked(const i32x4& srd, uint32_t off) {
     u32x4 v;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen ; UNTRACKED(%3)"
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen ; UNTRACKED(%3)"
                  : "=v"(v)
                  : "v"(off), "s"(srd), "i"(TAG)
                  : "memory");
@@ -251,10 +251,16 @@ __device__ __forceinline__ u32x4 ld_buf_untracked(const i32x4& srd, uint32_t off
 // from the address arithmetic -- one s_add per DMA where the asm's own
 // save / set / restore of the reserved M0 cost three s_mov; the prefill
 // body issues 8 DMAs a tile with one wave per SIMD, where every scalar
-// instruction takes an issue slot); s_nop 0 = the M0 -> LDS-DMA hazard.  Not
-// tracked by the compiler's s_waitcnt bookkeeping: every consumer waits with
-// an explicit vmcnt.  (-DFATTN_DMA_M0_SAVE: the round-5 save / restore form,
-// for A/B builds.)
+// instruction takes an issue slot).  s_nop 4 opens the string: hipcc pads
+// its own VMEM instructions but not an asm one, and it re-materialises the
+// descriptor's words with v_readfirstlane right before the statement -- a
+// VALU SGPR write needs 5 wait states before a VMEM instruction reads it
+// (cdna_hip_programming.md 'Insert its wait states'; with s_nop 0 multi-chunk
+// decodes read through a stale descriptor word; tools/isa_hazard_check.py
+// audits every asm VMEM instruction for it).  It also covers M0 -> LDS-DMA
+// (1 state).  Not tracked by the compiler's s_waitcnt bookkeeping: every
+// consumer waits with an explicit vmcnt.  (-DFATTN_DMA_M0_SAVE: the round-5
+// save / restore form, padded the same way, for A/B builds.)
 // NT: non-temporal policy for bytes one CU reads once (the decode KV stream,
 // MI355X_MICROARCH.md 'nt-weights'); never for tiles other workgroups re-read.
 template <int BYTES, bool NT = false>
@@ -266,14 +272,14 @@ __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds_any, uint32_t
 #ifdef FATTN_DMA_M0_SAVE
     uint32_t keep;
 #define FATTN_DMA_ASM(INSN, MOD)                                                                         \
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" INSN " %1, %2, 0 offen" MOD \
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 2\n\t" INSN " %1, %2, 0 offen" MOD \
                  "\n\ts_mov_b32 m0, %0"                                                                \
                  : "=&s"(keep)                                                                           \
                  : "v"(off), "s"(srd), "s"(lds)                                                          \
                  : "memory")
 #else
 #define FATTN_DMA_ASM(INSN, MOD) \
-    asm volatile("s_nop 0\n\t" INSN " %0, %1, 0 offen" MOD : : "v"(off), "s"(srd), "{m0}"(lds) : "memory")
+    asm volatile("s_nop 4\n\t" INSN " %0, %1, 0 offen" MOD : : "v"(off), "s"(srd), "{m0}"(lds) : "memory")
 #endif
     if constexpr (BYTES == 16 && NT) FATTN_DMA_ASM("buffer_load_dwordx4", " nt lds");
     else if constexpr (BYTES == 16) FATTN_DMA_ASM("buffer_load_dwordx4", " lds");

@@ -76,3 +76,26 @@ __global__ void probe_xdl_asm_read_padded(const f16x8* a, float* out, int flag) 
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tv_accvgpr_read_b32 %0, %1" : "=v"(t) : "a"(acc[0]));
     out[threadIdx.x] = t;
 }
+
+// VALU SGPR write -> asm VMEM read of it (the checker's fourth audit, round
+// 6): a descriptor word fresh from v_readfirstlane read by an asm LDS-DMA
+// opened with s_nop 0 only (the LDS-DMA helper's first "{m0}" form), and the
+// same with the helper's s_nop 4
+__device__ __forceinline__ i32x4 probe_srd(const uint8_t* p, const uint32_t* w) {
+    i32x4 r;
+    r.x = (int)(uint32_t)(uint64_t)p;
+    r.y = (int)(uint32_t)((uint64_t)p >> 32);
+    r.z = (int)__builtin_amdgcn_readfirstlane(w[threadIdx.x]);  // a loaded VGPR -> SGPR: a VALU write
+    r.w = 0x00020000;
+    return r;
+}
+__global__ void probe_sgpr_vmem(const uint8_t* p, const uint32_t* w, uint32_t lds) {
+    const i32x4 srd = probe_srd(p, w);
+    asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" : : "v"(threadIdx.x * 4), "s"(srd), "{m0}"(lds)
+                 : "memory");
+}
+__global__ void probe_sgpr_vmem_padded(const uint8_t* p, const uint32_t* w, uint32_t lds) {
+    const i32x4 srd = probe_srd(p, w);
+    asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, 0 offen lds" : : "v"(threadIdx.x * 4), "s"(srd), "{m0}"(lds)
+                 : "memory");
+}

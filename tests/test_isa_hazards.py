@@ -12,7 +12,9 @@ translation unit of libfattn.so (`make isa`, the library's own flags).
   correct form of the same kernel is not.
 * Its second audit (asm wait states): an asm v_add_f32 that reads a v_exp_f32
   result hipcc placed right before it is flagged; with the pad inside the asm
-  it is not.  The shipped ISA has none.
+  it is not.  The shipped ISA has none.  Likewise the third (an XDL result read
+  by asm) and the fourth (a v_readfirstlane'd descriptor word read by an asm
+  VMEM instruction within 5 wait states).
 """
 import os
 import subprocess
@@ -65,11 +67,19 @@ def test_audit_catches_injected_early_touch(tmp_path, capsys):
     for name, body in funcs.items():
         findings, loads, rets = ihc.check_function(name, body)
         key = next(k for k in ("probe_clean", "probe_early_store", "probe_early_copy", "probe_trans_asm_use",
-                               "probe_trans_asm_padded", "probe_xdl_asm_read_padded", "probe_xdl_asm_read")
+                               "probe_trans_asm_padded", "probe_xdl_asm_read_padded", "probe_xdl_asm_read",
+                               "probe_sgpr_vmem_padded", "probe_sgpr_vmem")
                    if k in name)
-        by[key] = (findings, loads, rets, ihc.check_wait_states(name, body) + ihc.check_xdl_asm_reads(name, body))
+        by[key] = (findings, loads, rets, ihc.check_wait_states(name, body) + ihc.check_xdl_asm_reads(name, body) +
+                   ihc.check_sgpr_vmem(name, body))
     assert set(by) == {"probe_clean", "probe_early_store", "probe_early_copy", "probe_trans_asm_use",
-                       "probe_trans_asm_padded", "probe_xdl_asm_read", "probe_xdl_asm_read_padded"}
+                       "probe_trans_asm_padded", "probe_xdl_asm_read", "probe_xdl_asm_read_padded",
+                       "probe_sgpr_vmem", "probe_sgpr_vmem_padded"}
+    # the fourth audit: a descriptor word fresh from v_readfirstlane read by an
+    # asm LDS-DMA after s_nop 0 is flagged; behind the helper's s_nop 4 it is not
+    sw = by["probe_sgpr_vmem"][3]
+    assert sw and sw[0][0].mnem.startswith("v_readfirstlane") and sw[0][1].mnem.startswith("buffer_load"), sw
+    assert by["probe_sgpr_vmem_padded"][3] == []
     # the third audit: an asm accumulator read right behind an XDL MFMA (across
     # the branch) is flagged; with 24 wait states of s_nop it is not
     xw = by["probe_xdl_asm_read"][3]

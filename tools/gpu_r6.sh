@@ -96,8 +96,8 @@ pass_i() {
 # against the round-5 save / restore form (lib/libfattn_m0save.so), processes
 # alternating.
 pass_j() {
-  run t_j 1000 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu
-  for r in 1 2 3; do
+  run t_j 900 python -u -m pytest tests -q --timeout 300 --timeout-method thread -m gpu
+  for r in 1 2; do
     for L in libfattn.so libfattn_m0save.so; do
       FATTN_LIB=$L run ab_m0_pf_${L%.so}_$r 200 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 2 --variant $L:
       FATTN_LIB=$L run ab_m0_c3_${L%.so}_$r 200 python -u tools/ab_decode.py --workload config3 --rounds 2 --variant $L:

@@ -43,6 +43,16 @@ instructions for an asm read of its destination registers.
 code: every function's instruction sequence (alignment nops aside) equals the
 disassembly of the gfx950 code objects inside the library.
 
+Fourth audit (round 6): a VALU instruction that writes an SGPR (v_readfirstlane,
+v_readlane, a VOP3 carry-out or compare mask) followed by a VMEM instruction
+that reads that SGPR (descriptor, soffset, base) needs 5 wait states; hipcc
+pads its own VMEM instructions, not an asm one, so every asm VMEM
+instruction's SGPR operands are checked against the VALU writes before it
+(its block and the straight-line block falling into it).  (The LDS-DMA
+helper's "{m0}" form once opened with s_nop 0 only: a readfirstlane'd
+descriptor word two instructions ahead made multi-chunk decodes read
+garbage.)
+
 Usage: isa_hazard_check.py [--same-as lib.so] file.s [file.s ...]
 Exit 0 = clean; 1 = hazards (listed); 2 = usage / parse problem.
 """
@@ -399,6 +409,75 @@ def check_wait_states(name, body):
     return findings
 
 
+SREG = re.compile(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b")
+SDST2 = ("v_add_co_", "v_sub_co_", "v_subrev_co_", "v_addc_co_", "v_subb_co_", "v_subbrev_co_", "v_mad_u64_u32",
+         "v_mad_i64_i32", "v_div_scale")
+
+
+def sregs(text: str) -> set[int]:
+    out = set()
+    for m in SREG.finditer(text):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def valu_sgpr_dest(ins: Insn) -> set[int]:
+    """SGPRs a VALU instruction writes (readfirstlane / readlane / compares' first operand, carry-outs' second)."""
+    mn = ins.mnem
+    if not mn.startswith("v_") or mn.startswith("v_mfma"):
+        return set()
+    ops = [o.strip() for o in ins.ops.split(",")]
+    if not ops:
+        return set()
+    if mn.startswith(("v_readfirstlane", "v_readlane")) or (mn.startswith("v_cmp") and mn.endswith("_e64")):
+        return sregs(ops[0])
+    if mn.startswith(SDST2) and len(ops) > 1:
+        return sregs(ops[1])
+    return set()
+
+
+def check_sgpr_vmem(name, body, need=5):
+    """(producer, consumer, need, got) for asm VMEM instructions reading a fresh VALU-written SGPR."""
+    blocks, _ = build_blocks(body)
+    findings = []
+    for i, (_, insns) in enumerate(blocks):
+        prev = []
+        if i > 0:
+            pb = blocks[i - 1][1]
+            if pb and not (pb[-1].mnem.startswith("s_branch") or pb[-1].mnem == "s_endpgm"):
+                prev = pb[-8:]
+        seq = prev + list(insns)
+        for c in range(len(prev), len(seq)):
+            cons = seq[c]
+            if not (cons.in_asm and is_vmem(cons.mnem)):
+                continue
+            reads = sregs(cons.ops)
+            if not reads:
+                continue
+            waits = 0
+            for prod in reversed(seq[max(0, c - 8):c]):
+                if valu_sgpr_dest(prod) & reads and waits < need:
+                    findings.append((prod, cons, need, waits))
+                    break
+                if prod.mnem.startswith("s_") and not prod.mnem.startswith(("s_nop", "s_waitcnt", "s_cmp")):
+                    reads = reads - sregs(prod.ops.split(",")[0])  # a later scalar write supersedes
+                    if not reads:
+                        break
+                if prod.mnem == "s_nop":
+                    try:
+                        waits += int(prod.ops.split()[0], 0) + 1
+                    except ValueError:
+                        waits += 1
+                else:
+                    waits += 1
+                if waits >= need:
+                    break
+    return findings
+
+
 # ------------------------------------------------------------------ shipped-library comparison
 
 def code_objects(lib_path):
@@ -479,7 +558,8 @@ def main(argv=None):
                 return 2
             total_loads += loads
             total_ret += rets
-            for prod, cons, need, got in check_wait_states(name, body) + check_xdl_asm_reads(name, body):
+            for prod, cons, need, got in (check_wait_states(name, body) + check_xdl_asm_reads(name, body) +
+                                          check_sgpr_vmem(name, body)):
                 bad += 1
                 nws += 1
                 print(f"WAITSTATE {os.path.basename(path)}:{cons.line} {name}: `{cons.text}` reads the result of "
