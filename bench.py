@@ -236,15 +236,16 @@ def cpu_baseline_prefill(rows=256):
             "extrapolation": f"linear: x {NQ // rows} rows x {H} heads (not measured)"}
 
 
-def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5, D=128, H=32):
+def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5, D=128, H=32, reps=3):
     """The MFMA-bound prefill shape of SURVEY.md §8d (n_q = N = 4096, 32 heads,
     head_dim 128, Q8_0 K/V, non-causal, an f16 mask of zeros -- "zero mask":
     every key visible; "random": U[-1,1) like kernel_test.h:48; "causal": 0 on
     and below the diagonal, -inf above): `steps` launches captured in one HIP
-    graph, HIP events around the replay on the launch stream.  Two rotated KV
-    caches (compute-bound: the cache state barely matters).  The mask pre-pass
-    (pf_mask_flags_kernel: live / all-zero block flags) is inside the timed
-    region.  (D / H: other head dims for tools/ab_prefill.py; the bench line
+    graph, HIP events around each of `reps` replays on the launch stream, the
+    median replay reported (all of them in kernel_ms_reps).  Two rotated KV
+    caches (compute-bound: the cache state barely matters).  The pre-pass
+    (pf_prepass_kernel: K / V staged to f16, live / all-zero mask block flags)
+    is inside the timed region.  (D / H: other head dims for tools/ab_prefill.py; the bench line
     is D = 128, H = 32.)"""
     import torch
     import fattn
@@ -289,14 +290,19 @@ def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5, D=128,
     with torch.cuda.stream(gs):
         graph.replay()
     torch.cuda.synchronize()
+    # `reps` timed replays, the median reported (one replay of 5 launches moved
+    # by +-5 % from replay to replay on one box: DVFS)
     f = C.c_float()
-    hip.hipEventRecord(evs[0], gs.cuda_stream)
-    with torch.cuda.stream(gs):
-        graph.replay()
-    hip.hipEventRecord(evs[1], gs.cuda_stream)
-    torch.cuda.synchronize()
-    hip.hipEventElapsedTime(C.byref(f), evs[0], evs[1])
-    ms = f.value / steps
+    reps_ms = []
+    for _ in range(reps):
+        hip.hipEventRecord(evs[0], gs.cuda_stream)
+        with torch.cuda.stream(gs):
+            graph.replay()
+        hip.hipEventRecord(evs[1], gs.cuda_stream)
+        torch.cuda.synchronize()
+        hip.hipEventElapsedTime(C.byref(f), evs[0], evs[1])
+        reps_ms.append(f.value / steps)
+    ms = sorted(reps_ms)[len(reps_ms) // 2]
     # algorithmic flops: the unmasked (query, key) pairs (all of them without causality)
     pairs = NQ * (NQ + 1) // 2 if causal else NQ * N
     flops = 4 * pairs * D * H
@@ -308,7 +314,8 @@ def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5, D=128,
     # HBM bytes per launch from the committed FETCH_SIZE / WRITE_SIZE passes of
     # this exact plan and source (tools/pmc_summary.py --traffic), else None
     traffic = committed_traffic(workload, kname)
-    return {"workload": workload, "kernel": kname, "kernel_ms_avg": round(ms, 5), "flops_per_step": flops,
+    return {"workload": workload, "kernel": kname, "kernel_ms_avg": round(ms, 5),
+            "kernel_ms_reps": [round(x, 5) for x in reps_ms], "flops_per_step": flops,
             "bytes_per_step": alg_bytes,
             "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic,
