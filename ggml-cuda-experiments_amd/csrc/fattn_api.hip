@@ -61,6 +61,7 @@ std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and compute
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
+std::atomic<int> g_opt_part_f16{0};         // second-launch merges' partials: 0 auto (f16 where supported), 1 f32, 2 f16
 std::atomic<int> g_opt_merge_plain{0};      // second-launch merges: 0 auto (sc1 loads), 1 sc1, 2 plain loads
 std::atomic<int> g_opt_split_loaders{0};    // split kernel, one-row tiles: loader waves (FATTN_OPT_SPLIT_LOADERS): 0 auto, 1 off, 2 on
 std::atomic<int> g_opt_split_xcd{0};        // split kernel, XCD-grouped workgroup order: 0 auto, 1 off, 2 on
@@ -134,6 +135,11 @@ bool combine_ok(int64_t nch, int rv, int D) {
 // 15.2 us, 2-rank shard 19.6 vs 19.9; profiles/r05_l).  The grid is sized so that
 // all (Y x S x chunks) workgroups are co-resident, limited by LDS (steps in
 // flight) and registers.
+// f16 chunk partials (SplitArgs::part_f16) for the second-launch merges of the
+// split kernel's multi-row tiles and the batched-decode kernels: not at D = 64
+// (merge_row_parts_h), not with the in-kernel merges
+bool part_f16_ok(int merge_launch, int D) { return merge_launch == 1 && D != 64 && g_opt_part_f16 != 1; }
+
 int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t NQ) {
     SplitArgs& a = pl.a;
     const Geom G = geom(pl.kt, pl.vt, pl.D);
@@ -246,6 +252,7 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     const bool resident = (int64_t)a.n_chunks * Y * S <= (int64_t)pl.cus * wgs_cu;
     a.merge_launch = (a.n_chunks >= 4 && a.wave_merge == 0 && !g_opt_split_fused_merge)
                          ? ((resident && g_opt_merge_in_kernel) ? 2 : 1) : 0;
+    a.part_f16 = part_f16_ok(a.merge_launch, pl.D) ? 1 : 0;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     // XCD-grouped order (tile_coords): a tile's chunk workgroups on one XCD.
     // Default for the one-row tiles that merge in-kernel (wg_row_merge):
@@ -382,6 +389,7 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     // co-resident -- one workgroup per CU by LDS) or in a second launch
     const bool resident = nch * Y * S <= (int64_t)pl.cus * per_cu;
     a.merge_launch = nch == 1 ? 0 : (resident && g_opt_merge_in_kernel) ? 2 : 1;
+    a.part_f16 = part_f16_ok(a.merge_launch, pl.D) ? 1 : 0;
     if (nch > 1) {
         // [arrival words, in-kernel merge only][(m, l) pairs][O partials]: [S][Y][chunks][64 rows]
         const size_t slots = (size_t)S * Y * nch * kBdRows;
@@ -734,6 +742,10 @@ int fattn_set_option(int option, int value) {
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_bd_xcd = value;
             return FATTN_OK;
+        case FATTN_OPT_PART_F16:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_part_f16 = value;
+            return FATTN_OK;
         case FATTN_OPT_MERGE_PLAIN:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_merge_plain = value;
@@ -821,7 +833,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,
                       hm, pl.a.xcd_group ? " (xcd order)" : "",
-                      pl.a.merge_launch == 1 ? (pl.merge_plain ? " + fattn_bd_merge_kernel(plain)" : " + fattn_bd_merge_kernel") : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
+                      pl.a.merge_launch == 1 ? (pl.a.part_f16 ? " + fattn_bd_merge_kernel(f16 partials)" : pl.merge_plain ? " + fattn_bd_merge_kernel(plain)" : " + fattn_bd_merge_kernel") : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     else if (pl.mq)
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,
                       pl.a.merge_launch ? " + fattn_mq_merge_kernel" : "");
@@ -829,7 +841,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
         std::snprintf(kern, sizeof kern, "%s<%s,%s,D%d,gran%d,%s,%dwaves%s>%s%s",
                       pl.nld ? "fattn_split_ld_kernel" : "fattn_split_kernel", tn(pl.kt), tn(pl.vt),
                       pl.D, pl.gran, hm, pl.nwv, pl.nld ? "+4loaders" : "", pl.a.xcd_group ? " (xcd order)" : "",
-                      pl.a.merge_launch == 1 ? (pl.merge_plain ? " + fattn_merge_kernel(plain)" : " + fattn_merge_kernel") : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
+                      pl.a.merge_launch == 1 ? (pl.a.part_f16 ? " + fattn_merge_kernel(f16 partials)" : pl.merge_plain ? " + fattn_merge_kernel(plain)" : " + fattn_merge_kernel") : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     const int n = std::snprintf(out, cap, "%s grid(%u,%u,%u) lds %d chunk %d steps/slots %d ws %zu", kern, pl.grid.x,
                                 pl.grid.y, pl.grid.z, pl.lds, pl.a.chunk_len, pl.a.nbuf, pl.ws_bytes);
     return n < 0 || (size_t)n >= cap ? FATTN_ERR_INVALID_ARG : FATTN_OK;

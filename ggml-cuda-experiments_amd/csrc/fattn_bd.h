@@ -344,9 +344,13 @@ __device__ __forceinline__ void bd_finish(const SplitArgs& a, uint8_t* smem, con
     // fattn_bd_merge_kernel, [tile][chunk][64 rows][D] and [..][64 rows][2] (the
     // kernel boundary orders these stores before the merge's loads)
     const int64_t slot = (((int64_t)iq3 * gridDim.y + y) * a.n_chunks + chunk) * kBdRows + pr;
-    float* po = a.ws_o + slot * D + c0;
+    if (a.part_f16) {  // (SplitArgs::part_f16: O / l in f16)
+        store_part_f16<kDpt>((uint16_t*)a.ws_o + slot * D + c0, acc, L);
+    } else {
+        float* po = a.ws_o + slot * D + c0;
 #pragma unroll
-    for (int e = 0; e < kDpt; e += 4) *(f32x4*)(po + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
+        for (int e = 0; e < kDpt; e += 4) *(f32x4*)(po + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
+    }
     if (c0 == 0) *(f32x2*)(a.ws_ml + 2 * slot) = f32x2{M, L};
 #ifdef FATTN_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -662,7 +666,7 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bd_kernel(const Spli
 // row) merges the row's chunk partials (merge_row_parts: the fa_reduce LSE
 // merge of src/flash_row_float.h:415-472 in fp32, fixed order) and writes the
 // normalised dst row.
-template <int D, int KIT, bool PLAIN = false>  // PLAIN: as fattn_merge_kernel
+template <int D, int KIT, bool PLAIN = false, bool F16 = false>  // PLAIN, F16: as fattn_merge_kernel
 __global__ __launch_bounds__(256) void fattn_bd_merge_kernel(const SplitArgs a) {
     const int lane = threadIdx.x & 63;
     const int p = blockIdx.x * 4 + (threadIdx.x >> 6);  // packed row of the tile
@@ -676,8 +680,13 @@ __global__ __launch_bounds__(256) void fattn_bd_merge_kernel(const SplitArgs a) 
     const int64_t slot0 = ((int64_t)iq3 * gridDim.y + y) * a.n_chunks * kBdRows + p;  // chunk 0's row
     const int rq = div_R(a, p);
     float* out = a.dst + (((int64_t)iq3 * a.NQ + qt * a.QPT + rq) * a.H + ik2 * a.rk2 + (p - rq * a.R)) * D;
-    merge_row_parts<D, KIT, PLAIN ? 0 : kAuxSc1>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane,
-                                                kBdRows * D, 2 * kBdRows);
+    if constexpr (F16) {
+        merge_row_parts_h<D, KIT>((const uint16_t*)a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane,
+                                  kBdRows * D, 2 * kBdRows);
+    } else {
+        merge_row_parts<D, KIT, PLAIN ? 0 : kAuxSc1>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane,
+                                                    kBdRows * D, 2 * kBdRows);
+    }
 }
 
 }  // namespace fattn

@@ -117,18 +117,24 @@ int launch_split_e(const Plan& pl, hipStream_t st, const Events& ev) {
                 const int rows = qrows * pl.a.R < kRows ? qrows * pl.a.R : kRows;
                 const dim3 g((unsigned)((rows + 3) / 4), pl.grid.y, pl.grid.z);
                 const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
-                auto go = [&](auto kit, auto plain) {
-                    hipLaunchKernelGGL((fattn_merge_kernel<D, decltype(kit)::value, decltype(plain)::value>), g,
-                                       dim3(256), 0, st, pl.a);
+                auto go = [&](auto kit, auto plain, auto f16) {
+                    hipLaunchKernelGGL((fattn_merge_kernel<D, decltype(kit)::value, decltype(plain)::value, decltype(f16)::value>),
+                                       g, dim3(256), 0, st, pl.a);
                 };
-                auto pick = [&](auto plain) {
-                    if (need <= 2) go(std::integral_constant<int, 2>(), plain);
-                    else if (need <= 4) go(std::integral_constant<int, 4>(), plain);
-                    else if (need <= 8) go(std::integral_constant<int, 8>(), plain);
-                    else go(std::integral_constant<int, 16>(), plain);
+                auto pick = [&](int nd, auto plain, auto f16) {
+                    if (nd <= 2) go(std::integral_constant<int, 2>(), plain, f16);
+                    else if (nd <= 4) go(std::integral_constant<int, 4>(), plain, f16);
+                    else if (nd <= 8) go(std::integral_constant<int, 8>(), plain, f16);
+                    else go(std::integral_constant<int, 16>(), plain, f16);
                 };
-                if (pl.merge_plain) pick(std::true_type());
-                else pick(std::false_type());
+                if constexpr (D != 64) {
+                    if (pl.a.part_f16) {  // (f16 partials: 16-B loads of 8 dims, merge_ppr_h parts per lane row)
+                        pick((pl.a.n_chunks + merge_ppr_h<D>() - 1) / merge_ppr_h<D>(), std::false_type(), std::true_type());
+                        return;
+                    }
+                }
+                if (pl.merge_plain) pick(need, std::true_type(), std::false_type());
+                else pick(need, std::false_type(), std::false_type());
             }
         }
     });
@@ -266,18 +272,24 @@ int launch_bd_hm(const Plan& pl, hipStream_t st, const Events& ev) {
         if (pl.a.merge_launch == 1) {
             const dim3 g(kBdRows / 4, pl.grid.y, pl.grid.z);
             const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
-            auto go = [&](auto kit, auto plain) {
-                hipLaunchKernelGGL((fattn_bd_merge_kernel<D, decltype(kit)::value, decltype(plain)::value>), g,
-                                   dim3(256), 0, st, pl.a);
+            auto go = [&](auto kit, auto plain, auto f16) {
+                hipLaunchKernelGGL((fattn_bd_merge_kernel<D, decltype(kit)::value, decltype(plain)::value, decltype(f16)::value>),
+                                   g, dim3(256), 0, st, pl.a);
             };
-            auto pick = [&](auto plain) {
-                if (need <= 2) go(std::integral_constant<int, 2>(), plain);
-                else if (need <= 4) go(std::integral_constant<int, 4>(), plain);
-                else if (need <= 8) go(std::integral_constant<int, 8>(), plain);
-                else go(std::integral_constant<int, 16>(), plain);
+            auto pick = [&](int nd, auto plain, auto f16) {
+                if (nd <= 2) go(std::integral_constant<int, 2>(), plain, f16);
+                else if (nd <= 4) go(std::integral_constant<int, 4>(), plain, f16);
+                else if (nd <= 8) go(std::integral_constant<int, 8>(), plain, f16);
+                else go(std::integral_constant<int, 16>(), plain, f16);
             };
-            if (pl.merge_plain) pick(std::true_type());
-            else pick(std::false_type());
+            if constexpr (D != 64) {
+                if (pl.a.part_f16) {  // (f16 partials: 16-B loads of 8 dims, merge_ppr_h parts per lane row)
+                    pick((pl.a.n_chunks + merge_ppr_h<D>() - 1) / merge_ppr_h<D>(), std::false_type(), std::true_type());
+                    return;
+                }
+            }
+            if (pl.merge_plain) pick(need, std::true_type(), std::false_type());
+            else pick(need, std::false_type(), std::false_type());
         }
     });
 }

@@ -94,6 +94,8 @@ struct SplitArgs {
                         // fattn_bd_merge_kernel), 2 = inside the launch (tile_arrive_wait: grid co-resident)
     int step_skip;      // split kernel: 1 = skip steps whose mask is all -inf for the tile (FATTN_OPT_SPLIT_SKIP)
     int xcd_group;      // workgroups in XCD-grouped order (tile_coords; grid size % 8 == 0): batched decode, split kernel
+    int part_f16;       // merge_launch 1: each chunk partial stored as O / l in f16 beside its (m, l) in f32
+                        // (half the partial bytes; store_part_f16, merge_row_parts_h)
 };
 
 // XOR mask of the 16-B chunk swizzle of an LDS row of `cpr` chunks: the largest
@@ -841,6 +843,96 @@ __device__ __forceinline__ void merge_row_parts(const float* parts_o, const floa
     *(f32x4*)(out + d4) = acc * inv;
 }
 
+// f16 chunk partials (SplitArgs::part_f16, second-launch merges): the
+// partial's EPT dims of O / l rounded to f16 -- bounded by max |v|, where the
+// unnormalised O is not -- (a fully masked chunk, l = 0, stores zeros: its
+// merge weight is 0); the (m, l) pair stays f32.  Plain stores: the kernel
+// boundary orders them before the merge launch's loads.
+template <int EPT>
+__device__ __forceinline__ void store_part_f16(uint16_t* dst, const float (&acc)[EPT], float L) {
+    static_assert(EPT % 4 == 0, "");
+    const float inv = L > 0.0f ? 1.0f / L : 0.0f;
+    uint32_t w[EPT / 2];
+#pragma unroll
+    for (int e = 0; e < EPT; e += 2) {
+        const f16x2 hp = {(_Float16)(acc[e] * inv), (_Float16)(acc[e + 1] * inv)};
+        w[e / 2] = __builtin_bit_cast(uint32_t, hp);
+    }
+    // (16-B stores when EPT is a multiple of 8 -- dst is then 16-B aligned --,
+    // else 8-B ones: the batched-decode epilogue's 12 dims at D = 96)
+    if constexpr (EPT % 8 == 0) {
+#pragma unroll
+        for (int e = 0; e < EPT / 2; e += 4) *(u32x4*)(dst + 2 * e) = u32x4{w[e], w[e + 1], w[e + 2], w[e + 3]};
+    } else {
+#pragma unroll
+        for (int e = 0; e < EPT / 2; e += 2) *(u32x2*)(dst + 2 * e) = u32x2{w[e], w[e + 1]};
+    }
+}
+
+// The merge of NP f16 partials of one row (merge_row_parts' fa_reduce LSE
+// merge, src/flash_row_float.h:415-472, in fp32, fixed order): lane (h, dl) =
+// (lane / (D/8), lane % (D/8)) loads 16 B = 8 dims of every part p = h (mod
+// 64 / (D/8)); part p weighs w_p l_p, w_p = 2^(m_p - M), and the row is
+// sum_p w_p l_p O~_p / sum_p w_p l_p.  Plain loads (a second launch).  D = 80,
+// 96, 128, 256 (D = 64 keeps f32 partials: 8 parts per lane row would need a
+// third lane-swap level).
+template <int D>
+constexpr int merge_ppr_h() { return 64 % (D / 8) == 0 ? 64 / (D / 8) : 1; }  // (4, 2, 1)
+template <int D, int kIt>
+__device__ __forceinline__ void merge_row_parts_h(const uint16_t* parts_o, const float* parts_ml, int NP, float* out,
+                                                  int lane, int ostride, int mstride) {
+    constexpr float kNegInf = -__builtin_inff();
+    constexpr int LPP = D / 8;
+    constexpr int PPR = merge_ppr_h<D>();
+    static_assert(PPR == 1 || PPR == 2 || PPR == 4, "");
+    const int h = lane / LPP, d8 = 8 * (lane % LPP);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the count)
+    const __amdgpu_buffer_rsrc_t osrd = make_rsrc(parts_o, (uint32_t)(NP * ostride * 2));
+    const __amdgpu_buffer_rsrc_t msrd = make_rsrc(parts_ml, (uint32_t)(NP * mstride * 4));
+    u32x4 v[kIt];
+    auto issue = [&](int p0) {
+#pragma unroll
+        for (int i = 0; i < kIt; i++)
+            v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 osrd, (uint32_t)(((p0 + PPR * i + h) * ostride + d8) * 2), 0, 0));
+    };
+    issue(0);
+    const uint32_t mlm = __builtin_amdgcn_raw_buffer_load_b32(msrd, (uint32_t)(lane * mstride * 4), 0, 0);
+    const uint32_t mll = __builtin_amdgcn_raw_buffer_load_b32(msrd, (uint32_t)(lane * mstride * 4 + 4), 0, 0);
+    const float mp = lane < NP ? __builtin_bit_cast(float, mlm) : kNegInf;
+    const float M = seg_reduce<true>(mp, 64);
+    const float w = (mp == kNegInf) ? 0.0f : __builtin_amdgcn_exp2f(mp - M) * __builtin_bit_cast(float, mll);
+    const float L = seg_reduce<false>(lane < NP ? w : 0.0f, 64);
+    const int wi = __builtin_bit_cast(int, w);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) acc[e] = 0.0f;
+    for (int p0 = 0; p0 < NP; p0 += kIt * PPR) {  // wave-uniform
+        if (p0 > 0) issue(p0);
+#pragma unroll
+        for (int i = 0; i < kIt; i++) {
+            float wp = 0.0f;
+#pragma unroll
+            for (int j = 0; j < PPR; j++) {
+                const float wj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(wi, (p0 + PPR * i + j) & 63));
+                wp = (h == j) ? wj : wp;
+            }
+            const f16x8 x = __builtin_bit_cast(f16x8, v[i]);
+#pragma unroll
+            for (int e = 0; e < 8; e++) acc[e] += wp * (float)x[e];
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        if constexpr (PPR == 4) acc[e] = xor16_pair(acc[e], false);
+        if constexpr (PPR >= 2) acc[e] = xor32_pair(acc[e], false);
+    }
+    if (h) return;
+    const float inv = L == 0.0f ? __builtin_nanf("") : 1.0f / L;  // L == 0 (row fully masked) -> NaN like the reference
+    *(f32x4*)(out + d8) = f32x4{acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv};
+    *(f32x4*)(out + d8 + 4) = f32x4{acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv};
+}
+
 // One-row tiles, NW waves per workgroup: every wave writes its row-0 state
 // (O, m, l) into its own LDS region (its steps have all landed), one barrier,
 // then wave 0 merges the NW states (lane (h, dl): states p = h mod PPR, dims
@@ -1091,6 +1183,16 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, f32x4 (&o)[D 
     // last adder reads the others' partials with sc1 loads -- all of them in
     // one round trip -- while its own stays in LDS.
     const int64_t tile = (int64_t)iq3 * gridDim.y + y;
+    if (a.merge_launch == 1 && a.part_f16) {
+        if constexpr (EPT % 4 == 0) {
+            if (tm < rv) {
+                const int64_t slot = (tile * a.n_chunks + chunk) * kRows + tm;
+                if (dok) store_part_f16<EPT>((uint16_t*)a.ws_o + slot * D + d0, acc, L);
+                if (tj == 0) *(f32x2*)(a.ws_ml + 2 * slot) = f32x2{M, L};
+            }
+        }
+        return;
+    }
     if (tm < rv) {
         const int64_t slot = (tile * a.n_chunks + chunk) * kRows + tm;
         auto bits = [](float x) { return __builtin_bit_cast(uint32_t, x); };
@@ -1721,8 +1823,9 @@ __global__ __launch_bounds__((NWV + NLD) * kWave, 1) void fattn_split_ld_kernel(
 // 128 KB, 6.4 us of a 14.7 us launch); here the same bytes spread over
 // (tiles x rows) waves, and the kernel boundary replaces drain + counter.
 // PLAIN: the partials read with plain loads instead of sc1 (FATTN_OPT_MERGE_PLAIN;
-// the kernel boundary already made the split kernel's stores visible).
-template <int D, int KIT, bool PLAIN = false>  // KIT: loads per lane per round trip, >= the tile's chunks / merge_ppr<D>() when possible
+// the kernel boundary already made the split kernel's stores visible).  F16:
+// the f16 partials of SplitArgs::part_f16 (merge_row_parts_h, plain loads).
+template <int D, int KIT, bool PLAIN = false, bool F16 = false>  // KIT: loads per lane per round trip, >= the tile's chunks / merge_ppr<D>() when possible
 __global__ __launch_bounds__(256) void fattn_merge_kernel(const SplitArgs a) {
     const int lane = threadIdx.x & 63;
     const int tm = blockIdx.x * 4 + (threadIdx.x >> 6);  // packed row of the tile
@@ -1739,8 +1842,13 @@ __global__ __launch_bounds__(256) void fattn_merge_kernel(const SplitArgs a) {
     const int riq1 = qt * a.QPT + rq;
     const int riq2 = ik2 * a.rk2 + hs * a.R + (tm - rq * a.R);
     float* out = a.dst + (((int64_t)iq3 * a.NQ + riq1) * a.H + riq2) * D;
-    merge_row_parts<D, KIT, PLAIN ? 0 : kAuxSc1>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kRows * D,
-                                                2 * kRows);
+    if constexpr (F16) {
+        merge_row_parts_h<D, KIT>((const uint16_t*)a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane,
+                                  kRows * D, 2 * kRows);
+    } else {
+        merge_row_parts<D, KIT, PLAIN ? 0 : kAuxSc1>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane,
+                                                    kRows * D, 2 * kRows);
+    }
 }
 
 // ---------------------------------------------------------------- combine

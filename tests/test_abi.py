@@ -239,18 +239,37 @@ def test_mq_min_rows_explicit_default_lifts_the_wide_gate():
 
 
 def test_merge_plain_option():
-    """FATTN_OPT_MERGE_PLAIN: 0 (auto) and 1 keep the second-launch merges'
-    sc1 loads, 2 names the plain-load kernels in the plan; out of range is
-    rejected."""
+    """FATTN_OPT_MERGE_PLAIN (f32 partials, FATTN_OPT_PART_F16 = 1): 0 (auto)
+    and 1 keep the second-launch merges' sc1 loads, 2 names the plain-load
+    kernels in the plan; out of range is rejected."""
     p = _params(NQ=1, H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0)  # config 4: 4-row tiles, second-launch merge
-    assert "fattn_merge_kernel" in fattn.describe(p) and "(plain)" not in fattn.describe(p)
-    with fattn.options({fattn.OPT_MERGE_PLAIN: 2}):
-        assert "fattn_merge_kernel(plain)" in fattn.describe(p)
-    with fattn.options({fattn.OPT_MERGE_PLAIN: 1}):
-        assert "(plain)" not in fattn.describe(p)
+    with fattn.options({fattn.OPT_PART_F16: 1}):
+        assert "fattn_merge_kernel" in fattn.describe(p) and "(plain)" not in fattn.describe(p)
+        with fattn.options({fattn.OPT_MERGE_PLAIN: 2}):
+            assert "fattn_merge_kernel(plain)" in fattn.describe(p)
+        with fattn.options({fattn.OPT_MERGE_PLAIN: 1}):
+            assert "(plain)" not in fattn.describe(p)
     for bad in (-1, 3):
         with pytest.raises(Exception):
             fattn.set_option(fattn.OPT_MERGE_PLAIN, bad)
+
+
+def test_part_f16_option():
+    """FATTN_OPT_PART_F16: the second-launch merges take f16 partials by
+    default (split kernel's multi-row tiles, batched decode) except at D = 64
+    and with the in-kernel merge; 1 keeps f32; out of range is rejected."""
+    c4 = _params(NQ=1, H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0)
+    c5 = _params(NQ=64, H=32, Hkv=32, N=4096, kt=fattn.TYPE_Q8_0)
+    for p, kern in ((c4, "fattn_merge_kernel(f16 partials)"), (c5, "fattn_bd_merge_kernel(f16 partials)")):
+        assert kern in fattn.describe(p), fattn.describe(p)
+        with fattn.options({fattn.OPT_PART_F16: 1}):
+            assert "f16 partials" not in fattn.describe(p)
+        with fattn.options({fattn.OPT_PART_F16: 2}):
+            assert kern in fattn.describe(p)
+    assert "f16 partials" not in fattn.describe(_params(D=64, NQ=1, H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0))
+    for bad in (-1, 3):
+        with pytest.raises(Exception):
+            fattn.set_option(fattn.OPT_PART_F16, bad)
 
 
 def test_pf_form_option():

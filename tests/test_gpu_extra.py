@@ -507,7 +507,8 @@ def test_row_merge_graph_replays_new_inputs(dev, xcd):
     assert ("(xcd order)" in desc) == (xcd == 0), desc
 
 
-@pytest.mark.parametrize("in_kernel", [1, 0, 2], ids=["in_kernel", "second_launch", "second_launch_plain"])
+@pytest.mark.parametrize("in_kernel", [1, 0, 2, 3], ids=["in_kernel", "second_launch", "second_launch_plain",
+                                                       "second_launch_f32"])
 @pytest.mark.parametrize("case", [
     dict(D=128, NQ=64, H=32, N=4096, kv_type="q8_0"),                 # config 5 (8 chunks per kv head)
     dict(D=128, NQ=64, H=16, N=4096, kv_type="q8_0"),                 # its 2-rank shard
@@ -519,14 +520,16 @@ def test_bd_chunk_merge_forms(dev, in_kernel, case):
     the second launch (default) or inside the launch (FATTN_OPT_MERGE_IN_KERNEL:
     every workgroup co-resident, each waits for the tile's count, then merges
     its share of the rows); both against the oracle, forced chunk counts
-    included; in_kernel 2: the second launch with plain loads
-    (FATTN_OPT_MERGE_PLAIN)."""
+    included.  The second launch reads f16 partials by default (0); 2: f32
+    partials with plain loads (FATTN_OPT_MERGE_PLAIN), 3: f32 partials with
+    sc1 loads (FATTN_OPT_PART_F16 = 1)."""
     import torch
     p = make_problem(seed=90 + case["H"], **case)
     ref = p.oracle()
     t = upload(p, dev)
     fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 1 if in_kernel == 1 else 0)
     fattn.set_option(fattn.OPT_MERGE_PLAIN, 2 if in_kernel == 2 else 0)
+    fattn.set_option(fattn.OPT_PART_F16, 1 if in_kernel >= 2 else 0)
     try:
         for chunk in (0, 1024):
             att = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=chunk)
@@ -537,6 +540,7 @@ def test_bd_chunk_merge_forms(dev, in_kernel, case):
             resident = g[0] * g[1] * g[2] <= cus  # one batched-decode workgroup per CU
             assert ("in-kernel" in desc) == (in_kernel == 1 and resident), desc
             assert ("merge_kernel(plain)" in desc) == (in_kernel == 2 and "merge_kernel" in desc), desc
+            assert ("merge_kernel(f16 partials)" in desc) == (in_kernel == 0 and "merge_kernel" in desc), desc
             t["dst"].fill_(float("nan"))
             att()
             torch.cuda.synchronize()
@@ -544,6 +548,7 @@ def test_bd_chunk_merge_forms(dev, in_kernel, case):
     finally:
         fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 0)
         fattn.set_option(fattn.OPT_MERGE_PLAIN, 0)
+        fattn.set_option(fattn.OPT_PART_F16, 0)
 
 
 def test_bd_in_kernel_merge_graph_replays_new_inputs(dev):
@@ -559,7 +564,8 @@ def test_bd_in_kernel_merge_graph_replays_new_inputs(dev):
     assert "in-kernel" in desc, desc
 
 
-@pytest.mark.parametrize("in_kernel", [1, 0, 2], ids=["in_kernel", "second_launch", "second_launch_plain"])
+@pytest.mark.parametrize("in_kernel", [1, 0, 2, 3], ids=["in_kernel", "second_launch", "second_launch_plain",
+                                                       "second_launch_f32"])
 @pytest.mark.parametrize("case", [
     dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0"),           # config 4
     dict(D=128, NQ=64, H=4, N=4096, kv_type="q8_0"),                  # config 5, 8-rank shard
@@ -571,20 +577,23 @@ def test_bd_in_kernel_merge_graph_replays_new_inputs(dev):
 def test_split_multirow_merge_forms(dev, in_kernel, case):
     """Multi-row split tiles over 4+ KV chunks: the partials merge one wave per
     (tile, row), inside the launch (the tile's workgroups wait for each other)
-    or in the second launch (in_kernel 2: with plain loads,
-    FATTN_OPT_MERGE_PLAIN); all against the oracle at several head dims."""
+    or in the second launch (f16 partials by default except at D = 64; 2:
+    f32 partials with plain loads, FATTN_OPT_MERGE_PLAIN; 3: f32 partials,
+    FATTN_OPT_PART_F16 = 1); all against the oracle at several head dims."""
     import torch
     p = make_problem(seed=70 + case["D"], **case)
     ref = p.oracle()
     t = upload(p, dev)
     fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 1 if in_kernel == 1 else 0)
     fattn.set_option(fattn.OPT_MERGE_PLAIN, 2 if in_kernel == 2 else 0)
+    fattn.set_option(fattn.OPT_PART_F16, 1 if in_kernel >= 2 else 0)
     fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
     try:
         for chunk in (0, 256):
             att = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=chunk)
             desc = att.describe()
             assert ("merge_kernel(plain)" in desc) == (in_kernel == 2 and "merge_kernel" in desc), desc
+            assert ("f16 partials" in desc) == (in_kernel == 0 and "merge_kernel" in desc and case["D"] != 64), desc
             t["dst"].fill_(float("nan"))
             att()
             torch.cuda.synchronize()
@@ -592,6 +601,7 @@ def test_split_multirow_merge_forms(dev, in_kernel, case):
     finally:
         fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 0)
         fattn.set_option(fattn.OPT_MERGE_PLAIN, 0)
+        fattn.set_option(fattn.OPT_PART_F16, 0)
         fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
 
 

@@ -716,8 +716,8 @@ def test_pf4_bit_identical_to_pf(dev, case):
         fattn.set_option(fattn.OPT_PF, 0)
         fattn.set_option(fattn.OPT_PF_FORM, 0)
     assert np.array_equal(outs[1], outs[4], equal_nan=True)
-    # the lean form (Q^T pre-scaled, chains started from -m) is not bit-identical
-    # -- one more f16 rounding of q * scale * log2(e) -- but within the oracle's bar,
+    # the lean form (S^T chains started from -m / c) is not bit-identical -- the
+    # -m / c enters the f32 accumulation -- but within the oracle's bar,
     # with the same NaN rows
     assert np.array_equal(np.isnan(outs[6]), np.isnan(outs[1]))
     assert attn_rel_err(outs[6], p.oracle()) <= RTOL

@@ -105,4 +105,15 @@ pass_j() {
     done
   done
 }
+# Eleventh pass: f16 chunk partials for the second-launch merges -- the merge
+# and batched-decode tests, then same-box A/B against f32 partials on config
+# 4, config 5 and its 8- / 4-rank shards; the prefill line's new median.
+pass_k() {
+  run t_k 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "merge or bd or config4 or config5 or shard or multirow or workspace or masked or nan"
+  run ab_p16_c5 300 python -u tools/ab_decode.py --workload config5 --rounds 6 --variant f16: --variant f32:PART_F16=1
+  run ab_p16_s8 300 python -u tools/ab_decode.py --workload config5_s8 --rounds 6 --variant f16: --variant f32:PART_F16=1
+  run ab_p16_s4 300 python -u tools/ab_decode.py --workload config5_s4 --rounds 6 --variant f16: --variant f32:PART_F16=1
+  run ab_p16_c4 300 python -u tools/ab_decode.py --workload config4 --rounds 6 --variant f16: --variant f32:PART_F16=1
+  run ab_p16_s2 300 python -u tools/ab_decode.py --workload config5_s2 --rounds 4 --variant f16: --variant f32:PART_F16=1
+}
 "$@"
