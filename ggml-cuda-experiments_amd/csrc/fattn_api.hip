@@ -252,7 +252,10 @@ int size_split(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N, int64_t 
     const bool resident = (int64_t)a.n_chunks * Y * S <= (int64_t)pl.cus * wgs_cu;
     a.merge_launch = (a.n_chunks >= 4 && a.wave_merge == 0 && !g_opt_split_fused_merge)
                          ? ((resident && g_opt_merge_in_kernel) ? 2 : 1) : 0;
-    a.part_f16 = part_f16_ok(a.merge_launch, pl.D) ? 1 : 0;
+    // (auto: f16 partials for tiles of 8+ rows -- the 8-rank config-5 shard
+    // 11.67 -> 11.50 us; config 4's 4-row tiles were 10.09 -> 10.33 us, so
+    // they keep f32; profiles/r06_f)
+    a.part_f16 = part_f16_ok(a.merge_launch, pl.D) && (g_opt_part_f16 == 2 || rv_max >= 8) ? 1 : 0;
     pl.grid = dim3(a.n_chunks, (unsigned)Y, (unsigned)S);
     // XCD-grouped order (tile_coords): a tile's chunk workgroups on one XCD.
     // Default for the one-row tiles that merge in-kernel (wg_row_merge):
@@ -389,6 +392,8 @@ int size_bd(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     // co-resident -- one workgroup per CU by LDS) or in a second launch
     const bool resident = nch * Y * S <= (int64_t)pl.cus * per_cu;
     a.merge_launch = nch == 1 ? 0 : (resident && g_opt_merge_in_kernel) ? 2 : 1;
+    // (f16 partials: config 5 22.81 -> 20.90 us, its 2-rank shard 19.78 -> 16.16
+    // us, same box, profiles/r06_f)
     a.part_f16 = part_f16_ok(a.merge_launch, pl.D) ? 1 : 0;
     if (nch > 1) {
         // [arrival words, in-kernel merge only][(m, l) pairs][O partials]: [S][Y][chunks][64 rows]

@@ -256,11 +256,16 @@ def test_merge_plain_option():
 
 def test_part_f16_option():
     """FATTN_OPT_PART_F16: the second-launch merges take f16 partials by
-    default (split kernel's multi-row tiles, batched decode) except at D = 64
-    and with the in-kernel merge; 1 keeps f32; out of range is rejected."""
+    default for batched decode and for split tiles of 8+ rows (config 4's
+    4-row tiles keep f32: measured slower), never at D = 64 or with the
+    in-kernel merge; 1 forces f32, 2 f16; out of range is rejected."""
     c4 = _params(NQ=1, H=32, Hkv=8, N=8192, kt=fattn.TYPE_Q4_0)
     c5 = _params(NQ=64, H=32, Hkv=32, N=4096, kt=fattn.TYPE_Q8_0)
-    for p, kern in ((c4, "fattn_merge_kernel(f16 partials)"), (c5, "fattn_bd_merge_kernel(f16 partials)")):
+    s8 = _params(NQ=64, H=4, Hkv=4, N=4096, kt=fattn.TYPE_Q8_0)
+    assert "f16 partials" not in fattn.describe(c4), fattn.describe(c4)
+    with fattn.options({fattn.OPT_PART_F16: 2}):
+        assert "fattn_merge_kernel(f16 partials)" in fattn.describe(c4)
+    for p, kern in ((s8, "fattn_merge_kernel(f16 partials)"), (c5, "fattn_bd_merge_kernel(f16 partials)")):
         assert kern in fattn.describe(p), fattn.describe(p)
         with fattn.options({fattn.OPT_PART_F16: 1}):
             assert "f16 partials" not in fattn.describe(p)

@@ -520,16 +520,16 @@ def test_bd_chunk_merge_forms(dev, in_kernel, case):
     the second launch (default) or inside the launch (FATTN_OPT_MERGE_IN_KERNEL:
     every workgroup co-resident, each waits for the tile's count, then merges
     its share of the rows); both against the oracle, forced chunk counts
-    included.  The second launch reads f16 partials by default (0); 2: f32
-    partials with plain loads (FATTN_OPT_MERGE_PLAIN), 3: f32 partials with
-    sc1 loads (FATTN_OPT_PART_F16 = 1)."""
+    included.  The second launch with f16 partials (0, FATTN_OPT_PART_F16 =
+    2; the default here), f32 partials with plain loads (2,
+    FATTN_OPT_MERGE_PLAIN) or with sc1 loads (3)."""
     import torch
     p = make_problem(seed=90 + case["H"], **case)
     ref = p.oracle()
     t = upload(p, dev)
     fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 1 if in_kernel == 1 else 0)
     fattn.set_option(fattn.OPT_MERGE_PLAIN, 2 if in_kernel == 2 else 0)
-    fattn.set_option(fattn.OPT_PART_F16, 1 if in_kernel >= 2 else 0)
+    fattn.set_option(fattn.OPT_PART_F16, 1 if in_kernel >= 2 else 2 if in_kernel == 0 else 0)
     try:
         for chunk in (0, 1024):
             att = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=chunk)
@@ -540,7 +540,8 @@ def test_bd_chunk_merge_forms(dev, in_kernel, case):
             resident = g[0] * g[1] * g[2] <= cus  # one batched-decode workgroup per CU
             assert ("in-kernel" in desc) == (in_kernel == 1 and resident), desc
             assert ("merge_kernel(plain)" in desc) == (in_kernel == 2 and "merge_kernel" in desc), desc
-            assert ("merge_kernel(f16 partials)" in desc) == (in_kernel == 0 and "merge_kernel" in desc), desc
+            # (in_kernel 1 on a grid that is not co-resident: the second launch, auto = f16)
+            assert ("merge_kernel(f16 partials)" in desc) == (in_kernel in (0, 1) and "merge_kernel" in desc), desc
             t["dst"].fill_(float("nan"))
             att()
             torch.cuda.synchronize()
@@ -577,23 +578,24 @@ def test_bd_in_kernel_merge_graph_replays_new_inputs(dev):
 def test_split_multirow_merge_forms(dev, in_kernel, case):
     """Multi-row split tiles over 4+ KV chunks: the partials merge one wave per
     (tile, row), inside the launch (the tile's workgroups wait for each other)
-    or in the second launch (f16 partials by default except at D = 64; 2:
-    f32 partials with plain loads, FATTN_OPT_MERGE_PLAIN; 3: f32 partials,
-    FATTN_OPT_PART_F16 = 1); all against the oracle at several head dims."""
+    or in the second launch (0: f16 partials forced, FATTN_OPT_PART_F16 = 2,
+    except at D = 64; 2: f32 partials with plain loads, FATTN_OPT_MERGE_PLAIN;
+    3: f32 partials); all against the oracle at several head dims."""
     import torch
     p = make_problem(seed=70 + case["D"], **case)
     ref = p.oracle()
     t = upload(p, dev)
     fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 1 if in_kernel == 1 else 0)
     fattn.set_option(fattn.OPT_MERGE_PLAIN, 2 if in_kernel == 2 else 0)
-    fattn.set_option(fattn.OPT_PART_F16, 1 if in_kernel >= 2 else 0)
+    fattn.set_option(fattn.OPT_PART_F16, 1 if in_kernel >= 2 else 2 if in_kernel == 0 else 0)
     fattn.set_option(fattn.OPT_MQ_DISABLE, 1)
     try:
         for chunk in (0, 256):
             att = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=chunk)
             desc = att.describe()
             assert ("merge_kernel(plain)" in desc) == (in_kernel == 2 and "merge_kernel" in desc), desc
-            assert ("f16 partials" in desc) == (in_kernel == 0 and "merge_kernel" in desc and case["D"] != 64), desc
+            if in_kernel != 1:
+                assert ("f16 partials" in desc) == (in_kernel == 0 and "merge_kernel" in desc and case["D"] != 64), desc
             t["dst"].fill_(float("nan"))
             att()
             torch.cuda.synchronize()
