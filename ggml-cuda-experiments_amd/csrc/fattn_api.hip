@@ -61,6 +61,7 @@ std::atomic<int> g_opt_split_no_skip{0};    // 1: split kernel loads and compute
 std::atomic<int> g_opt_split_fused_merge{0};  // 1: multi-row split tiles merge in the last-arriving workgroup
 std::atomic<int> g_opt_bd{0};               // batched-decode kernel: 0 auto, 1 never, 2 whenever eligible
 std::atomic<int> g_opt_bd_xcd{0};           // batched decode, XCD-grouped workgroup order: 0 auto (on), 1 off, 2 on
+std::atomic<int> g_opt_gqa_unpack{0};       // GQA one-row decode: 0 auto (packed), 1 packed, 2 one q head per tile
 std::atomic<int> g_opt_part_f16{0};         // second-launch merges' partials: 0 auto (f16 where supported), 1 f32, 2 f16
 std::atomic<int> g_opt_merge_plain{0};      // second-launch merges: 0 auto (sc1 loads), 1 sc1, 2 plain loads
 std::atomic<int> g_opt_split_loaders{0};    // split kernel, one-row tiles: loader waves (FATTN_OPT_SPLIT_LOADERS): 0 auto, 1 off, 2 on
@@ -588,6 +589,18 @@ int make_plan(const fattn_params* p, Plan& pl) {
         a.QPT = kBdRows / a.R;
         a.n_qt = (int)((NQ + a.QPT - 1) / a.QPT);
     }
+    // GQA decode of one query row (config 4): one q head per split tile instead
+    // of the kv head's R heads packed -- one-row tiles, so the in-launch row
+    // merge (wg_row_merge) replaces the merge launch; each K/V byte is read
+    // by the R tiles of its kv head (the first from HBM, the rest mostly from
+    // the caches) (FATTN_OPT_GQA_UNPACK)
+    if (!pl.mq && !pl.pf && !pl.bd && NQ == 1 && a.rk2 > 1 && g_opt_gqa_unpack == 2) {
+        a.R = 1;
+        a.R_inv = 1.0f;
+        a.QPT = kRows;
+        a.n_hsub = a.rk2;
+        a.n_qt = 1;
+    }
     const int64_t Y = (int64_t)Hkv * a.n_hsub * a.n_qt;
     if (Y > 65535 || S > 65535) return FATTN_ERR_INVALID_ARG;
     if (pl.bd) return size_bd(pl, p->kv_chunk, Y, S, N);
@@ -746,6 +759,10 @@ int fattn_set_option(int option, int value) {
         case FATTN_OPT_BD_XCD:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
             g_opt_bd_xcd = value;
+            return FATTN_OK;
+        case FATTN_OPT_GQA_UNPACK:
+            if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;
+            g_opt_gqa_unpack = value;
             return FATTN_OK;
         case FATTN_OPT_PART_F16:
             if (value < 0 || value > 2) return FATTN_ERR_INVALID_ARG;

@@ -58,12 +58,13 @@ OPT_PF_FORM = 29
 OPT_SPLIT_LOADERS = 30
 OPT_MERGE_PLAIN = 31
 OPT_PART_F16 = 32
+OPT_GQA_UNPACK = 33
 # every option's default (include/fattn_debug.h): reset_options() restores them
 OPTION_DEFAULTS = {
     OPT_MQ_ROWS_PER_WAVE: 0, OPT_MQ_DISABLE: 0, OPT_SPLIT_STEPS: 0, OPT_SPLIT_INFLIGHT: 0, OPT_PF: 0,
     OPT_PF_STAGGER: 2, OPT_SPLIT_WAVE_MERGE: 0, OPT_SPLIT_PRIO: 0, OPT_PF_SKIP: 0, OPT_MQ_MIN_ROWS: 0,
     OPT_SPLIT_WAVES: 0, OPT_SPLIT_SKIP: 0, OPT_SPLIT_MERGE: 0, OPT_BD: 0, OPT_MERGE_IN_KERNEL: 0, OPT_BD_XCD: 0, OPT_SPLIT_XCD: 0,
-    OPT_PF_STAGE: 0, OPT_PF_FORM: 0, OPT_SPLIT_LOADERS: 0, OPT_MERGE_PLAIN: 0, OPT_PART_F16: 0,
+    OPT_PF_STAGE: 0, OPT_PF_FORM: 0, OPT_SPLIT_LOADERS: 0, OPT_MERGE_PLAIN: 0, OPT_PART_F16: 0, OPT_GQA_UNPACK: 0,
 }
 
 

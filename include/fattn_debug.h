@@ -94,6 +94,9 @@ enum {
                                        rows, D = 64 / 128, one K / V type): 0 = auto, 1 = off (every wave issues its
                                        own steps), 2 = 4 loader waves issue every step up front and hand each over
                                        to its compute wave by LDS flags (fattn_split_ld_kernel) */
+    FATTN_OPT_GQA_UNPACK = 33,      /* GQA decode of one query row (config 4): 0 = auto (packed), 1 = the kv head's
+                                       R q heads packed in one split tile (second-launch merge), 2 = one q head
+                                       per tile (one-row tiles, merged in the launch; K/V read R times) */
     FATTN_OPT_PART_F16 = 32,        /* chunk partials of the second-launch merges (multi-row split tiles, batched
                                        decode; D != 64): 0 = auto (f16 for batched decode and for split tiles of 8+
                                        rows), 1 = f32 (O unnormalised), 2 = f16 (O / l in f16 beside (m, l) in

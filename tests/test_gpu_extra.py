@@ -619,3 +619,31 @@ def test_split_in_kernel_merge_graph_replays_new_inputs(dev):
         fattn.set_option(fattn.OPT_MQ_DISABLE, 0)
         fattn.set_option(fattn.OPT_MERGE_IN_KERNEL, 0)
     assert "in-kernel" in desc, desc
+
+
+@pytest.mark.parametrize("case", [
+    dict(D=128, NQ=1, H=32, Hkv=8, N=8192, kv_type="q4_0"),                # config 4
+    dict(D=128, NQ=1, H=32, Hkv=8, N=4096, kv_type="q8_0", mask="tail"),   # whole chunks -inf
+    dict(D=128, NQ=1, H=16, Hkv=2, N=2048, kv_type="f16"),                 # R = 8, f16
+    dict(D=128, NQ=1, H=12, Hkv=2, N=4000, kv_type="q8_0"),                # R = 6, ragged
+    dict(D=64, NQ=1, H=32, Hkv=8, N=4096, kv_type="q8_0", extreme=True),   # D = 64, rescales
+], ids=["cfg4", "tail", "f16_r8", "r6_ragged", "d64_extreme"])
+def test_gqa_unpacked_decode(dev, case):
+    """FATTN_OPT_GQA_UNPACK = 2: a one-row GQA decode takes one q head per
+    split tile (one-row tiles, the chunk rows merged inside the launch, each
+    K/V byte read by the kv head's R tiles) -- against the oracle, over
+    repeated launches on one workspace."""
+    import torch
+    p = make_problem(seed=77 + case["H"], **case)
+    ref = p.oracle()
+    t = upload(p, dev)
+    with fattn.options({fattn.OPT_GQA_UNPACK: 2}):
+        att = fattn.Attention(*views(p, t), t["dst"], p.scale)
+        desc = att.describe()
+        assert "merge_kernel" not in desc, desc
+        for _ in range(3):
+            t["dst"].fill_(float("nan"))
+            att()
+            torch.cuda.synchronize()
+            got = t["dst"].cpu().numpy()
+            assert attn_rel_err(got, ref) <= RTOL, desc

@@ -116,4 +116,11 @@ pass_k() {
   run ab_p16_c4 300 python -u tools/ab_decode.py --workload config4 --rounds 6 --variant f16: --variant f32:PART_F16=1
   run ab_p16_s2 300 python -u tools/ab_decode.py --workload config5_s2 --rounds 4 --variant f16: --variant f32:PART_F16=1
 }
+# Twelfth pass: the GQA one-row decode with one q head per tile (config 4) --
+# parity, same-box A/B against the packed plan; the merge tests after the
+# f16-partial policy change.
+pass_l() {
+  run t_l 900 python -u -m pytest tests/test_gpu_extra.py tests/test_gpu_parity.py -q --timeout 300 --timeout-method thread -m gpu -k "gqa_unpacked or merge_forms or config4 or shard"
+  run ab_unpack_c4 300 python -u tools/ab_decode.py --workload config4 --rounds 6 --variant packed: --variant unpack:GQA_UNPACK=2 --variant unpack_s2:GQA_UNPACK=2,SPLIT_STEPS=2 --variant unpack_w4:GQA_UNPACK=2,SPLIT_WAVES=4
+}
 "$@"
