@@ -236,6 +236,67 @@ def cpu_baseline_prefill(rows=256):
             "extrapolation": f"linear: x {NQ // rows} rows x {H} heads (not measured)"}
 
 
+def seq64_measure(dev, hip, evs, steps=20, S=64, H=32, N=4096, D=128, kvn="q8_0"):
+    """SURVEY.md §8d's alternative reading of config 5, reported as a labelled
+    extra: 64 independent sequences (ggml ne03 = 64), one query row each, each
+    with its own 4096-position Q8_0 cache -- 2.28 GB of K + V per step, read
+    once (a step alone is 9x the 256 MiB Infinity Cache: no rotation needed).
+    The mask row is broadcast over the sequences (ggml's ne32 = 1).  `steps`
+    launches captured in one HIP graph, HIP events around the replay on the
+    launch stream."""
+    import torch
+    import fattn
+    typ = fattn.TYPE_NAMES[kvn]
+    rb = fattn.row_size(typ, D)
+    g = torch.Generator(device=dev)
+    g.manual_seed(6464)
+    kv = []
+    for _ in range(2):  # K, V: [S][H][N][row], quantised one sequence at a time
+        buf = torch.empty((S, H * N * rb), dtype=torch.uint8, device=dev)
+        for s_ in range(S):
+            x = torch.rand((H * N, D), generator=g, device=dev, dtype=torch.float32) * 2 - 1
+            buf[s_].copy_(fattn.quantize(x, typ).reshape(-1))
+            del x
+        kv.append(buf.reshape(-1))
+    q = torch.rand((S, 1, H, D), generator=g, device=dev) * 2 - 1
+    mask = (torch.rand((1, (N + 63) // 64 * 64), generator=g, device=dev) * 2 - 1).to(torch.float16)
+    out = torch.empty((S, 1, H, D), dtype=torch.float32, device=dev)
+    att = fattn.Attention(fattn.q_view(q), fattn.kv_view(kv[0], typ, D, N, H, S), fattn.kv_view(kv[1], typ, D, N, H, S),
+                          fattn.mask_view(mask), out, 1.0 / D ** 0.5)
+    gs = torch.cuda.Stream(dev)
+    gs.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(gs):
+        for _ in range(2):
+            att()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=gs):
+        for _ in range(steps):
+            att()
+    with torch.cuda.stream(gs):
+        graph.replay()
+    torch.cuda.synchronize()
+    f = C.c_float()
+    hip.hipEventRecord(evs[0], gs.cuda_stream)
+    with torch.cuda.stream(gs):
+        graph.replay()
+    hip.hipEventRecord(evs[1], gs.cuda_stream)
+    torch.cuda.synchronize()
+    hip.hipEventElapsedTime(C.byref(f), evs[0], evs[1])
+    ms = f.value / steps
+    alg = 2 * S * H * N * rb + 2 * S * H * D * 4 + N * 2  # K + V + Q + O + the broadcast mask row
+    gbs = alg / (ms * 1e-3) / 1e9
+    res = {"workload": f"decode_{kvn}_h{H}_d{D}_n{N}_q1_s{S}", "kernel": att.describe(), "kernel_ms_avg": round(ms, 5),
+           "bytes_per_step": alg, "value": round(gbs, 2), "unit": "GB/s",
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": 8000.0, "unit": "GB/s",
+                        "frac": round(gbs / 8000.0, 4)},
+           "note": "SURVEY.md 8(d)'s alternative reading of config 5, labelled as an extra: 64 independent "
+                   "sequences (ne03 = 64), one query row each, each its own 4096-position Q8_0 cache"}
+    del kv, q, out, att, graph
+    torch.cuda.empty_cache()
+    return res
+
+
 def prefill_measure(dev, hip, evs, kvn="q8_0", mask_kind="zero", steps=5, D=128, H=32, reps=3):
     """The MFMA-bound prefill shape of SURVEY.md §8d (n_q = N = 4096, 32 heads,
     head_dim 128, Q8_0 K/V, non-causal, an f16 mask of zeros -- "zero mask":
@@ -912,6 +973,9 @@ def main():
                 "kernel_ms_avg": round(r5["kernel_ms_avg"], 5), "kernel": r5["kernel"],
                 "note": "bench.py --gpus N runs this workload head-sharded; strong-scaling efficiency = "
                         "value(N) / (N * this value)"}
+        if not args.no_scale_ref and workload == "config3":
+            hip, evs = hip_events(2)
+            line["config5_seq64"] = seq64_measure(dev, hip, evs)
         if not args.no_prefill and shape["n_q"] == 1:
             hip, evs = hip_events(2)
             line["prefill"] = prefill_measure(dev, hip, evs, args.prefill_kv, args.prefill_mask)

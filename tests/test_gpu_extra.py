@@ -17,7 +17,7 @@ import fattn
 from fattn.shard import assemble_heads, head_views, shard_heads
 from gpu_util import run_gpu, upload, views
 from oracle import oracle as orc
-from problems import attn_rel_err, make_problem
+from problems import attn_elem_err, attn_rel_err, make_problem
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-3
@@ -647,3 +647,14 @@ def test_gqa_unpacked_decode(dev, case):
             torch.cuda.synchronize()
             got = t["dst"].cpu().numpy()
             assert attn_rel_err(got, ref) <= RTOL, desc
+
+
+def test_seq64_decode(dev):
+    """SURVEY 8(d)'s alternative reading of config 5 at a reduced cache: 64
+    independent sequences (ne03 = 64), one query row each, each its own KV
+    (4 heads x 1024 positions, Q8_0), the mask row broadcast -- the bench's
+    config5_seq64 line runs the same plan family at 32 heads x 4096."""
+    p = make_problem(D=128, NQ=1, H=4, Hkv=4, N=1024, kv_type="q8_0", S=64, seed=64)
+    got, ref = run_gpu(p), p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0

@@ -123,4 +123,10 @@ pass_l() {
   run t_l 900 python -u -m pytest tests/test_gpu_extra.py tests/test_gpu_parity.py -q --timeout 300 --timeout-method thread -m gpu -k "gqa_unpacked or merge_forms or config4 or shard"
   run ab_unpack_c4 300 python -u tools/ab_decode.py --workload config4 --rounds 6 --variant packed: --variant unpack:GQA_UNPACK=2 --variant unpack_s2:GQA_UNPACK=2,SPLIT_STEPS=2 --variant unpack_w4:GQA_UNPACK=2,SPLIT_WAVES=4
 }
+# Thirteenth pass: config 5's 64-sequence reading (bench side line) -- parity
+# at a reduced cache, the bench line on the final kernels.
+pass_m() {
+  run t_m 300 python -u -m pytest tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "seq64 or gqa_unpacked"
+  run bench 600 python -u bench.py
+}
 "$@"
