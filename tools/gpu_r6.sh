@@ -129,4 +129,10 @@ pass_m() {
   run t_m 300 python -u -m pytest tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "seq64 or gqa_unpacked"
   run bench 600 python -u bench.py
 }
+# Fourteenth pass: with f16 partials, does the batched-decode role form now
+# beat the split kernel on the 4- and 8-rank config-5 shards?
+pass_n() {
+  run ab_bd_s8 300 python -u tools/ab_decode.py --workload config5_s8 --rounds 6 --variant auto: --variant bdp:BD=3 --variant bd:BD=2
+  run ab_bd_s4 300 python -u tools/ab_decode.py --workload config5_s4 --rounds 6 --variant auto: --variant bdp:BD=3 --variant bd:BD=2
+}
 "$@"
