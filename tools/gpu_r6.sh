@@ -135,4 +135,9 @@ pass_n() {
   run ab_bd_s8 300 python -u tools/ab_decode.py --workload config5_s8 --rounds 6 --variant auto: --variant bdp:BD=3 --variant bd:BD=2
   run ab_bd_s4 300 python -u tools/ab_decode.py --workload config5_s4 --rounds 6 --variant auto: --variant bdp:BD=3 --variant bd:BD=2
 }
+# Fifteenth pass: config 5 (bdp) variants around the f16-partial plan: the
+# in-kernel merge (f32 sc1 partials), plain workgroup order.
+pass_o() {
+  run ab_c5_var 400 python -u tools/ab_decode.py --workload config5 --rounds 6 --variant auto: --variant inkernel:MERGE_IN_KERNEL=1 --variant plainxcd:BD_XCD=1 --variant f32:PART_F16=1
+}
 "$@"
