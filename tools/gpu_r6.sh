@@ -140,4 +140,8 @@ pass_n() {
 pass_o() {
   run ab_c5_var 400 python -u tools/ab_decode.py --workload config5 --rounds 6 --variant auto: --variant inkernel:MERGE_IN_KERNEL=1 --variant plainxcd:BD_XCD=1 --variant f32:PART_F16=1
 }
+# Sixteenth pass: config 5's bdp timeline on the f16-partial tree (stamps build).
+pass_p() {
+  run st_bdp_c5 200 python -u tools/stamps_bd.py --form bdp --heads 32 --kv-len 4096 --n-q 64
+}
 "$@"
