@@ -450,16 +450,21 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             // descriptor (no traffic; into a slot nothing reads again), so every
             // counted wait is one constant and the issues sit inside B's steps
             // without a branch.
-            auto k_piece = [&](int s, int i) {
+            // (slot: the ring slot s % 3, which the balanced loop carries from tile
+            // to tile instead of dividing -- four mod-3 divisions a tile were 16
+            // scalar instructions of a one-wave-per-SIMD loop)
+            auto k_piece_at = [&](int s, int slot, int i) {
                 const uint32_t nk = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.k_nb1;
-                const uint32_t dst = lds0 + C::kOff + (s % C::KS) * C::img + (wave + kPf4Waves * i) * 1024;
-                dma<16>(rs.k, dst, s < nt ? nk + koff0 + 64 * i : a.k_span);
+                const uint32_t dst = lds0 + C::kOff + slot * C::img + (wave + kPf4Waves * i) * 1024;
+                dma<16, false, 0>(rs.k, dst, s < nt ? nk + koff0 + 64 * i : a.k_span);
             };
-            auto v_piece = [&](int s, int i) {
+            auto v_piece_at = [&](int s, int slot, int i) {
                 const uint32_t nv = (uint32_t)(t0 + s) * kPfKeys * (uint32_t)a.v_nb1;
-                const uint32_t dst = lds0 + C::vOff + (s % C::VS) * C::img + (wave + kPf4Waves * i) * 1024;
-                dma<16>(rs.v, dst, s < nt ? nv + voff0 + 64 * i : a.v_span);
+                const uint32_t dst = lds0 + C::vOff + slot * C::img + (wave + kPf4Waves * i) * 1024;
+                dma<16, false, 0>(rs.v, dst, s < nt ? nv + voff0 + 64 * i : a.v_span);
             };
+            auto k_piece = [&](int s, int i) { k_piece_at(s, s % C::KS, i); };
+            auto v_piece = [&](int s, int i) { v_piece_at(s, s % C::VS, i); };
             // (skip: tile s past the end or a +-0 block, decided once per tile --
             // inside B's steps a branch would split the phase)
             auto m_skip = [&](int s) { return s >= nt || zero_of(s); };
@@ -527,11 +532,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             // ahead of their MFMA -- with all of a phase's reads at its head the
             // 4-bit lgkmcnt cannot name the first one, and the first MFMA waited
             // for half of them)
-            auto k_base = [&](int s) {
-                uint32_t kb = (uint32_t)(C::kOff + (s % C::KS) * C::img) + kbase;
+            auto k_base_at = [&](int slot) {
+                uint32_t kb = (uint32_t)(C::kOff + slot * C::img) + kbase;
                 PF4_OPAQUE_V(kb);
                 return kb;
             };
+            auto k_base = [&](int s) { return k_base_at(s % C::KS); };
             auto k_read1 = [&](uint32_t kb, int t, int kk) {
                 kr[t][kk] = *(const __attribute__((address_space(3))) f16x8*)((const lds_u8*)smem + kb + kk * (kPfKeys * 32) +
                                                                            t * 1024);
@@ -886,14 +892,17 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
 #else
             constexpr bool kDiagNoDma = false;
 #endif
-            auto iter_bal = [&](int j, auto first) {
+            static_assert(C::KS == 3 && C::VS == 3, "the balanced loop carries j % 3");
+            // r0 = j % 3 (K_j, V_j, K_{j+3}: ring slot r0; K_{j+1}: r1; V_{j-1}: rm)
+            auto iter_bal = [&](int j, auto first, int r0) {
                 constexpr bool F = decltype(first)::value;
+                const int r1 = r0 == 2 ? 0 : r0 + 1, rm = r0 == 0 ? 2 : r0 - 1;
                 PF4_T(7);
                 wait_vmcnt_c<C::NKI + MI>();  // B_{j-1}'s issues (K_{j+2}, mask j+1) may fly
                 PF4_T(0);
                 f16x8 va[2][2][NDB];
-                uint32_t vb0 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[0];
-                uint32_t vb1 = (uint32_t)(C::vOff + (((j > 0 ? j : 1) - 1) % C::VS) * C::img) + vbase[1];
+                uint32_t vb0 = (uint32_t)(C::vOff + (F ? 0 : rm) * C::img) + vbase[0];
+                uint32_t vb1 = (uint32_t)(C::vOff + (F ? 0 : rm) * C::img) + vbase[1];
                 PF4_OPAQUE_V2(vb0, vb1);
                 auto v_read1 = [&](int v) {
                     const int t = v >> 3, q = (v >> 2) & 1, db = v & 3;
@@ -904,7 +913,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     va[t][q][db] = __builtin_bit_cast(f16x8, u32x4{a2.x, a2.y, b2.x, b2.y});
                 };
                 u32x2 mk1[2][4], mk0[2][4];
-                const uint32_t kb = k_base(j);
+                const uint32_t kb = k_base_at(r0);
                 if constexpr (F) {
 #pragma unroll
                     for (int kk = 0; kk < 4; kk++) k_read1(kb, 0, kk);
@@ -921,7 +930,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     if constexpr (!F) {
                         if (i >= 24 && !(i & 1)) v_read1((i - 24) >> 1);
                     }
-                    if (!kDiagNoDma && i < 16 && (i & 3) == 1) v_piece(j, i >> 2);
+                    if (!kDiagNoDma && i < 16 && (i & 3) == 1) v_piece_at(j, r0, i >> 2);
                     if constexpr (MM) {
                         if (i == 8) mask_reads(j, 1, mk1);
                         if (i == 14) mask_reads(j, 0, mk0);
@@ -994,7 +1003,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 PF4_T(4);
                 __builtin_amdgcn_sched_barrier(0);
                 float tred0 = 0.0f, tred1 = 0.0f;
-                const uint32_t kbn = k_base(j + 1);
+                const uint32_t kbn = k_base_at(r1);
 #pragma unroll
                 for (int i = 0; i < 32; i++) {
                     if (i == 0 && !LN) {
@@ -1038,7 +1047,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                         const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
                         o[rb][db] = mfma32(va[t][q][db], rb ? p1[t][q] : p0[t][q], o[rb][db]);
                     }
-                    if (!kDiagNoDma && i < 16 && (i & 3) == 1) k_piece(j + 3, i >> 2);
+                    if (!kDiagNoDma && i < 16 && (i & 3) == 1) k_piece_at(j + 3, r0, i >> 2);
                     if (!kDiagNoDma && i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
                     if (i >= 28) k_read1(kbn, 0, i - 28);
                     __builtin_amdgcn_sched_barrier(0);
@@ -1076,8 +1085,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             kt_loop0 = __builtin_amdgcn_s_memtime();
 #endif
             if constexpr (SCHED >= 3) {
-                if (nt > 0) iter_bal(0, std::true_type());
-                for (int j = 1; j < nt; j++) iter_bal(j, std::false_type());
+                if (nt > 0) iter_bal(0, std::true_type(), 0);
+                int r0 = 0;
+                for (int j = 1; j < nt; j++) {
+                    r0 = r0 == 2 ? 0 : r0 + 1;  // (j % 3)
+                    iter_bal(j, std::false_type(), r0);
+                }
                 if (nt > 0) {
                     // ---- A_nt, B_nt: rb 0's exponentials of the last tile, its P.V
                     wait_vmcnt_c<0>();

@@ -265,9 +265,14 @@ __device__ __forceinline__ u32x4 ld_buf_untracked(const i32x4& srd, uint32_t off
 // save / restore form, padded the same way, for A/B builds.)
 // NT: non-temporal policy for bytes one CU reads once (the decode KV stream,
 // MI355X_MICROARCH.md 'nt-weights'); never for tiles other workgroups re-read.
-template <int BYTES, bool NT = false>
+// PAD: the opening s_nop's count -- 4 (5 wait states) unless the caller's
+// descriptor is provably not freshly VALU-written (pf4's loop: its descriptors
+// are loop-invariant SGPRs; tools/isa_hazard_check.py checks every call site
+// on the shipped ISA, so a PAD that is too small fails the CPU test suite)
+template <int BYTES, bool NT = false, int PAD = 4>
 __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds_any, uint32_t off) {
     static_assert(BYTES == 16 || BYTES == 4, "");
+    static_assert(PAD >= 0 && PAD <= 4, "");
     // wave-uniform by construction; readfirstlane keeps it an SGPR operand even
     // where divergent code around the call hides that from the compiler
     const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_any);
@@ -280,8 +285,9 @@ __device__ __forceinline__ void dma(const i32x4& srd, uint32_t lds_any, uint32_t
                  : "v"(off), "s"(srd), "s"(lds)                                                          \
                  : "memory")
 #else
-#define FATTN_DMA_ASM(INSN, MOD) \
-    asm volatile("s_nop 4\n\t" INSN " %0, %1, 0 offen" MOD : : "v"(off), "s"(srd), "{m0}"(lds) : "memory")
+#define FATTN_DMA_ASM(INSN, MOD)                                                                     \
+    asm volatile("s_nop %3\n\t" INSN " %0, %1, 0 offen" MOD : : "v"(off), "s"(srd), "{m0}"(lds), "n"(PAD) \
+                 : "memory")
 #endif
     if constexpr (BYTES == 16 && NT) FATTN_DMA_ASM("buffer_load_dwordx4", " nt lds");
     else if constexpr (BYTES == 16) FATTN_DMA_ASM("buffer_load_dwordx4", " lds");

@@ -144,4 +144,17 @@ pass_o() {
 pass_p() {
   run st_bdp_c5 200 python -u tools/stamps_bd.py --form bdp --heads 32 --kv-len 4096 --n-q 64
 }
+# Seventeenth pass: the lean loop's ring slots carried (no mod-3 divisions)
+# and its K / V DMA opened by s_nop 0 (loop-invariant descriptors, audited) --
+# prefill parity, then processes alternating libfattn.so and the previous
+# tree's libfattn_prev.so.
+pass_q() {
+  run t_q 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "pf or prefill"
+  for r in 1 2 3; do
+    for L in libfattn.so libfattn_prev.so; do
+      FATTN_LIB=$L run ab_q_z_${L%.so}_$r 200 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 2 --variant $L:
+      FATTN_LIB=$L run ab_q_f_${L%.so}_$r 200 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 2 --variant $L:
+    done
+  done
+}
 "$@"
