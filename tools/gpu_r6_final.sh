@@ -21,7 +21,7 @@ fi
 run bench 600 python bench.py
 grep '^{' gpurun_out/bench.log > $F/bench.json || true
 run kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6f_kt -o kt -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline
-python tools/kstats.py $(find gpurun_out/r6f_kt -name "*kernel_stats.csv") > $F/kernel_stats_summary.txt 2>&1 || true
+python tools/kstats.py $(find gpurun_out/r6f_kt -name "*kernel_stats.csv") $(find gpurun_out/r6f_kt -name "*kernel_trace.csv") > $F/kernel_stats_summary.txt 2>&1 || true
 D="--no-cpu-baseline --no-scale-ref --no-copy-peak --no-prefill --steps 50 --warmup 5"
 run fetch_cfg3 180 timeout -s KILL 170 rocprofv3 --output-format csv --pmc FETCH_SIZE -d gpurun_out/r6f_fetch -o f -- python3 bench.py $D
 run write_cfg3 180 timeout -s KILL 170 rocprofv3 --output-format csv --pmc WRITE_SIZE -d gpurun_out/r6f_write -o w -- python3 bench.py $D
