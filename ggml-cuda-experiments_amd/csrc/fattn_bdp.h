@@ -310,20 +310,15 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
     // 0 .. nRaw - 1.  Build waves: Q | their pieces of raw 0 .. nRaw - 1; after
     // the barrier that completes raw 0 they dequantise it into pair 0.
     const int npro = min(C::nRaw, ntiles);  // raw tiles of the prologue
-    // (raw 0 and 1 before raw 0's dequantisation, the rest after it: issuing all
-    // nRaw up front kept the build waves in a full memory queue for ~4.5 us
-    // before they could start on raw 0 -- profiles/r06_k; not in the
-    // all-waves-issue A/B build, whose compute waves count raw pieces too)
-    const int nearly = C::kAll ? npro : min(2, npro);
     if (compute) {
         if (ntiles > 0) mask_issue(0);
         if (ntiles > 1) mask_issue(1);
     }
-    for (int t = 0; t < nearly; t++) bdp_issue<KT, D>(rs, c_lo + t * kBdpKeys, raw_lds(t), wave, lane);
+    for (int t = 0; t < npro; t++) bdp_issue<KT, D>(rs, c_lo + t * kBdpKeys, raw_lds(t), wave, lane);
     FATTN_STAMP(1);
     // Q, (masks 0 and 1,) this wave's pieces of raw 0 landed
-    if (compute) bdp_compute_wait<KT, D, NM>(max(nearly - 1, 0), 0);
-    else bdp_build_wait<KT, D>(nearly - 1);
+    if (compute) bdp_compute_wait<KT, D, NM>(max(npro - 1, 0), 0);
+    else bdp_build_wait<KT, D>(npro - 1);
     __syncthreads();  // Q and raw 0 complete in LDS
     f16x8 qop[NK];
     if (compute) {
@@ -343,7 +338,6 @@ __global__ __launch_bounds__(kBdWaves* kWave, 2) void fattn_bdp_kernel(const Spl
     } else {
         if (ntiles > 0) {
             bdp_dequant<KT, D>(raw_ptr(0), smem, smem + C::img, bw, lane);
-            for (int t = nearly; t < npro; t++) bdp_issue<KT, D>(rs, c_lo + t * kBdpKeys, raw_lds(t), wave, lane);
             // raw 1 landed (raw 2 .. nRaw - 1 may fly on).  Raw nRaw goes into
             // slot 0 after the loop's first barrier: every build wave reads all
             // of a slot's rows, so a slot is free only once they all have.
