@@ -157,4 +157,16 @@ pass_q() {
     done
   done
 }
+# Eighteenth pass (reverted change): bdp's prologue issuing raw 0 and 1 only
+# before raw 0's dequantisation -- batched-decode parity, then processes
+# alternating libfattn.so and the previous tree's libfattn_prev.so.
+pass_r() {
+  run t_r 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "bd or config5 or batched or shard"
+  for r in 1 2 3; do
+    for L in libfattn.so libfattn_prev.so; do
+      FATTN_LIB=$L run ab_r_c5_${L%.so}_$r 200 python -u tools/ab_decode.py --workload config5 --rounds 2 --variant $L:
+      FATTN_LIB=$L run ab_r_s2_${L%.so}_$r 200 python -u tools/ab_decode.py --workload config5_s2 --rounds 2 --variant $L:
+    done
+  done
+}
 "$@"
