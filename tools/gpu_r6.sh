@@ -169,4 +169,8 @@ pass_r() {
     done
   done
 }
+# Nineteenth pass: how much of the oracle bar the f16 chunk partials use.
+pass_s() {
+  run err_part 300 python -u tools/err_part.py
+}
 "$@"
