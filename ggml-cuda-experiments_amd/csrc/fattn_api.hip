@@ -651,7 +651,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
         // form 1 keeps the 8-wave body)
         const int form = g_opt_pf_form == 0 ? 6 : (int)g_opt_pf_form;
         pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && form >= 4;
-        pl.pf4_sched = form - 2;  // 4: pipelined (SCHED 2), 5: balanced (SCHED 3), 6: lean (SCHED 4), 7: lean2 (SCHED 5)
+        pl.pf4_sched = form - 2;  // 4: pipelined (SCHED 2), 5: balanced (SCHED 3), 6: lean (SCHED 4)
         if (pl.pf4) pl.lds = Pf4Cfg<128>::ldsBytes;
         pl.grid = dim3(1, (unsigned)Y, (unsigned)S);
         // workspace: live-block flags, n_qt x N/64 bytes (masked prefill).  They
@@ -782,7 +782,7 @@ int fattn_set_option(int option, int value) {
             return FATTN_OK;
         case FATTN_OPT_PF_FORM:
             // 2, 3: round 5's unpipelined one-wave-per-SIMD forms, removed (slower)
-            if (value < 0 || value > 7 || value == 2 || value == 3) return FATTN_ERR_INVALID_ARG;
+            if (value < 0 || value > 6 || value == 2 || value == 3) return FATTN_ERR_INVALID_ARG;
             g_opt_pf_form = value;
             return FATTN_OK;
         case FATTN_OPT_PF_STAGE:
@@ -850,7 +850,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
                       pl.pf_stage ? (pl.stage_kt == FATTN_TYPE_Q8_0 ? "kv_stage_f16<q8_0>" : "kv_stage_f16<q4_0>") : "",
                       pl.pf_stage && pl.pf_flags ? " + " : "", pl.pf_flags ? "pf_mask_flags" : "",
                       (pl.pf_stage || pl.pf_flags) ? "] + " : "",
-                      pl.pf4 ? (pl.pf4_sched == 5 ? "fattn_pf4_kernel(lean2)" : pl.pf4_sched == 4 ? "fattn_pf4_kernel(lean)" : pl.pf4_sched == 3 ? "fattn_pf4_kernel(balanced)" : "fattn_pf4_kernel(pipelined)") : "fattn_pf_kernel",
+                      pl.pf4 ? (pl.pf4_sched == 4 ? "fattn_pf4_kernel(lean)" : pl.pf4_sched == 3 ? "fattn_pf4_kernel(balanced)" : "fattn_pf4_kernel(pipelined)") : "fattn_pf_kernel",
                       tn(pl.kt), pl.D, hm);
     else if (pl.bd)
         std::snprintf(kern, sizeof kern, "%s<%s,D%d,%s>%s%s", pl.bdp ? "fattn_bdp_kernel" : "fattn_bd_kernel", tn(pl.kt), pl.D,

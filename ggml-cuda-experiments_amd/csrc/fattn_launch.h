@@ -214,8 +214,7 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
     const void* main_kern = (const void*)kern;
     if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
         if (pl.pf4)
-            main_kern = pl.pf4_sched == 5   ? (const void*)fattn_pf4_kernel<D, HM, 5>
-                        : pl.pf4_sched == 4 ? (const void*)fattn_pf4_kernel<D, HM, 4>
+            main_kern = pl.pf4_sched == 4   ? (const void*)fattn_pf4_kernel<D, HM, 4>
                         : pl.pf4_sched == 3 ? (const void*)fattn_pf4_kernel<D, HM, 3>
                                             : (const void*)fattn_pf4_kernel<D, HM, 2>;
     }
@@ -244,9 +243,7 @@ int launch_pf_hm(const Plan& pl, hipStream_t st, const Events& ev) {
         }
         if constexpr (KT == FATTN_TYPE_F16 && D == 128) {
             if (pl.pf4) {
-                if (pl.pf4_sched == 5)
-                    hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 5>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
-                else if (pl.pf4_sched == 4)
+                if (pl.pf4_sched == 4)
                     hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 4>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);
                 else if (pl.pf4_sched == 3)
                     hipLaunchKernelGGL((fattn_pf4_kernel<D, HM, 3>), pl.grid, dim3(kPf4Waves * kWave), pl.lds, st, pl.a);

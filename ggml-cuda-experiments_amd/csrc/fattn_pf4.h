@@ -190,16 +190,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     // stays h(q) (src/utils.h:10): pre-scaling it by c instead (one rounding
     // more) cost 5e-3 on large scores.  Not bit-identical to the 8-wave body
     // (the -m / c enters the f32 chain): the oracle's 1e-3 is the bar.
-    // SCHED 5 ("lean2", FATTN_OPT_PF_FORM 7): the lean arithmetic with the S^T
-    // chains started from 0 and the argument fma(s, c, -m) -- the same one
-    // VALU per score as lean's multiply, without the 32 AGPRs of chain starts
-    // -- and each row's sum l taken by the matrix core: in phase B, beside
-    // P.V, an extra MFMA per (subtile, k-half) multiplies a ones matrix by the
-    // same P^T fragments (l = sum of the f16 p that P.V uses), so the row-sum
-    // adds (64 VALU a tile) leave the vector pipe for 8 MFMAs; the
-    // accumulator is rescaled with O.  Bodies without mask values only.
-    constexpr bool LEAN = SCHED >= 4;
-    constexpr bool LEAN2 = SCHED == 5;
+    constexpr bool LEAN = SCHED == 4;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -360,23 +351,13 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     }
     f32x16 s0[2], s1[2];  // S^T of rb 0 and rb 1 (both computed in A_j), per subtile
     f32x16 ci[2];         // (SCHED 4) each row block's S^T chain start: -m / c of the row (0 while m = -inf)
-    f32x16 lacc[2];       // (SCHED 5) each row block's row sums by MFMA (every register of a lane: its row's l)
-    f16x8 ones;           // (SCHED 5) the all-ones A operand of those MFMAs
-    bool lean2_used = false;  // (SCHED 5) this workgroup's body took the row sums by MFMA
-#pragma unroll
-    for (int e = 0; e < 8; e++) ones[e] = (f16)1.0f;
-#pragma unroll
-    for (int rb = 0; rb < 2; rb++) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) lacc[rb][j] = 0.0f;
-    }
 #pragma unroll
     for (int rb = 0; rb < 2; rb++) {
 #pragma unroll
         for (int j = 0; j < 16; j++) ci[rb][j] = 0.0f;
         // (held in AGPRs, where the MFMAs take it as srcC: from VGPRs hipcc
         // copied it to AGPRs before every chain, 32 v_accvgpr_write a tile)
-        if constexpr (SCHED == 4) asm volatile("" : "+a"(ci[rb]));  // (SCHED 5: unused)
+        if constexpr (SCHED == 4) asm volatile("" : "+a"(ci[rb]));
     }
 
     // mask values of row block rb for tile s (a +-0 block's slot holds the
@@ -585,7 +566,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
                     for (int db = 0; db < NDB; db++) scale_acc16(o[rb][db], alpha);
-                    if constexpr (LEAN2 && LN) scale_acc16(lacc[rb], alpha);
                 }
             };
             // The phases are written as 32 explicit (MFMA, vector piece) steps, each
@@ -632,10 +612,8 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             };
             auto e3 = [&](f16x8 (&pb)[2][2], float& la, float& lb, int pc) {
                 const int t = pc >> 3, k = 2 * (pc & 7);
-                if constexpr (!(LEAN2 && LN)) {  // (SCHED 5 without mask values: the row sums by MFMA in phase B)
-                    la = add_f32(la, sE[pc][0]);
-                    lb = add_f32(lb, sE[pc][1]);
-                }
+                la = add_f32(la, sE[pc][0]);
+                lb = add_f32(lb, sE[pc][1]);
                 pb[t][k >> 3][k & 7] = (f16)sE[pc][0];
                 pb[t][k >> 3][(k & 7) + 1] = (f16)sE[pc][1];
                 asm volatile("" : "+v"(la), "+v"(lb));
@@ -647,15 +625,10 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 asm volatile("" : "+v"(mX[pc][0]), "+v"(mX[pc][1]));
             };
             // (SCHED 4 without mask values: the accumulator times c IS the argument)
-            auto m1u = [&](const f32x16 (&st)[2], float (&us)[2][16], int pc, float nm) {
+            auto m1u = [&](const f32x16 (&st)[2], float (&us)[2][16], int pc) {
                 const int t = pc >> 3, k = 2 * (pc & 7);
-                if constexpr (LEAN2) {  // (chains from 0: the argument fma(s, c, -m))
-                    us[t][k] = fmaf(st[t][k], a.scale_log2, nm);
-                    us[t][k + 1] = fmaf(st[t][k + 1], a.scale_log2, nm);
-                } else {
-                    us[t][k] = st[t][k] * a.scale_log2;
-                    us[t][k + 1] = st[t][k + 1] * a.scale_log2;
-                }
+                us[t][k] = st[t][k] * a.scale_log2;
+                us[t][k + 1] = st[t][k + 1] * a.scale_log2;
                 asm volatile("" : "+v"(us[t][k]), "+v"(us[t][k + 1]));
             };
             auto m2 = [&](const u32x2 (&mk)[2][4], float (&us)[2][16], int pc) {
@@ -694,14 +667,12 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
 #pragma unroll
                         for (int k = 0; k < 16; k++) us[t][k] -= dlt;
                     }
+                    l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
                     m_run[rb] = m_new;
-                    if constexpr (!LEAN2) {  // (SCHED 5: l is rescaled with O; no chain start)
-                        l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
-                        const float nci = m_new == kNegInf ? 0.0f : -m_new / a.scale_log2;
+                    const float nci = m_new == kNegInf ? 0.0f : -m_new / a.scale_log2;
 #pragma unroll
-                        for (int j = 0; j < 16; j++) ci[rb][j] = nci;
-                        asm volatile("" : "+a"(ci[rb]));
-                    }
+                    for (int j = 0; j < 16; j++) ci[rb][j] = nci;
+                    asm volatile("" : "+a"(ci[rb]));
                 }
             };
             auto m3 = [&](const float (&us)[2][16], float& tmax, int pc) {
@@ -949,7 +920,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 }
                 // ---- A_j
                 const float nm0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
-                const float nmu1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];  // (SCHED 5: rb 1's -m for its arguments)
                 float la0 = l2[0].x, lb0 = l2[0].y, tmax1 = kNegInf;
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -980,21 +950,21 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                                   q1 = sched_inv<22, 15, 9>(i);
                         if (q3 >= 0) m3(us1, tmax1, q3);
                         if constexpr (LN && !MM) {
-                            if (q1 >= 0) m1u(s1, us1, q1, nmu1);
+                            if (q1 >= 0) m1u(s1, us1, q1);
                         } else {
                             if (q2 >= 0) m2(mk1, us1, q2);
                             if (q1 >= 0) m1(s1, q1);
                         }
                     }
                     if (i < 16) {
-                        if constexpr (LN && !LEAN2) {
+                        if constexpr (LN) {
                             s1[t] = mfma32(kr[t][kk], qop[1][kk], kk == 0 ? ci[1] : s1[t]);
                         } else {
                             if (kk == 0) s1[t] = f32x16{};
                             s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
                         }
                     } else {
-                        if constexpr (LN && !LEAN2) {
+                        if constexpr (LN) {
                             s0[t] = mfma32(kr[t][kk], qop[0][kk], kk == 0 ? ci[0] : s0[t]);
                         } else {
                             if (kk == 0) s0[t] = f32x16{};
@@ -1028,7 +998,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 // ---- B_j
                 PF4_T(3);
                 float tmax0 = kNegInf, nm1 = 0.0f, la1 = LN ? l2[1].x : 0.0f, lb1 = LN ? l2[1].y : 0.0f;
-                const float nmu0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];  // (SCHED 5: rb 0's -m for its arguments)
                 f16x8 p1n[2][2];
                 const bool mskip = MM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
                 PF4_T(4);
@@ -1062,7 +1031,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                         }
                         if (m3p >= 0) m3(us0, tmax0, m3p);
                         if constexpr (LN && !MM) {
-                            if (m1p >= 0) m1u(s0, us0, m1p, nmu0);
+                            if (m1p >= 0) m1u(s0, us0, m1p);
                         } else {
                             if (m2p >= 0) m2(mk0, us0, m2p);
                             if (m1p >= 0) m1(s0, m1p);
@@ -1077,10 +1046,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                         if (!(i & 1) && i < 24) v_read1((i >> 1) + 4);
                         const int t = i >> 4, q = (i >> 3) & 1, db = (i >> 1) & 3, rb = i & 1;
                         o[rb][db] = mfma32(va[t][q][db], rb ? p1[t][q] : p0[t][q], o[rb][db]);
-                        // (SCHED 5: row block rb's sums of this (t, q) P^T fragment, once per fragment)
-                        if constexpr (LN && LEAN2) {
-                            if (db == NDB - 1) lacc[rb] = mfma32(ones, rb ? p1[t][q] : p0[t][q], lacc[rb]);
-                        }
                     }
                     if (!kDiagNoDma && i < 16 && (i & 3) == 1) k_piece_at(j + 3, r0, i >> 2);
                     if (!kDiagNoDma && i >= 16 && (i & 1)) m_piece(j + 2, (i - 16) >> 1, mskip);
@@ -1133,17 +1098,6 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     sexp(0, 1, us0, p0, LN);
                     __syncthreads();  // every wave's pieces of V nt-1 landed
                     pv2(nt - 1, p0, p1);
-                    if constexpr (LN && LEAN2) {
-#pragma unroll
-                        for (int t = 0; t < 2; t++) {
-#pragma unroll
-                            for (int q = 0; q < 2; q++) {
-                                lacc[0] = mfma32(ones, p0[t][q], lacc[0]);
-                                lacc[1] = mfma32(ones, p1[t][q], lacc[1]);
-                            }
-                        }
-                        lean2_used = true;
-                    }
                 }
             } else {
             if (nt > 0) iter(0, std::true_type());
@@ -1183,9 +1137,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
     float* park = (float*)smem + wave * (kPf4RowsW * kStride);
 #pragma unroll
     for (int rb = 0; rb < 2; rb++) {
-        // (SCHED 5 in a body without mask values: l from the MFMA row sums, every
-        // register of the lane holding its row's)
-        const float l_tot = lean2_used ? lacc[rb][0] : PF4_XOR32(l2[rb].x + l2[rb].y, false);
+        const float l_tot = PF4_XOR32(l2[rb].x + l2[rb].y, false);
         const float inv = 1.0f / l_tot;  // fully masked row -> NaN like the reference
         float* pk = park + (32 * rb + c32) * kStride + 4 * h;
 #pragma unroll

@@ -287,13 +287,12 @@ def test_pf_form_option():
     p = _params(NQ=4096, kt=fattn.TYPE_F16)
     assert "fattn_pf4_kernel(lean)<f16,D128" in fattn.describe(p)
     want = {1: "fattn_pf_kernel<f16,D128", 4: "fattn_pf4_kernel(pipelined)<f16,D128",
-            5: "fattn_pf4_kernel(balanced)<f16,D128", 6: "fattn_pf4_kernel(lean)<f16,D128",
-            7: "fattn_pf4_kernel(lean2)<f16,D128"}
+            5: "fattn_pf4_kernel(balanced)<f16,D128", 6: "fattn_pf4_kernel(lean)<f16,D128"}
     for form, name in want.items():
         with fattn.options({fattn.OPT_PF_FORM: form}):
             assert name in fattn.describe(p), (form, fattn.describe(p))
     assert "fattn_pf_kernel<f16,D64" in fattn.describe(_params(NQ=4096, D=64, kt=fattn.TYPE_F16))
-    for bad in (2, 3, 8):
+    for bad in (2, 3, 7):
         with pytest.raises(Exception):
             with fattn.options({fattn.OPT_PF_FORM: bad}):
                 pass

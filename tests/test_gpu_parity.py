@@ -664,14 +664,14 @@ def test_wave_merge_fully_masked_is_nan(dev):
 # 256-row workgroups over 64-key tiles (32x32 MFMA); auto-selected when the
 # workgroups fill the chip, forced here (OPT_PF = 2) on small problems.
 
-@pytest.fixture(params=[(0, 1), (1, 1), (0, 4), (0, 5), (0, 6), (0, 7)],
-                ids=["staged", "inkernel_deq", "staged_pf4p", "staged_pf4b", "staged_pf4l", "staged_pf4l2"])
+@pytest.fixture(params=[(0, 1), (1, 1), (0, 4), (0, 5), (0, 6)],
+                ids=["staged", "inkernel_deq", "staged_pf4p", "staged_pf4b", "staged_pf4l"])
 def pf_force(request):
     """The prefill kernels on every eligible problem: Q8_0 / Q4_0 K/V staged
     to f16 first (the default) or dequantised inside the kernel
     (FATTN_OPT_PF_STAGE = 1); the f16 body in its 8-wave form (fattn_pf.h)
     or one wave per SIMD (fattn_pf4.h, D = 128; FATTN_OPT_PF_FORM = the
-    pipelined 4, the balanced 5, the lean 6 and the lean2 7)."""
+    pipelined 4 and the balanced 5)."""
     stage, form = request.param
     fattn.set_option(fattn.OPT_PF, 2)
     fattn.set_option(fattn.OPT_PF_STAGE, stage)
@@ -702,14 +702,13 @@ def test_pf4_bit_identical_to_pf(dev, case):
     outs = {}
     fattn.set_option(fattn.OPT_PF, 2)
     try:
-        for form in (1, 4, 5, 6, 7):
+        for form in (1, 4, 5, 6):
             fattn.set_option(fattn.OPT_PF_FORM, form)
             t = upload(p)
             att = fattn.Attention(*views(p, t), t["dst"], p.scale)
             assert ("fattn_pf4_kernel" in att.describe()) == (form >= 4), att.describe()
             assert ("(pipelined)" in att.describe()) == (form == 4), att.describe()
             assert ("(lean)" in att.describe()) == (form == 6), att.describe()
-            assert ("(lean2)" in att.describe()) == (form == 7), att.describe()
             assert ("(balanced)" in att.describe()) == (form == 5), att.describe()
             att()
             outs[form] = t["dst"].cpu().numpy()
@@ -723,10 +722,6 @@ def test_pf4_bit_identical_to_pf(dev, case):
     assert np.array_equal(np.isnan(outs[6]), np.isnan(outs[1]))
     assert attn_rel_err(outs[6], p.oracle()) <= RTOL
     assert attn_elem_err(outs[6], p.oracle()) <= 1.0
-    # lean2 (chains from 0, row sums of the f16 P by MFMA) likewise
-    assert np.array_equal(np.isnan(outs[7]), np.isnan(outs[1]))
-    assert attn_rel_err(outs[7], p.oracle()) <= RTOL
-    assert attn_elem_err(outs[7], p.oracle()) <= 1.0
     assert np.array_equal(outs[1], outs[5], equal_nan=True)
     assert attn_rel_err(outs[4], p.oracle()) <= RTOL
 
