@@ -173,4 +173,12 @@ pass_r() {
 pass_s() {
   run err_part 300 python -u tools/err_part.py
 }
+# Twentieth pass (reverted change): lean2 (PF_FORM 7: chains from 0, row sums
+# by MFMA) -- the prefill parity suite (every form), then same-box A/B against
+# lean (6).
+pass_t() {
+  run t_t 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "pf or prefill"
+  run ab_l2_q8z 400 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 6 --variant lean:PF_FORM=6 --variant lean2:PF_FORM=7
+  run ab_l2_f16 400 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 6 --variant lean:PF_FORM=6 --variant lean2:PF_FORM=7
+}
 "$@"
