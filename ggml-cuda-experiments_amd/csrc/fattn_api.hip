@@ -328,6 +328,7 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     a.chunk_len = (int)(tpc * kStep);
     a.n_chunks = (int)nch;
     a.merge_launch = (nch > 1 && !fused) ? 1 : 0;
+    a.part_f16 = part_f16_ok(a.merge_launch, pl.D) && g_opt_part_f16 == 2 ? 1 : 0;  // (multi-query: on request)
     a.ncp = 1;
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     a.nbuf = 0;
@@ -858,7 +859,7 @@ int fattn_describe(const fattn_params* p, char* out, size_t cap) {
                       pl.a.merge_launch == 1 ? (pl.a.part_f16 ? " + fattn_bd_merge_kernel(f16 partials)" : pl.merge_plain ? " + fattn_bd_merge_kernel(plain)" : " + fattn_bd_merge_kernel") : pl.a.merge_launch == 2 ? " (in-kernel merge)" : "");
     else if (pl.mq)
         std::snprintf(kern, sizeof kern, "fattn_mq_kernel<%s,D%d,%dwaves,%s>%s", tn(pl.kt), pl.D, pl.nw, hm,
-                      pl.a.merge_launch ? " + fattn_mq_merge_kernel" : "");
+                      pl.a.merge_launch ? (pl.a.part_f16 ? " + fattn_mq_merge_kernel(f16 partials)" : " + fattn_mq_merge_kernel") : "");
     else
         std::snprintf(kern, sizeof kern, "%s<%s,%s,D%d,gran%d,%s,%dwaves%s>%s%s",
                       pl.nld ? "fattn_split_ld_kernel" : "fattn_split_kernel", tn(pl.kt), tn(pl.vt),

@@ -191,10 +191,23 @@ int launch_mq_hm(const Plan& pl, hipStream_t st, const Events& ev) {
             constexpr int SUBS = NW == 8 ? 16 : 4;
             const dim3 g(kRows / 4, pl.grid.y * SUBS, pl.grid.z);
             const int need = (pl.a.n_chunks + merge_ppr<D>() - 1) / merge_ppr<D>();
-            if (need <= 2) hipLaunchKernelGGL((fattn_mq_merge_kernel<D, 2, SUBS>), g, dim3(256), 0, st, pl.a);
-            else if (need <= 4) hipLaunchKernelGGL((fattn_mq_merge_kernel<D, 4, SUBS>), g, dim3(256), 0, st, pl.a);
-            else if (need <= 8) hipLaunchKernelGGL((fattn_mq_merge_kernel<D, 8, SUBS>), g, dim3(256), 0, st, pl.a);
-            else hipLaunchKernelGGL((fattn_mq_merge_kernel<D, 16, SUBS>), g, dim3(256), 0, st, pl.a);
+            auto go = [&](auto kit, auto f16) {
+                hipLaunchKernelGGL((fattn_mq_merge_kernel<D, decltype(kit)::value, SUBS, decltype(f16)::value>), g,
+                                   dim3(256), 0, st, pl.a);
+            };
+            auto pick = [&](int nd, auto f16) {
+                if (nd <= 2) go(std::integral_constant<int, 2>(), f16);
+                else if (nd <= 4) go(std::integral_constant<int, 4>(), f16);
+                else if (nd <= 8) go(std::integral_constant<int, 8>(), f16);
+                else go(std::integral_constant<int, 16>(), f16);
+            };
+            if constexpr (D != 64) {
+                if (pl.a.part_f16) {
+                    pick((pl.a.n_chunks + merge_ppr_h<D>() - 1) / merge_ppr_h<D>(), std::true_type());
+                    return;
+                }
+            }
+            pick(need, std::false_type());
         }
     });
 }

@@ -438,8 +438,19 @@ __global__ __launch_bounds__(NW * kWave, NW == 8 ? 1 : 2) void fattn_mq_kernel(c
 #pragma unroll
         for (int gi = 0; gi < NG; gi++) {
             const int64_t slot = ((tile * SUBS + wave * NG + gi) * a.n_chunks + chunk) * kRows + i16;
+            if (a.part_f16) {  // (SplitArgs::part_f16: O / l in f16, 8 B per 4 dims)
+                const float inv = l_tot[gi] > 0.0f ? 1.0f / l_tot[gi] : 0.0f;
 #pragma unroll
-            for (int c = 0; c < NC; c++) *(f32x4*)(a.ws_o + slot * D + 16 * c + 4 * g) = o[gi][c];
+                for (int c = 0; c < NC; c++) {
+                    const f16x2 lo = {(_Float16)(o[gi][c][0] * inv), (_Float16)(o[gi][c][1] * inv)};
+                    const f16x2 hi = {(_Float16)(o[gi][c][2] * inv), (_Float16)(o[gi][c][3] * inv)};
+                    *(u32x2*)((uint16_t*)a.ws_o + slot * D + 16 * c + 4 * g) =
+                        u32x2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < NC; c++) *(f32x4*)(a.ws_o + slot * D + 16 * c + 4 * g) = o[gi][c];
+            }
             if (g == 0) *(f32x2*)(a.ws_ml + 2 * slot) = f32x2{m_run[gi], l_tot[gi]};
         }
         return;
@@ -483,7 +494,7 @@ __global__ __launch_bounds__(NW * kWave, NW == 8 ? 1 : 2) void fattn_mq_kernel(c
 // in fp32, fixed order) and writes the normalised dst row.  grid.y runs over
 // (tile, subtile) pairs, y' = tile_y * SUBS + sub, so the partial slots are
 // the multi-query kernel's ((tile * SUBS + sub) * chunks + chunk) * 16 + row.
-template <int D, int KIT, int SUBS>
+template <int D, int KIT, int SUBS, bool F16 = false>  // F16: the f16 partials of SplitArgs::part_f16
 __global__ __launch_bounds__(256) void fattn_mq_merge_kernel(const SplitArgs a) {
     const int lane = threadIdx.x & 63;
     const int tm = blockIdx.x * 4 + (threadIdx.x >> 6);  // row of the subtile
@@ -499,7 +510,12 @@ __global__ __launch_bounds__(256) void fattn_mq_merge_kernel(const SplitArgs a) 
     const int64_t slot0 = ((int64_t)iq3 * gridDim.y + ys) * a.n_chunks * kRows + tm;  // chunk 0's row
     const int rq = div_R(a, p);
     float* out = a.dst + (((int64_t)iq3 * a.NQ + qt * a.QPT + rq) * a.H + ik2 * a.rk2 + (p - rq * a.R)) * D;
-    merge_row_parts<D, KIT>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kRows * D, 2 * kRows);
+    if constexpr (F16) {
+        merge_row_parts_h<D, KIT>((const uint16_t*)a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane,
+                                  kRows * D, 2 * kRows);
+    } else {
+        merge_row_parts<D, KIT>(a.ws_o + slot0 * D, a.ws_ml + 2 * slot0, a.n_chunks, out, lane, kRows * D, 2 * kRows);
+    }
 }
 
 }  // namespace fattn

@@ -241,6 +241,26 @@ def test_mq_d256(dev, mq_on, case):
     assert attn_elem_err(got, ref) <= 1.0
 
 
+@pytest.mark.parametrize("case", [
+    dict(D=256, kv_type="q4_0", NQ=64, H=8, Hkv=2, N=1024, mask="random"),   # R = 4, KV split + merge launch
+    dict(D=256, kv_type="q8_0", NQ=64, H=4, Hkv=4, N=2048, mask="neginf_blocks"),
+    dict(D=128, kv_type="q8_0", NQ=48, H=8, Hkv=2, N=1024, extreme=True),
+], ids=["d256_q4_gqa", "d256_q8_neginf", "d128_extreme"])
+def test_mq_f16_partials(dev, mq_on, case):
+    """The multi-query kernel's second-launch merge over f16 chunk partials
+    (FATTN_OPT_PART_F16 = 2; off by default for this kernel), chunked so the
+    merge runs: against the oracle."""
+    p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000 + 7, **case)
+    with fattn.options({fattn.OPT_PART_F16: 2}):
+        t = upload(p, dev)
+        d = fattn.Attention(*views(p, t), t["dst"], p.scale, kv_chunk=256).describe()
+        assert "fattn_mq_merge_kernel(f16 partials)" in d, d
+        got = run_gpu(p, kv_chunk=256)
+    ref = p.oracle()
+    assert attn_rel_err(got, ref) <= RTOL
+    assert attn_elem_err(got, ref) <= 1.0
+
+
 @pytest.fixture
 def rpw64():
     """Force the 256-row workgroups (8 waves x 32 rows) on small problems."""

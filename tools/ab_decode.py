@@ -27,6 +27,7 @@ SHAPES = {
     "config5_s8": dict(kv_type="q8_0", H=4, Hkv=4, N=4096, NQ=64, D=128),
     "config5_s4": dict(kv_type="q8_0", H=8, Hkv=8, N=4096, NQ=64, D=128),
     "config5_s2": dict(kv_type="q8_0", H=16, Hkv=16, N=4096, NQ=64, D=128),
+    "config5_d256": dict(kv_type="q8_0", H=32, Hkv=32, N=4096, NQ=64, D=256),
 }
 
 

@@ -181,4 +181,10 @@ pass_t() {
   run ab_l2_q8z 400 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 6 --variant lean:PF_FORM=6 --variant lean2:PF_FORM=7
   run ab_l2_f16 400 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 6 --variant lean:PF_FORM=6 --variant lean2:PF_FORM=7
 }
+# Twenty-first pass: f16 partials for the multi-query merge (D = 256) --
+# parity, then same-box A/B on the config-5 shape at D = 256.
+pass_u() {
+  run t_u 600 python -u -m pytest tests/test_gpu_parity.py -q --timeout 300 --timeout-method thread -m gpu -k "mq"
+  run ab_mq16 300 python -u tools/ab_decode.py --workload config5_d256 --rounds 6 --variant f32: --variant f16:PART_F16=2
+}
 "$@"
