@@ -328,7 +328,8 @@ int size_mq(Plan& pl, int kv_chunk, int64_t Y, int64_t S, int64_t N) {
     a.chunk_len = (int)(tpc * kStep);
     a.n_chunks = (int)nch;
     a.merge_launch = (nch > 1 && !fused) ? 1 : 0;
-    a.part_f16 = part_f16_ok(a.merge_launch, pl.D) && g_opt_part_f16 == 2 ? 1 : 0;  // (multi-query: on request)
+    // (f16 partials: the config-5 shape at D = 256 55.14 -> 50.82 us, profiles/r06_p)
+    a.part_f16 = part_f16_ok(a.merge_launch, pl.D) ? 1 : 0;
     a.ncp = 1;
     while (a.ncp < a.n_chunks) a.ncp <<= 1;
     a.nbuf = 0;
@@ -648,7 +649,7 @@ int make_plan(const fattn_params* p, Plan& pl) {
         // 0-4 % faster than the 8-wave body on f16 rows, 12-21 % on staged Q8_0
         // with the zero mask and 1-3 % faster than the pipelined form 4
         // (profiles/r05_h, r05_p); the lean form's chains started from -m / c
-        // take 1.5 % (f16) to 3.6 % (Q8_0 zero mask) off it, profiles/r06_e;
+        // take 1.5 % (f16) to 3.6 % (Q8_0 zero mask) off it, profiles/r06_c;
         // form 1 keeps the 8-wave body)
         const int form = g_opt_pf_form == 0 ? 6 : (int)g_opt_pf_form;
         pl.pf4 = pl.kt == FATTN_TYPE_F16 && D == 128 && form >= 4;

@@ -98,9 +98,9 @@ enum {
                                        R q heads packed in one split tile (second-launch merge), 2 = one q head
                                        per tile (one-row tiles, merged in the launch; K/V read R times) */
     FATTN_OPT_PART_F16 = 32,        /* chunk partials of the second-launch merges (multi-row split tiles, batched
-                                       decode; D != 64): 0 = auto (f16 for batched decode and for split tiles of 8+
-                                       rows), 1 = f32 (O unnormalised), 2 = f16 (O / l in f16 beside (m, l) in
-                                       f32: half the partial bytes) */
+                                       decode, multi-query; D != 64): 0 = auto (f16 for batched decode, multi-query
+                                       and split tiles of 8+ rows), 1 = f32 (O unnormalised), 2 = f16 (O / l in
+                                       f16 beside (m, l) in f32: half the partial bytes) */
     FATTN_OPT_MERGE_PLAIN = 31,     /* second-launch merges of multi-row split / batched-decode plans
                                        (fattn_merge_kernel, fattn_bd_merge_kernel): 0 = auto (sc1 loads), 1 = sc1
                                        loads, 2 = plain loads (the kernel boundary already orders the partials) */

@@ -248,8 +248,8 @@ def test_mq_d256(dev, mq_on, case):
 ], ids=["d256_q4_gqa", "d256_q8_neginf", "d128_extreme"])
 def test_mq_f16_partials(dev, mq_on, case):
     """The multi-query kernel's second-launch merge over f16 chunk partials
-    (FATTN_OPT_PART_F16 = 2; off by default for this kernel), chunked so the
-    merge runs: against the oracle."""
+    (FATTN_OPT_PART_F16 = 2, the default's choice too), chunked so the merge
+    runs: against the oracle."""
     p = make_problem(seed=zlib.crc32(str(sorted(case.items())).encode()) % 1000 + 7, **case)
     with fattn.options({fattn.OPT_PART_F16: 2}):
         t = upload(p, dev)
