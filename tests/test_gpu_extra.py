@@ -514,7 +514,9 @@ def test_row_merge_graph_replays_new_inputs(dev, xcd):
     dict(D=128, NQ=64, H=16, N=4096, kv_type="q8_0"),                 # its 2-rank shard
     dict(D=128, NQ=40, H=32, Hkv=8, N=4096, kv_type="q4_0", mask="causal"),  # GQA, partial row tile, causal
     dict(D=128, NQ=64, H=8, N=8192, kv_type="q8_0", mask="tail"),     # whole chunks -inf
-], ids=["cfg5", "cfg5_h16", "gqa_causal", "tail"])
+    dict(D=96, NQ=64, H=32, N=4096, kv_type="q8_0"),                  # role form at D = 96: 12 dims a thread (8-B f16 stores)
+    dict(D=64, NQ=64, H=32, N=4096, kv_type="q4_0"),                  # D = 64: f32 partials always
+], ids=["cfg5", "cfg5_h16", "gqa_causal", "tail", "d96", "d64"])
 def test_bd_chunk_merge_forms(dev, in_kernel, case):
     """The batched-decode kernel over several KV chunks: the partials merge in
     the second launch (default) or inside the launch (FATTN_OPT_MERGE_IN_KERNEL:
@@ -537,11 +539,13 @@ def test_bd_chunk_merge_forms(dev, in_kernel, case):
             assert desc.startswith(("fattn_bd_kernel", "fattn_bdp_kernel")), desc
             g = [int(x) for x in desc.split("grid(")[1].split(")")[0].split(",")]
             cus = torch.cuda.get_device_properties(dev).multi_processor_count
-            resident = g[0] * g[1] * g[2] <= cus  # one batched-decode workgroup per CU
+            lds = int(desc.split(" lds ")[1].split()[0])
+            resident = g[0] * g[1] * g[2] <= cus * max(1, 163840 // lds)  # (the planner's rule: workgroups a CU's LDS holds)
             assert ("in-kernel" in desc) == (in_kernel == 1 and resident), desc
             assert ("merge_kernel(plain)" in desc) == (in_kernel == 2 and "merge_kernel" in desc), desc
             # (in_kernel 1 on a grid that is not co-resident: the second launch, auto = f16)
-            assert ("merge_kernel(f16 partials)" in desc) == (in_kernel in (0, 1) and "merge_kernel" in desc), desc
+            assert ("merge_kernel(f16 partials)" in desc) == (in_kernel in (0, 1) and "merge_kernel" in desc
+                                                               and case["D"] != 64), desc
             t["dst"].fill_(float("nan"))
             att()
             torch.cuda.synchronize()
@@ -574,7 +578,8 @@ def test_bd_in_kernel_merge_graph_replays_new_inputs(dev):
     dict(D=64, NQ=8, H=16, Hkv=4, N=4096, kv_type="q8_0"),
     dict(D=96, NQ=4, H=16, Hkv=4, N=4096, kv_type="q8_0"),
     dict(D=256, NQ=4, H=8, Hkv=2, N=2048, kv_type="f16"),
-], ids=["cfg4", "cfg5_shard", "tail", "d64", "d96", "d256"])
+    dict(D=80, NQ=4, H=16, Hkv=4, N=2048, kv_type="f16"),             # D = 80: 10 lanes a part (f16 merge)
+], ids=["cfg4", "cfg5_shard", "tail", "d64", "d96", "d256", "d80"])
 def test_split_multirow_merge_forms(dev, in_kernel, case):
     """Multi-row split tiles over 4+ KV chunks: the partials merge one wave per
     (tile, row), inside the launch (the tile's workgroups wait for each other)

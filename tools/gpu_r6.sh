@@ -187,4 +187,8 @@ pass_u() {
   run t_u 600 python -u -m pytest tests/test_gpu_parity.py -q --timeout 300 --timeout-method thread -m gpu -k "mq"
   run ab_mq16 300 python -u tools/ab_decode.py --workload config5_d256 --rounds 6 --variant f32: --variant f16:PART_F16=2
 }
+# Twenty-second pass: the merge forms at D = 64 / 80 / 96 (f16 partial paths).
+pass_v() {
+  run t_v 600 python -u -m pytest tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "merge_forms"
+}
 "$@"
