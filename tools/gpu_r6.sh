@@ -191,4 +191,16 @@ pass_u() {
 pass_v() {
   run t_v 600 python -u -m pytest tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "merge_forms"
 }
+# Twenty-third pass (reverted change): the prefill bodies without mask values issuing K 0-2
+# before Q's loads -- prefill parity, then processes alternating libfattn.so
+# and the previous tree's libfattn_prev.so.
+pass_w() {
+  run t_w 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "pf or prefill"
+  for r in 1 2 3; do
+    for L in libfattn.so libfattn_prev.so; do
+      FATTN_LIB=$L run ab_w_z_${L%.so}_$r 200 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 2 --variant $L:
+      FATTN_LIB=$L run ab_w_f_${L%.so}_$r 200 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 2 --variant $L:
+    done
+  done
+}
 "$@"
