@@ -109,6 +109,27 @@ __device__ __forceinline__ void scale_acc16(f32x16& o, float alpha) {
           "=&v"(t)
         : "v"(alpha));
 }
+// S^T chain steps of the lean body with the accumulator in VGPRs and Q^T's
+// operand in AGPRs: hipcc puts every MFMA's accumulator of a 512-register
+// kernel in AGPRs, so each score cost a v_accvgpr_read beside its multiply
+// (64 of the tile's ~380 vector instructions).  Q^T is loop-invariant and an
+// MFMA takes srcB from AGPRs, so the two swap files; the chain starts from 0
+// and the row's -m enters the exponent argument's fma.  Wait states hipcc
+// cannot see (its hazard pass knows only its own MFMAs): the accumulator ->
+// first VALU read (an 8-pass XDL write: 12 states) and Q^T's v_accvgpr_write
+// -> MFMA read, checked on the .s by tools/isa_hazard_check.py (xdl-vgpr).
+#ifndef FATTN_PF4_SAGPR
+#define FATTN_PF4_SVGPR 1
+#else
+#define FATTN_PF4_SVGPR 0
+#endif
+__device__ __forceinline__ void mfma_s_first(f32x16& d, const f16x8& k, const f16x8& q) {
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(d) : "v"(k), "a"(q));
+}
+__device__ __forceinline__ void mfma_s_next(f32x16& d, const f16x8& k, const f16x8& q) {
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(k), "a"(q));
+}
+
 // registers through an empty volatile asm: code that reads them cannot move
 // above the asm (pins a phase's VALU below the branches at its start)
 __device__ __forceinline__ void pin16(float (&x)[16]) {
@@ -278,6 +299,17 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
             }
         }
     }
+    if constexpr (LEAN && FATTN_PF4_SVGPR) {
+        // (Q^T into AGPRs once, where the lean chains take it as srcB: from
+        // VGPRs hipcc copied it there before every MFMA, 64 v_accvgpr_write a tile)
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++) {
+#pragma unroll
+            for (int kk = 0; kk < NK; kk++) asm volatile("" : "+a"(qop[rb][kk]));
+        }
+        // (the accumulator-write -> MFMA-read wait states of those writes)
+        asm volatile("s_nop 4");
+    }
 
     // ---- DMA source offsets (tile-relative; + n0 * nb1 per tile): piece
     // j = wave + 4i of the K image and of the V image, laid out as the image
@@ -357,7 +389,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
         for (int j = 0; j < 16; j++) ci[rb][j] = 0.0f;
         // (held in AGPRs, where the MFMAs take it as srcC: from VGPRs hipcc
         // copied it to AGPRs before every chain, 32 v_accvgpr_write a tile)
-        if constexpr (SCHED == 4) asm volatile("" : "+a"(ci[rb]));
+        if constexpr (SCHED == 4 && !FATTN_PF4_SVGPR) asm volatile("" : "+a"(ci[rb]));
     }
 
     // mask values of row block rb for tile s (a +-0 block's slot holds the
@@ -625,10 +657,16 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 asm volatile("" : "+v"(mX[pc][0]), "+v"(mX[pc][1]));
             };
             // (SCHED 4 without mask values: the accumulator times c IS the argument)
-            auto m1u = [&](const f32x16 (&st)[2], float (&us)[2][16], int pc) {
+            auto m1u = [&](const f32x16 (&st)[2], float (&us)[2][16], float nr, int pc) {
                 const int t = pc >> 3, k = 2 * (pc & 7);
+#if FATTN_PF4_SVGPR
+                us[t][k] = fmaf(st[t][k], a.scale_log2, nr);
+                us[t][k + 1] = fmaf(st[t][k + 1], a.scale_log2, nr);
+#else
+                (void)nr;
                 us[t][k] = st[t][k] * a.scale_log2;
                 us[t][k + 1] = st[t][k + 1] * a.scale_log2;
+#endif
                 asm volatile("" : "+v"(us[t][k]), "+v"(us[t][k + 1]));
             };
             auto m2 = [&](const u32x2 (&mk)[2][4], float (&us)[2][16], int pc) {
@@ -670,9 +708,13 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                     l2[rb] = f32x2{l2[rb].x * alpha, l2[rb].y * alpha};
                     m_run[rb] = m_new;
                     const float nci = m_new == kNegInf ? 0.0f : -m_new / a.scale_log2;
+                    if constexpr (!FATTN_PF4_SVGPR) {
 #pragma unroll
-                    for (int j = 0; j < 16; j++) ci[rb][j] = nci;
-                    asm volatile("" : "+a"(ci[rb]));
+                        for (int j = 0; j < 16; j++) ci[rb][j] = nci;
+                        asm volatile("" : "+a"(ci[rb]));
+                    } else {
+                        (void)nci;
+                    }
                 }
             };
             auto m3 = [&](const float (&us)[2][16], float& tmax, int pc) {
@@ -920,6 +962,8 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 }
                 // ---- A_j
                 const float nm0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
+                // (lean, accumulators in VGPRs: rb 1's -m_ref for its arguments of tile j)
+                const float nr1 = (m_run[1] == kNegInf) ? 0.0f : -m_run[1];
                 float la0 = l2[0].x, lb0 = l2[0].y, tmax1 = kNegInf;
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -950,21 +994,31 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                                   q1 = sched_inv<22, 15, 9>(i);
                         if (q3 >= 0) m3(us1, tmax1, q3);
                         if constexpr (LN && !MM) {
-                            if (q1 >= 0) m1u(s1, us1, q1);
+                            // (the first tile's step 9 reads s1[0] two steps after its
+                            // chain's last MFMA with no exponentials between: the
+                            // remaining accumulator -> VALU wait states)
+                            if (F && FATTN_PF4_SVGPR && i == 9) asm volatile("s_nop 3" : "+v"(s1[0]));
+                            if (q1 >= 0) m1u(s1, us1, nr1, q1);
                         } else {
                             if (q2 >= 0) m2(mk1, us1, q2);
                             if (q1 >= 0) m1(s1, q1);
                         }
                     }
                     if (i < 16) {
-                        if constexpr (LN) {
+                        if constexpr (LN && FATTN_PF4_SVGPR) {
+                            if (kk == 0) mfma_s_first(s1[t], kr[t][kk], qop[1][kk]);
+                            else mfma_s_next(s1[t], kr[t][kk], qop[1][kk]);
+                        } else if constexpr (LN) {
                             s1[t] = mfma32(kr[t][kk], qop[1][kk], kk == 0 ? ci[1] : s1[t]);
                         } else {
                             if (kk == 0) s1[t] = f32x16{};
                             s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
                         }
                     } else {
-                        if constexpr (LN) {
+                        if constexpr (LN && FATTN_PF4_SVGPR) {
+                            if (kk == 0) mfma_s_first(s0[t], kr[t][kk], qop[0][kk]);
+                            else mfma_s_next(s0[t], kr[t][kk], qop[0][kk]);
+                        } else if constexpr (LN) {
                             s0[t] = mfma32(kr[t][kk], qop[0][kk], kk == 0 ? ci[0] : s0[t]);
                         } else {
                             if (kk == 0) s0[t] = f32x16{};
@@ -998,6 +1052,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 // ---- B_j
                 PF4_T(3);
                 float tmax0 = kNegInf, nm1 = 0.0f, la1 = LN ? l2[1].x : 0.0f, lb1 = LN ? l2[1].y : 0.0f;
+                const float nr0 = (m_run[0] == kNegInf) ? 0.0f : -m_run[0];
                 f16x8 p1n[2][2];
                 const bool mskip = MM ? __builtin_amdgcn_readfirstlane(m_skip(j + 2) ? 1 : 0) != 0 : true;
                 PF4_T(4);
@@ -1031,7 +1086,7 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                         }
                         if (m3p >= 0) m3(us0, tmax0, m3p);
                         if constexpr (LN && !MM) {
-                            if (m1p >= 0) m1u(s0, us0, m1p);
+                            if (m1p >= 0) m1u(s0, us0, nr0, m1p);
                         } else {
                             if (m2p >= 0) m2(mk0, us0, m2p);
                             if (m1p >= 0) m1(s0, m1p);

@@ -203,4 +203,26 @@ pass_w() {
     done
   done
 }
+# Twenty-fourth pass: the lean body's S^T chains as asm MFMAs into VGPRs with
+# Q^T's operands in AGPRs (no accumulator reads) -- prefill parity, then
+# processes alternating libfattn.so and the previous tree's libfattn_prev.so.
+pass_x() {
+  run t_x 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "pf or prefill"
+  for r in 1 2 3; do
+    for L in libfattn.so libfattn_prev.so; do
+      FATTN_LIB=$L run ab_x_z_${L%.so}_$r 200 python -u tools/ab_prefill.py --kv q8_0 --mask zero --rounds 2 --variant $L:
+      FATTN_LIB=$L run ab_x_f_${L%.so}_$r 200 python -u tools/ab_prefill.py --kv f16 --mask none --rounds 2 --variant $L:
+    done
+  done
+}
+# Twenty-fifth pass: the same change in the stamps build (cycles per tile,
+# both lean bodies), new form against FATTN_PF4_SAGPR (the committed one).
+pass_y() {
+  for r in 1 2; do
+    for L in libfattn_stnew.so libfattn_stold.so; do
+      FATTN_LIB=$L run st_y_z_${L%.so}_$r 200 python -u tools/pf_stamps.py --kv-type q8_0 --mask-zero
+      FATTN_LIB=$L run st_y_f_${L%.so}_$r 200 python -u tools/pf_stamps.py --kv-type f16 --no-mask
+    done
+  done
+}
 "$@"

@@ -316,10 +316,16 @@ def aregs(text: str) -> set[int]:
 
 def xdl_waits(mnem: str) -> int:
     """Wait states a VALU read (v_accvgpr_read included) of an XDL MFMA's result
-    needs on gfx950: the MFMA's passes + 3 (2-pass 5, 4-pass 7, 8-pass 11,
-    16-pass 19; LLVM's GCNHazardRecognizer, the XDL-write -> VALU-read rows).
-    Passes from the shape: 32x32 16, 16x16 8, 4x4 4 -- the larger form of each
-    (conservative: 32x32x16 f16 is 8 passes on gfx950)."""
+    needs on gfx950: the pads hipcc itself places after a builtin MFMA read by
+    the next VALU (32x32x16 f16 / bf16 12 states, 16x16x32 8: measured on
+    hipcc's gfx950 output); other shapes by their passes + 3, the larger form
+    of each (32x32 16 passes, 16x16 8, 4x4 4)."""
+    # gfx950's own pads (hipcc on a builtin MFMA read by the next VALU):
+    # 32x32x16 f16 / bf16 s_nop 11, 16x16x32 f16 / bf16 s_nop 7
+    if re.search(r"32x32x16_(f16|bf16)$", mnem):
+        return 12
+    if re.search(r"16x16x32_(f16|bf16)$", mnem):
+        return 8
     if "32x32" in mnem:
         return 19
     if "16x16" in mnem:
@@ -327,11 +333,22 @@ def xdl_waits(mnem: str) -> int:
     return 7
 
 
+def accumulate_chain(prod: Insn, cons: Insn) -> bool:
+    """cons is the next step of prod's accumulate chain: the same MFMA taking
+    prod's whole destination as srcC and writing it back (0 wait states)."""
+    if cons.mnem != prod.mnem:
+        return False
+    po = [o.strip() for o in prod.ops.split(",")]
+    co = [o.strip() for o in cons.ops.split(",")]
+    return len(po) >= 4 and len(co) >= 4 and co[0] == po[0] and co[3] == po[0]
+
+
 def check_xdl_asm_reads(name, body, horizon=40):
-    """XDL MFMA result -> an asm instruction reading it (round-6 advisor item):
-    hipcc pads the wait states of its own VALU reads of an MFMA's result, not
-    those of an asm statement's (fattn_pf4.h's scale_acc16 reads O's AGPRs in
-    the rare rescale branch, behind a hand-placed s_nop pad).  Every path from
+    """XDL MFMA result -> an asm instruction reading it (round-6 advisor item),
+    or an asm MFMA's result -> any vector reader: hipcc pads the wait states of
+    its own VALU reads of its own MFMAs' results only (fattn_pf4.h's scale_acc16
+    reads O's AGPRs in the rare rescale branch, behind a hand-placed s_nop pad;
+    the lean body's S^T chains are asm MFMAs into VGPRs that hipcc's code reads).  Every path from
     each MFMA, through branches, up to `horizon` instructions or a
     redefinition, is walked; an asm instruction that names one of the MFMA's
     destination registers before the wait states have passed is a finding."""
@@ -359,7 +376,10 @@ def check_xdl_asm_reads(name, body, horizon=40):
                     if waits >= need or steps >= horizon:
                         stopped = True
                         break
-                    if cons.in_asm and cons.mnem.startswith("v_"):
+                    if (cons.in_asm or prod.in_asm) and cons.mnem.startswith(("v_", "ds_", "buffer_", "global_")):
+                        if accumulate_chain(prod, cons):
+                            stopped = True  # the chain's next step redefines the registers
+                            break
                         if (vregs(cons.ops) & dv) or (aregs(cons.ops) & da):
                             findings.append((prod, cons, need, waits))
                             stopped = True
