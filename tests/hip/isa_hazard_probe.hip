@@ -77,6 +77,24 @@ __global__ void probe_xdl_asm_read_padded(const f16x8* a, float* out, int flag) 
     out[threadIdx.x] = t;
 }
 
+// asm XDL MFMA result -> hipcc's read of it (the third audit's other half,
+// round 6): an asm accumulate chain into VGPRs (fattn_pf4.h's lean S^T
+// chains) whose result hipcc's code reads at once -- hipcc pads only its own
+// MFMAs -- and the same chain ending in the 12 states of a 32x32x16 MFMA (the
+// chain's second step takes the first's result whole as srcC: no wait)
+__global__ void probe_xdl_vgpr_read(const f16x8* a, float* out) {
+    pf32x16 acc;
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a[threadIdx.x]), "v"(a[threadIdx.x + 64]));
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a[threadIdx.x + 128]), "v"(a[threadIdx.x + 192]));
+    out[threadIdx.x] = acc[0] * 3.0f;
+}
+__global__ void probe_xdl_vgpr_read_padded(const f16x8* a, float* out) {
+    pf32x16 acc;
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a[threadIdx.x]), "v"(a[threadIdx.x + 64]));
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0\n\ts_nop 11" : "+v"(acc) : "v"(a[threadIdx.x + 128]), "v"(a[threadIdx.x + 192]));
+    out[threadIdx.x] = acc[0] * 3.0f;
+}
+
 // VALU SGPR write -> asm VMEM read of it (the checker's fourth audit, round
 // 6): a descriptor word fresh from v_readfirstlane read by an asm LDS-DMA
 // opened with s_nop 0 only (the LDS-DMA helper's first "{m0}" form), and the

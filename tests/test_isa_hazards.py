@@ -68,13 +68,14 @@ def test_audit_catches_injected_early_touch(tmp_path, capsys):
         findings, loads, rets = ihc.check_function(name, body)
         key = next(k for k in ("probe_clean", "probe_early_store", "probe_early_copy", "probe_trans_asm_use",
                                "probe_trans_asm_padded", "probe_xdl_asm_read_padded", "probe_xdl_asm_read",
+                               "probe_xdl_vgpr_read_padded", "probe_xdl_vgpr_read",
                                "probe_sgpr_vmem_padded", "probe_sgpr_vmem")
                    if k in name)
         by[key] = (findings, loads, rets, ihc.check_wait_states(name, body) + ihc.check_xdl_asm_reads(name, body) +
                    ihc.check_sgpr_vmem(name, body))
     assert set(by) == {"probe_clean", "probe_early_store", "probe_early_copy", "probe_trans_asm_use",
                        "probe_trans_asm_padded", "probe_xdl_asm_read", "probe_xdl_asm_read_padded",
-                       "probe_sgpr_vmem", "probe_sgpr_vmem_padded"}
+                       "probe_xdl_vgpr_read", "probe_xdl_vgpr_read_padded", "probe_sgpr_vmem", "probe_sgpr_vmem_padded"}
     # the fourth audit: a descriptor word fresh from v_readfirstlane read by an
     # asm LDS-DMA after s_nop 0 is flagged; behind the helper's s_nop 4 it is not
     sw = by["probe_sgpr_vmem"][3]
@@ -85,6 +86,12 @@ def test_audit_catches_injected_early_touch(tmp_path, capsys):
     xw = by["probe_xdl_asm_read"][3]
     assert xw and xw[0][0].mnem.startswith("v_mfma") and xw[0][1].mnem.startswith("v_accvgpr_read"), xw
     assert by["probe_xdl_asm_read_padded"][3] == []
+    # ... and hipcc's read right behind an asm MFMA chain into VGPRs is flagged
+    # (once: the chain's own second step is not), not behind the chain's pad
+    vw = by["probe_xdl_vgpr_read"][3]
+    assert len(vw) == 1 and vw[0][0].in_asm and vw[0][0].ops.endswith(vw[0][0].ops.split(",")[0].strip()), vw
+    assert not vw[0][1].in_asm and vw[0][1].mnem.startswith("v_"), vw
+    assert by["probe_xdl_vgpr_read_padded"][3] == []
     ws = by["probe_trans_asm_use"][3]
     assert ws and ws[0][0].mnem.startswith("v_exp") and ws[0][1].mnem.startswith("v_add"), ws
     assert by["probe_trans_asm_padded"][3] == []
