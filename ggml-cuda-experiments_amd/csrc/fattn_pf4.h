@@ -654,7 +654,9 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                 const int t = pc >> 3, k = 2 * (pc & 7);
                 mX[pc][0] = st[t][k];
                 mX[pc][1] = st[t][k + 1];
-                asm volatile("" : "+v"(mX[pc][0]), "+v"(mX[pc][1]));
+                // (an accumulator read staged a step ahead; with the chains in VGPRs
+                // (lean kernels) there is nothing to stage, and the pin made copies)
+                if constexpr (!(LEAN && FATTN_PF4_SVGPR)) asm volatile("" : "+v"(mX[pc][0]), "+v"(mX[pc][1]));
             };
             // (SCHED 4 without mask values: the accumulator times c IS the argument)
             auto m1u = [&](const f32x16 (&st)[2], float (&us)[2][16], float nr, int pc) {
@@ -1010,6 +1012,9 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                             else mfma_s_next(s1[t], kr[t][kk], qop[1][kk]);
                         } else if constexpr (LN) {
                             s1[t] = mfma32(kr[t][kk], qop[1][kk], kk == 0 ? ci[1] : s1[t]);
+                        } else if constexpr (LEAN && FATTN_PF4_SVGPR) {
+                            if (kk == 0) mfma_s_first(s1[t], kr[t][kk], qop[1][kk]);
+                            else mfma_s_next(s1[t], kr[t][kk], qop[1][kk]);
                         } else {
                             if (kk == 0) s1[t] = f32x16{};
                             s1[t] = mfma32(kr[t][kk], qop[1][kk], s1[t]);
@@ -1020,6 +1025,9 @@ __global__ __launch_bounds__(kPf4Waves* kWave, 1) void fattn_pf4_kernel(const Sp
                             else mfma_s_next(s0[t], kr[t][kk], qop[0][kk]);
                         } else if constexpr (LN) {
                             s0[t] = mfma32(kr[t][kk], qop[0][kk], kk == 0 ? ci[0] : s0[t]);
+                        } else if constexpr (LEAN && FATTN_PF4_SVGPR) {
+                            if (kk == 0) mfma_s_first(s0[t], kr[t][kk], qop[0][kk]);
+                            else mfma_s_next(s0[t], kr[t][kk], qop[0][kk]);
                         } else {
                             if (kk == 0) s0[t] = f32x16{};
                             s0[t] = mfma32(kr[t][kk], qop[0][kk], s0[t]);

@@ -225,4 +225,19 @@ pass_y() {
     done
   done
 }
+# Twenty-sixth pass: the masked prefill body's S^T chains in VGPRs too (its
+# accumulator reads gone) -- prefill parity, then stamps (libfattn_stnew.so /
+# libfattn_stold.so, the tree before) and processes alternating libfattn.so /
+# libfattn_prev.so on the random mask.
+pass_z() {
+  run t_z 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_extra.py -q --timeout 300 --timeout-method thread -m gpu -k "pf or prefill"
+  for L in libfattn_stnew.so libfattn_stold.so; do
+    FATTN_LIB=$L run st_z_r_${L%.so} 200 python -u tools/pf_stamps.py --kv-type q8_0
+  done
+  for r in 1 2 3; do
+    for L in libfattn.so libfattn_prev.so; do
+      FATTN_LIB=$L run ab_z_r_${L%.so}_$r 200 python -u tools/ab_prefill.py --kv q8_0 --mask random --rounds 2 --variant $L:
+    done
+  done
+}
 "$@"
